@@ -1,0 +1,321 @@
+/*
+ * dht_oracle.cpp -- CPU restatement of OpenDHT's XOR-closest-node path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see dht_oracle.h).  Never linked into libdhtgpu.
+ *
+ * Every function cites the reference file:line it restates.  Reference paths are
+ * relative to the OpenDHT source tree (Dale-M/opendht @ v0).
+ */
+#include "dht_oracle.h"
+
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <iterator>
+#include <list>
+#include <stdexcept>
+#include <thread>
+#include <vector>
+
+namespace {
+
+constexpr unsigned HASH_LEN = 20;          /* include/opendht/infohash.h:267 */
+constexpr unsigned TARGET_NODES = 8;       /* include/opendht/routing_table.h:26 */
+using Id = std::array<uint8_t, HASH_LEN>;
+
+inline Id load(const uint8_t* p) { Id r; std::memcpy(r.data(), p, HASH_LEN); return r; }
+
+/* Hash<N>::xorCmp, include/opendht/infohash.h:179-194: at the first byte where id1
+ * and id2 differ, compare id1^self with id2^self. */
+inline int xor_cmp(const uint8_t* self, const uint8_t* a, const uint8_t* b) {
+    for (unsigned i = 0; i < HASH_LEN; i++) {
+        if (a[i] == b[i]) continue;
+        uint8_t x1 = a[i] ^ self[i], x2 = b[i] ^ self[i];
+        return x1 < x2 ? -1 : 1;
+    }
+    return 0;
+}
+
+/* Hash<N>::commonBits, include/opendht/infohash.h:154-176. */
+inline unsigned common_bits(const uint8_t* a, const uint8_t* b) {
+    unsigned i = 0;
+    for (; i < HASH_LEN; i++)
+        if (a[i] != b[i]) break;
+    if (i == HASH_LEN) return 8 * HASH_LEN;
+    uint8_t x = a[i] ^ b[i];
+    unsigned j = 0;
+    while ((x & 0x80) == 0) { x <<= 1; j++; }
+    return 8 * i + j;
+}
+
+/* Hash<N>::lowbit, include/opendht/infohash.h:132-143. */
+inline int lowbit(const uint8_t* a) {
+    int i, j;
+    for (i = HASH_LEN - 1; i >= 0; i--)
+        if (a[i] != 0) break;
+    if (i < 0) return -1;
+    for (j = 7; j >= 0; j--)
+        if ((a[i] & (0x80 >> j)) != 0) break;
+    return 8 * i + j;
+}
+
+/* Hash<N>::cmp, include/opendht/infohash.h:149-151 (memcmp). */
+inline int cmp(const uint8_t* a, const uint8_t* b) { return std::memcmp(a, b, HASH_LEN); }
+
+/* Hash<N>::setBit, include/opendht/infohash.h:205-210. */
+inline void set_bit(Id& id, unsigned nbit, bool b) {
+    uint8_t& num = id[nbit / 8];
+    unsigned bit = 7 - (nbit % 8);
+    num ^= (-(int)b ^ num) & (1 << bit);
+}
+
+inline uint64_t splitmix(uint64_t seed, uint64_t j) {
+    uint64_t z = seed + (j + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+inline void put_be64(uint8_t* p, uint64_t v, unsigned nbytes) {
+    for (unsigned i = 0; i < nbytes; i++) p[i] = (uint8_t)(v >> (56 - 8 * i));
+}
+
+template <class F>
+void parallel_for(uint64_t n, int threads, F f) {
+    if (threads <= 1 || n < 2) { for (uint64_t i = 0; i < n; i++) f(i); return; }
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++)
+        th.emplace_back([&, t] { for (uint64_t i = t; i < n; i += threads) f(i); });
+    for (auto& x : th) x.join();
+}
+
+/* ---- RoutingTable restatement (src/routing_table.cpp, include/opendht/routing_table.h) ---- */
+struct Bucket {
+    Id first {};
+    std::list<uint32_t> nodes;   /* node handles, list order as in Bucket::nodes (routing_table.h:38) */
+};
+
+} // namespace
+
+struct orc_table {
+    Id myid {};
+    bool is_client {false};
+    std::list<Bucket> buckets;
+    std::vector<Id> ids;          /* node handle -> id */
+
+    using It = std::list<Bucket>::iterator;
+
+    /* RoutingTable::findBucket, src/routing_table.cpp:153-166 */
+    It find_bucket(const Id& id) {
+        if (buckets.empty()) return buckets.end();
+        auto b = buckets.begin();
+        while (true) {
+            auto next = std::next(b);
+            if (next == buckets.end()) return b;
+            if (cmp(id.data(), next->first.data()) < 0) return b;
+            b = next;
+        }
+    }
+    /* RoutingTable::contains, include/opendht/routing_table.h:64-67 */
+    bool contains(It b, const Id& id) {
+        return cmp(b->first.data(), id.data()) <= 0 &&
+               (std::next(b) == buckets.end() || cmp(id.data(), std::next(b)->first.data()) < 0);
+    }
+    /* RoutingTable::depth, src/routing_table.cpp:100-107 */
+    unsigned depth(It b) {
+        if (b == buckets.end()) return 0;
+        int bit1 = lowbit(b->first.data());
+        int bit2 = std::next(b) != buckets.end() ? lowbit(std::next(b)->first.data()) : -1;
+        return std::max(bit1, bit2) + 1;
+    }
+    /* RoutingTable::split (+ middle, src/routing_table.cpp:87-97), :169-200 */
+    bool split(It b) {
+        unsigned bit = depth(b);
+        if (bit >= 8 * HASH_LEN) return false;         /* middle() throws out_of_range */
+        Id new_id = b->first;
+        set_bit(new_id, bit, true);
+        Bucket nb; nb.first = new_id;
+        buckets.insert(std::next(b), nb);
+        std::list<uint32_t> nodes;
+        nodes.splice(nodes.begin(), b->nodes);
+        while (!nodes.empty()) {
+            auto n = nodes.begin();
+            auto bb = find_bucket(ids[*n]);
+            if (bb == buckets.end()) nodes.erase(n);
+            else bb->nodes.splice(bb->nodes.begin(), nodes, n);
+        }
+        return true;
+    }
+    /* RoutingTable::onNewNode, src/routing_table.cpp:204-262, with every node good
+     * (no expired node to replace, no dubious node, sendPing is a no-op). */
+    int on_new_node(const Id& id) {
+        for (int guard = 0; guard < 8 * (int)HASH_LEN + 2; guard++) {
+            auto b = find_bucket(id);
+            if (b == buckets.end()) return 0;
+            for (auto n : b->nodes)
+                if (ids[n] == id) return 0;          /* same node already there */
+            bool mybucket = contains(b, myid);
+            if (b->nodes.size() >= TARGET_NODES) {
+                const bool dubious = false;
+                if ((mybucket || (is_client && depth(b) < 6)) && (!dubious || buckets.size() == 1)) {
+                    if (!split(b)) return 0;
+                    continue;                        /* return onNewNode(node, ...) */
+                }
+                return 0;                            /* cached away */
+            }
+            ids.push_back(id);
+            b->nodes.emplace_front((uint32_t)(ids.size() - 1));
+            return 1;
+        }
+        return 0;
+    }
+};
+
+extern "C" {
+
+void orc_gen_ids(uint64_t seed, uint64_t start, uint64_t n, uint8_t* out20) {
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t g = start + i;
+        uint8_t* p = out20 + 20 * i;
+        put_be64(p, splitmix(seed, 3 * g), 8);
+        put_be64(p + 8, splitmix(seed, 3 * g + 1), 8);
+        put_be64(p + 16, splitmix(seed, 3 * g + 2), 4);
+    }
+}
+
+int orc_xor_cmp(const uint8_t* self, const uint8_t* a, const uint8_t* b) { return xor_cmp(self, a, b); }
+unsigned orc_common_bits(const uint8_t* a, const uint8_t* b) { return common_bits(a, b); }
+int orc_lowbit(const uint8_t* a) { return lowbit(a); }
+int orc_cmp(const uint8_t* a, const uint8_t* b) { int c = cmp(a, b); return (c > 0) - (c < 0); }
+
+/* std::partial_sort(first, first+k, last, [t](a,b){ return t.xorCmp(a,b) < 0; })
+ * over an index array; equal ids tie-break by lower index. */
+void orc_topk(const uint8_t* ids20, uint64_t n, const uint8_t* targets20, uint32_t q,
+              uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, int threads) {
+    parallel_for(q, threads, [&](uint64_t qi) {
+        const uint8_t* t = targets20 + 20 * qi;
+        std::vector<uint32_t> idx(n);
+        for (uint64_t i = 0; i < n; i++) idx[i] = (uint32_t)i;
+        uint64_t kk = std::min<uint64_t>(k, n);
+        std::partial_sort(idx.begin(), idx.begin() + kk, idx.end(), [&](uint32_t a, uint32_t b) {
+            int c = xor_cmp(t, ids20 + 20ull * a, ids20 + 20ull * b);
+            return c < 0 || (c == 0 && a < b);
+        });
+        for (uint32_t i = 0; i < k; i++) out_idx[qi * k + i] = i < kk ? idx[i] : 0xFFFFFFFFu;
+        out_cnt[qi] = (uint32_t)kk;
+    });
+}
+
+orc_table* orc_table_new(const uint8_t* myid20, int is_client) {
+    auto* t = new orc_table;
+    t->myid = load(myid20);
+    t->is_client = is_client != 0;
+    t->buckets.emplace_back();                     /* Dht ctor: one bucket, first = zero hash */
+    return t;
+}
+void orc_table_free(orc_table* t) { delete t; }
+int orc_table_insert(orc_table* t, const uint8_t* id20) { return t->on_new_node(load(id20)); }
+uint32_t orc_table_nbuckets(const orc_table* t) { return (uint32_t)t->buckets.size(); }
+uint32_t orc_table_nnodes(const orc_table* t) {
+    uint32_t c = 0;
+    for (auto& b : t->buckets) c += (uint32_t)b.nodes.size();
+    return c;
+}
+void orc_table_export(const orc_table* t, uint8_t* firsts20, uint32_t* off, uint8_t* ids20) {
+    uint32_t bi = 0, ni = 0;
+    for (auto& b : t->buckets) {
+        std::memcpy(firsts20 + 20 * bi, b.first.data(), 20);
+        off[bi] = ni;
+        for (auto n : b.nodes) { std::memcpy(ids20 + 20ull * ni, t->ids[n].data(), 20); ni++; }
+        bi++;
+    }
+    off[bi] = ni;
+}
+
+/* RoutingTable::findBucket, src/routing_table.cpp:153-166 (linear walk). */
+int orc_find_bucket(uint32_t nb, const uint8_t* firsts20, const uint8_t* id20) {
+    if (nb == 0) return -1;
+    uint32_t b = 0;
+    while (true) {
+        uint32_t next = b + 1;
+        if (next == nb) return (int)b;
+        if (cmp(id20, firsts20 + 20 * next) < 0) return (int)b;
+        b = next;
+    }
+}
+
+unsigned orc_depth(uint32_t nb, const uint8_t* firsts20, uint32_t b) {
+    if (b >= nb) return 0;
+    int bit1 = lowbit(firsts20 + 20 * b);
+    int bit2 = b + 1 < nb ? lowbit(firsts20 + 20 * (b + 1)) : -1;
+    return (unsigned)(std::max(bit1, bit2) + 1);
+}
+
+/* RoutingTable::findClosestNodes, src/routing_table.cpp:110-150. */
+uint32_t orc_find_closest(uint32_t nb, const uint8_t* firsts20, const uint32_t* off,
+                          const uint8_t* ids20, const uint8_t* good, const uint8_t* target20,
+                          uint32_t count, uint32_t* out_idx) {
+    std::vector<uint32_t> nodes;
+    nodes.reserve(count);
+    int bucket = orc_find_bucket(nb, firsts20, target20);
+    if (bucket < 0) return 0;
+    auto sorted_bucket_insert = [&](int b) {
+        for (uint32_t n = off[b]; n < off[b + 1]; n++) {
+            if (!good[n]) continue;
+            auto here = std::find_if(nodes.begin(), nodes.end(), [&](uint32_t node) {
+                return xor_cmp(target20, ids20 + 20ull * n, ids20 + 20ull * node) < 0;
+            });
+            nodes.insert(here, n);
+        }
+    };
+    int itn = bucket;                  /* end() == nb */
+    int itp = bucket - 1;              /* end() == -1 */
+    while (nodes.size() < count && (itn < (int)nb || itp >= 0)) {
+        if (itn < (int)nb) { sorted_bucket_insert(itn); itn++; }
+        if (itp >= 0) { sorted_bucket_insert(itp); itp--; }
+    }
+    if (nodes.size() > count) nodes.resize(count);
+    for (size_t i = 0; i < nodes.size(); i++) out_idx[i] = nodes[i];
+    return (uint32_t)nodes.size();
+}
+
+void orc_classify(uint32_t nb, const uint8_t* firsts20, const uint8_t* myid20,
+                  const uint8_t* ids20, uint64_t n, uint8_t* out_bucket, uint64_t* hist161) {
+    for (unsigned i = 0; i <= 8 * HASH_LEN; i++) hist161[i] = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t* id = ids20 + 20 * i;
+        int b = orc_find_bucket(nb, firsts20, id);
+        out_bucket[i] = (uint8_t)(b < 0 ? 0xFF : b);
+        hist161[common_bits(id, myid20)]++;
+    }
+}
+
+/* NodeCache::getCachedNodes, src/node_cache.cpp:42-74. END plays the role of c.cend(). */
+uint32_t orc_cached_nodes(const uint8_t* sorted_ids20, uint64_t n, const uint8_t* accept,
+                          const uint8_t* target20, uint32_t count, uint32_t* out_idx) {
+    const uint64_t END = n;
+    uint64_t lo = 0, hi = n;                       /* c.lower_bound(id) */
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) / 2;
+        if (cmp(sorted_ids20 + 20 * mid, target20) < 0) lo = mid + 1; else hi = mid;
+    }
+    uint64_t it_p = lo, it_n = lo;
+    auto dec_it = [&](uint64_t& it) {
+        uint64_t ret = it;
+        it = (it == 0) ? END : it - 1;             /* cbegin() -> cend(), else prev() */
+        return ret;
+    };
+    if (n != 0) dec_it(it_p);
+    uint32_t cnt = 0;
+    while (cnt < count && (it_n != END || it_p != END)) {
+        uint64_t it;
+        if (it_p == END) it = it_n++;
+        else if (it_n == END) it = dec_it(it_p);
+        else it = xor_cmp(target20, sorted_ids20 + 20 * it_p, sorted_ids20 + 20 * it_n) < 0
+                      ? dec_it(it_p) : it_n++;
+        if (accept[it]) out_idx[cnt++] = (uint32_t)it;
+    }
+    return cnt;
+}
+
+} // extern "C"

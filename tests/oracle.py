@@ -1,0 +1,187 @@
+"""ctypes wrapper around oracle/liboracle.so -- the CPU restatement used as the
+parity CHECKER.  Test infrastructure only: imported by tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg; never by the opendht_amd product path."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_LIB = os.path.join(ROOT, "oracle", "liboracle.so")
+_lib = None
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = ctypes.CDLL(_LIB)
+        L.orc_gen_ids.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u8p]
+        L.orc_xor_cmp.argtypes = [u8p, u8p, u8p]
+        L.orc_xor_cmp.restype = ctypes.c_int
+        L.orc_common_bits.argtypes = [u8p, u8p]
+        L.orc_common_bits.restype = ctypes.c_uint
+        L.orc_lowbit.argtypes = [u8p]
+        L.orc_lowbit.restype = ctypes.c_int
+        L.orc_cmp.argtypes = [u8p, u8p]
+        L.orc_cmp.restype = ctypes.c_int
+        L.orc_topk.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint32, ctypes.c_uint32,
+                               u32p, u32p, ctypes.c_int]
+        L.orc_table_new.argtypes = [u8p, ctypes.c_int]
+        L.orc_table_new.restype = ctypes.c_void_p
+        L.orc_table_free.argtypes = [ctypes.c_void_p]
+        L.orc_table_insert.argtypes = [ctypes.c_void_p, u8p]
+        L.orc_table_insert.restype = ctypes.c_int
+        L.orc_table_nbuckets.argtypes = [ctypes.c_void_p]
+        L.orc_table_nbuckets.restype = ctypes.c_uint32
+        L.orc_table_nnodes.argtypes = [ctypes.c_void_p]
+        L.orc_table_nnodes.restype = ctypes.c_uint32
+        L.orc_table_export.argtypes = [ctypes.c_void_p, u8p, u32p, u8p]
+        L.orc_find_bucket.argtypes = [ctypes.c_uint32, u8p, u8p]
+        L.orc_find_bucket.restype = ctypes.c_int
+        L.orc_depth.argtypes = [ctypes.c_uint32, u8p, ctypes.c_uint32]
+        L.orc_depth.restype = ctypes.c_uint
+        L.orc_find_closest.argtypes = [ctypes.c_uint32, u8p, u32p, u8p, u8p, u8p, ctypes.c_uint32, u32p]
+        L.orc_find_closest.restype = ctypes.c_uint32
+        L.orc_classify.argtypes = [ctypes.c_uint32, u8p, u8p, u8p, ctypes.c_uint64, u8p, u64p]
+        L.orc_cached_nodes.argtypes = [u8p, ctypes.c_uint64, u8p, u8p, ctypes.c_uint32, u32p]
+        L.orc_cached_nodes.restype = ctypes.c_uint32
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def h(hexstr):
+    return np.frombuffer(bytes.fromhex(hexstr), dtype=np.uint8).copy()
+
+
+def gen_ids(seed, n, start=0):
+    out = np.empty((n, 20), dtype=np.uint8)
+    lib().orc_gen_ids(seed, start, n, _p(out, u8p))
+    return out
+
+
+def xor_cmp(t, a, b):
+    return lib().orc_xor_cmp(_p(t, u8p), _p(a, u8p), _p(b, u8p))
+
+
+def common_bits(a, b):
+    return lib().orc_common_bits(_p(a, u8p), _p(b, u8p))
+
+
+def lowbit(a):
+    return lib().orc_lowbit(_p(a, u8p))
+
+
+def cmp(a, b):
+    return lib().orc_cmp(_p(a, u8p), _p(b, u8p))
+
+
+def topk(ids, targets, k, threads=os.cpu_count() or 1):
+    ids = np.ascontiguousarray(ids, dtype=np.uint8)
+    targets = np.ascontiguousarray(targets, dtype=np.uint8)
+    q = targets.shape[0]
+    out = np.empty((q, k), dtype=np.uint32)
+    cnt = np.empty(q, dtype=np.uint32)
+    lib().orc_topk(_p(ids, u8p), ids.shape[0], _p(targets, u8p), q, k, _p(out, u32p), _p(cnt, u32p),
+                   min(threads, 16))
+    return out, cnt
+
+
+class Table:
+    """A RoutingTable grown with onNewNode (src/routing_table.cpp:204-262)."""
+
+    def __init__(self, myid, is_client=False):
+        self.myid = np.ascontiguousarray(myid, dtype=np.uint8)
+        self._t = lib().orc_table_new(_p(self.myid, u8p), int(is_client))
+
+    def __del__(self):
+        if getattr(self, "_t", None):
+            lib().orc_table_free(self._t)
+            self._t = None
+
+    def insert(self, id20):
+        id20 = np.ascontiguousarray(id20, dtype=np.uint8)
+        return lib().orc_table_insert(self._t, _p(id20, u8p))
+
+    def grow(self, ids):
+        for row in np.ascontiguousarray(ids, dtype=np.uint8):
+            self.insert(row)
+        return self
+
+    def export(self):
+        nb = lib().orc_table_nbuckets(self._t)
+        nn = lib().orc_table_nnodes(self._t)
+        firsts = np.zeros((nb, 20), dtype=np.uint8)
+        off = np.zeros(nb + 1, dtype=np.uint32)
+        ids = np.zeros((max(nn, 1), 20), dtype=np.uint8)
+        lib().orc_table_export(self._t, _p(firsts, u8p), _p(off, u32p), _p(ids, u8p))
+        return firsts, off, ids[:nn]
+
+
+def find_bucket(firsts, id20):
+    firsts = np.ascontiguousarray(firsts, dtype=np.uint8)
+    return lib().orc_find_bucket(firsts.shape[0], _p(firsts, u8p), _p(np.ascontiguousarray(id20), u8p))
+
+
+def depth(firsts, b):
+    firsts = np.ascontiguousarray(firsts, dtype=np.uint8)
+    return lib().orc_depth(firsts.shape[0], _p(firsts, u8p), b)
+
+
+def find_closest(firsts, off, ids, good, target, count):
+    firsts = np.ascontiguousarray(firsts, dtype=np.uint8)
+    ids = np.ascontiguousarray(ids, dtype=np.uint8)
+    good = np.ascontiguousarray(good, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint32)
+    target = np.ascontiguousarray(target, dtype=np.uint8)
+    out = np.empty(max(count, 1), dtype=np.uint32)
+    c = lib().orc_find_closest(firsts.shape[0], _p(firsts, u8p), _p(off, u32p), _p(ids, u8p),
+                               _p(good, u8p), _p(target, u8p), count, _p(out, u32p))
+    return out[:c].copy()
+
+
+def classify(firsts, myid, ids):
+    firsts = np.ascontiguousarray(firsts, dtype=np.uint8)
+    ids = np.ascontiguousarray(ids, dtype=np.uint8)
+    myid = np.ascontiguousarray(myid, dtype=np.uint8)
+    n = ids.shape[0]
+    out = np.empty(max(n, 1), dtype=np.uint8)
+    hist = np.zeros(161, dtype=np.uint64)
+    lib().orc_classify(firsts.shape[0], _p(firsts, u8p), _p(myid, u8p), _p(ids, u8p), n,
+                       _p(out, u8p), _p(hist, u64p))
+    return out[:n].copy(), hist
+
+
+def cached_nodes(sorted_ids, accept, target, count):
+    sorted_ids = np.ascontiguousarray(sorted_ids, dtype=np.uint8)
+    accept = np.ascontiguousarray(accept, dtype=np.uint8)
+    target = np.ascontiguousarray(target, dtype=np.uint8)
+    out = np.empty(max(count, 1), dtype=np.uint32)
+    c = lib().orc_cached_nodes(_p(sorted_ids, u8p), sorted_ids.shape[0], _p(accept, u8p),
+                               _p(target, u8p), count, _p(out, u32p))
+    return out[:c].copy()
+
+
+# ---- independent pure-Python restatement (big integers) used to cross-check the C oracle ----
+def py_dist(t, a):
+    return int.from_bytes(bytes(t), "big") ^ int.from_bytes(bytes(a), "big")
+
+
+def py_topk(ids, target, k):
+    d = [(py_dist(target, row), i) for i, row in enumerate(ids)]
+    d.sort()
+    return [i for _, i in d[:k]]
