@@ -1,0 +1,135 @@
+/*
+ * dhtgpu.h -- C ABI of libdhtgpu, the MI355X (gfx950) engine for OpenDHT's
+ * XOR-closest-node lookup.
+ *
+ * Plain C: pointers and sizes only, integer status codes, no exceptions and no
+ * callbacks cross this boundary.  Node IDs cross it as 20-byte big-endian
+ * arrays, byte-for-byte dht::InfoHash::data() (include/opendht/infohash.h:263,
+ * HASH_LEN = 20 at :267).  Results are INDICES into the ID array the caller
+ * uploaded last; the caller maps them back to its Sp<Node>.
+ *
+ * Reference interfaces replaced (paths relative to the OpenDHT tree):
+ *   dhtgpu_topk            std::partial_sort(ids, k, InfoHash::xorCmp)          (SURVEY §8 a12,
+ *                          include/opendht/infohash.h:179-194) -- the flat exact k-NN
+ *                          behind findClosestNodesBatch(targets[], k)
+ *   dhtgpu_find_closest    RoutingTable::findClosestNodes(id, now, count)
+ *                          (include/opendht/routing_table.h:56, src/routing_table.cpp:110-150)
+ *   dhtgpu_cached_nodes    NodeCache::getCachedNodes(id, af, count)
+ *                          (include/opendht/node_cache.h:31, src/node_cache.cpp:42-74)
+ *   dhtgpu_classify        RoutingTable::findBucket (src/routing_table.cpp:153-166) +
+ *                          InfoHash::commonBits (include/opendht/infohash.h:154-176)
+ *
+ * Threading (mirrors the reference, src/dhtrunner.cpp:115-150): one context per
+ * thread, or external locking; every host-pointer call is synchronous.
+ * The *_dev entry points take device pointers and a hipStream_t (void*), are
+ * stream-ordered and do not synchronise (for batch/bench/multi-GPU use).
+ */
+#ifndef DHTGPU_H
+#define DHTGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DHTGPU_HASH_LEN 20u
+#define DHTGPU_WORDS 5u              /* a 160-bit id = 5 big-endian u32 words */
+#define DHTGPU_MAX_K 32u             /* largest k / count served */
+#define DHTGPU_NONE 0xFFFFFFFFu      /* index padding for short results */
+
+enum {
+    DHTGPU_OK = 0,
+    DHTGPU_EINVAL = -1,              /* bad argument (null pointer, k == 0 or > DHTGPU_MAX_K, ...) */
+    DHTGPU_ENOMEM = -2,              /* device allocation failed */
+    DHTGPU_EDEVICE = -3,             /* HIP runtime / kernel launch error */
+    DHTGPU_ENOIDS = -4,              /* no id set uploaded */
+    DHTGPU_EUNSORTED = -5,           /* cached_nodes needs a lexicographically sorted, unique id set */
+    DHTGPU_ERANGE = -6               /* size out of range (e.g. more than 2^32-1 ids) */
+};
+
+typedef struct dhtgpu_ctx dhtgpu_ctx;
+
+/* ---- context ---------------------------------------------------------------- */
+int dhtgpu_ctx_create(int device, dhtgpu_ctx** out);
+void dhtgpu_ctx_destroy(dhtgpu_ctx* ctx);
+const char* dhtgpu_strerror(int code);
+int dhtgpu_device_count(int* out);
+/* Device stream used by the synchronous calls (hipStream_t as void*). */
+void* dhtgpu_ctx_stream(dhtgpu_ctx* ctx);
+
+/* ---- the id set (the device mirror of the routing table / node cache) --------- */
+/* Upload n ids (20-byte big-endian each).  The device keeps them as five u32
+ * word planes (struct of arrays).  Also records whether the set is sorted and
+ * unique (needed by dhtgpu_cached_nodes). */
+int dhtgpu_set_ids(dhtgpu_ctx* ctx, const uint8_t* ids20_be, uint64_t n);
+/* Generate n synthetic ids directly in HBM: splitmix64 stream,
+ * id i = BE(x(3g)) || BE(x(3g+1)) || top4(BE(x(3g+2))), g = start + i. */
+int dhtgpu_gen_ids(dhtgpu_ctx* ctx, uint64_t seed, uint64_t start, uint64_t n);
+uint64_t dhtgpu_num_ids(const dhtgpu_ctx* ctx);
+/* Read back ids [first, first+n) as 20-byte big-endian. */
+int dhtgpu_get_ids(dhtgpu_ctx* ctx, uint64_t first, uint64_t n, uint8_t* out20_be);
+/* Device view of the planes: word j of id i is planes[j*stride + i]. */
+int dhtgpu_ids_dev(dhtgpu_ctx* ctx, const uint32_t** planes, uint64_t* stride);
+
+/* ---- K1: flat exact top-k (std::partial_sort over xorCmp) ------------------- */
+/* For each of q targets, the k ids closest by XOR distance, ascending; equal ids
+ * (not produced by OpenDHT) tie-break by lower index.  out_idx[q*k] (DHTGPU_NONE
+ * padded), out_cnt[q] = min(k, n).  1 <= k <= DHTGPU_MAX_K. */
+int dhtgpu_topk(dhtgpu_ctx* ctx, const uint8_t* targets20_be, uint32_t q, uint32_t k,
+                uint32_t* out_idx, uint32_t* out_cnt);
+
+/* Device form.  Targets as word planes (t_planes[j*t_stride + i]).  Writes either
+ * the final indices (out_idx/out_cnt, offset by idx_base) or, if out_rec != NULL,
+ * candidate records out_rec[(qi*k + r)*6 + {w0..w4, idx}] for a cross-shard merge
+ * (idx offset by idx_base, DHTGPU_NONE for empty slots). */
+int dhtgpu_topk_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
+                    uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec,
+                    uint32_t idx_base, void* stream);
+
+/* K3: merge `lists` candidate-record lists per target (rec[((l*q)+qi)*k_in + r]*6,
+ * as written by dhtgpu_topk_dev) into the final top-k.  Used after the RCCL
+ * all-gather of per-GPU shards. */
+int dhtgpu_merge_dev(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_t k_in,
+                     const uint32_t* t_planes, uint64_t t_stride, uint32_t k,
+                     uint32_t* out_idx, uint32_t* out_cnt, void* stream);
+
+/* Convert 20-byte big-endian ids (device) into word planes (device). */
+int dhtgpu_pack_dev(const uint8_t* ids20_be, uint64_t n, uint32_t* planes, uint64_t stride,
+                    void* stream);
+/* Generate synthetic ids (same stream as dhtgpu_gen_ids) into device planes. */
+int dhtgpu_gen_dev(uint64_t seed, uint64_t start, uint64_t n, uint32_t* planes, uint64_t stride,
+                   void* stream);
+
+/* ---- K1r: RoutingTable::findClosestNodes over a table snapshot ------------------ */
+/* Snapshot: nb buckets in list order with firsts20[nb*20] (Bucket::first),
+ * bucket_off[nb+1] (bucket b owns nodes [off[b], off[b+1]) of node_ids20), and
+ * good[nn] = Node::isGood(now) (src/node.cpp:42-47).  For each target: the
+ * min(count, C) XOR-closest good nodes of the contiguous bucket range visited by
+ * the reference's outward walk, ascending.  out_idx[q*count] indexes node_ids20. */
+int dhtgpu_find_closest(dhtgpu_ctx* ctx, uint32_t nb, const uint8_t* firsts20,
+                        const uint32_t* bucket_off, const uint8_t* node_ids20,
+                        const uint8_t* good, const uint8_t* targets20_be, uint32_t q,
+                        uint32_t count, uint32_t* out_idx, uint32_t* out_cnt);
+
+/* ---- K2: routing-bucket classification over the context's id set -------------- */
+/* out_bucket[n] (nullable) = findBucket(id) index; hist161[161] = histogram of
+ * commonBits(id, myid).  nb in [1, 256], firsts sorted ascending (as in the table). */
+int dhtgpu_classify(dhtgpu_ctx* ctx, uint32_t nb, const uint8_t* firsts20,
+                    const uint8_t* myid20, uint8_t* out_bucket, uint64_t* hist161);
+int dhtgpu_classify_dev(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t nb,
+                        const uint32_t* d_first_planes /* 5*nb, word-major */,
+                        const uint32_t* myid_words /* host, 5 words */, uint8_t* out_bucket,
+                        unsigned long long* d_hist161, void* stream);
+
+/* ---- a8: NodeCache::getCachedNodes walk over the context's (sorted) id set ------- */
+/* accept[n] (nullable = all) = lock() && !isExpired() && !isClient().  Output in
+ * the reference's walk order (not sorted), indices into the id set. */
+int dhtgpu_cached_nodes(dhtgpu_ctx* ctx, const uint8_t* accept, const uint8_t* targets20_be,
+                        uint32_t q, uint32_t count, uint32_t* out_idx, uint32_t* out_cnt);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DHTGPU_H */

@@ -1,0 +1,232 @@
+"""opendht_amd -- Python host binding for libdhtgpu, the MI355X engine behind
+OpenDHT's XOR-closest-node lookup.
+
+This is a thin ctypes layer over the C ABI declared in include/dhtgpu.h; every
+compute call runs the hand-written HIP kernels in opendht_amd/libdhtgpu.so.  There is
+no CPU fallback: if the native library is missing or cannot be loaded, import of the
+compute API raises.
+
+Reference interfaces mirrored (OpenDHT tree paths):
+  Context.topk            std::partial_sort(.., InfoHash::xorCmp)  (include/opendht/infohash.h:179-194)
+  Context.find_closest    RoutingTable::findClosestNodes            (src/routing_table.cpp:110-150)
+  Context.cached_nodes    NodeCache::getCachedNodes                 (src/node_cache.cpp:42-74)
+  Context.classify        RoutingTable::findBucket + InfoHash::commonBits
+"""
+import ctypes
+import os
+
+import numpy as np
+
+__all__ = ["Context", "DhtGpuError", "NONE", "MAX_K", "lib", "LIB_PATH", "id_words"]
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdhtgpu.so")
+NONE = 0xFFFFFFFF
+MAX_K = 32
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_vp = ctypes.c_void_p
+_lib = None
+
+
+class DhtGpuError(RuntimeError):
+    def __init__(self, code, what=""):
+        msg = _lib.dhtgpu_strerror(code).decode() if _lib is not None else str(code)
+        super().__init__(f"libdhtgpu: {what}: {msg} ({code})")
+        self.code = code
+
+
+def _check(code, what):
+    if code != 0:
+        raise DhtGpuError(code, what)
+
+
+def lib():
+    """Load libdhtgpu.so (raises if absent: there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libdhtgpu.so not built at {LIB_PATH}: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    try:  # share the HIP runtime with torch when both live in the process
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "dhtgpu_strerror": ([ctypes.c_int], ctypes.c_char_p),
+        "dhtgpu_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+        "dhtgpu_ctx_create": ([ctypes.c_int, ctypes.POINTER(_vp)], ctypes.c_int),
+        "dhtgpu_ctx_destroy": ([_vp], None),
+        "dhtgpu_ctx_stream": ([_vp], _vp),
+        "dhtgpu_set_ids": ([_vp, _u8p, ctypes.c_uint64], ctypes.c_int),
+        "dhtgpu_gen_ids": ([_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64], ctypes.c_int),
+        "dhtgpu_num_ids": ([_vp], ctypes.c_uint64),
+        "dhtgpu_get_ids": ([_vp, ctypes.c_uint64, ctypes.c_uint64, _u8p], ctypes.c_int),
+        "dhtgpu_ids_dev": ([_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+        "dhtgpu_topk": ([_vp, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p], ctypes.c_int),
+        "dhtgpu_topk_dev": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp,
+                             ctypes.c_uint32, _vp], ctypes.c_int),
+        "dhtgpu_merge_dev": ([_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _vp, ctypes.c_uint64,
+                              ctypes.c_uint32, _vp, _vp, _vp], ctypes.c_int),
+        "dhtgpu_pack_dev": ([_vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp], ctypes.c_int),
+        "dhtgpu_gen_dev": ([ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp],
+                           ctypes.c_int),
+        "dhtgpu_find_closest": ([_vp, ctypes.c_uint32, _u8p, _u32p, _u8p, _u8p, _u8p, ctypes.c_uint32,
+                                 ctypes.c_uint32, _u32p, _u32p], ctypes.c_int),
+        "dhtgpu_classify": ([_vp, ctypes.c_uint32, _u8p, _u8p, _u8p, _u64p], ctypes.c_int),
+        "dhtgpu_classify_dev": ([_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, _vp, _u32p, _vp, _vp,
+                                 _vp], ctypes.c_int),
+        "dhtgpu_cached_nodes": ([_vp, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p],
+                                ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def exported_symbols():
+    """Names of every entry point declared in include/dhtgpu.h (for the ABI test)."""
+    return ["dhtgpu_strerror", "dhtgpu_device_count", "dhtgpu_ctx_create", "dhtgpu_ctx_destroy",
+            "dhtgpu_ctx_stream", "dhtgpu_set_ids", "dhtgpu_gen_ids", "dhtgpu_num_ids", "dhtgpu_get_ids",
+            "dhtgpu_ids_dev", "dhtgpu_topk", "dhtgpu_topk_dev", "dhtgpu_merge_dev", "dhtgpu_pack_dev",
+            "dhtgpu_gen_dev", "dhtgpu_find_closest", "dhtgpu_classify", "dhtgpu_classify_dev",
+            "dhtgpu_cached_nodes"]
+
+
+def _ids(a, name="ids"):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    if a.ndim == 1:
+        a = a.reshape(-1, 20)
+    if a.ndim != 2 or a.shape[1] != 20:
+        raise ValueError(f"{name}: expected (n, 20) uint8 big-endian InfoHash bytes, got {a.shape}")
+    return a
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def id_words(ids):
+    """(n,20) big-endian bytes -> (5, n) uint32 word planes (the device layout)."""
+    ids = _ids(ids)
+    return ids.view(">u4").reshape(-1, 5).astype(np.uint32).T.copy()
+
+
+class Context:
+    """One device context (mirrors the reference's single dht_thread ownership:
+    not thread-safe, calls are synchronous)."""
+
+    def __init__(self, device=0):
+        L = lib()
+        h = _vp()
+        _check(L.dhtgpu_ctx_create(int(device), ctypes.byref(h)), "ctx_create")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().dhtgpu_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def stream(self):
+        return lib().dhtgpu_ctx_stream(self._h)
+
+    # ---- id set -------------------------------------------------------------
+    def set_ids(self, ids):
+        ids = _ids(ids)
+        _check(lib().dhtgpu_set_ids(self._h, _p(ids, _u8p), ids.shape[0]), "set_ids")
+
+    def gen_ids(self, seed, n, start=0):
+        _check(lib().dhtgpu_gen_ids(self._h, seed, start, n), "gen_ids")
+
+    @property
+    def num_ids(self):
+        return int(lib().dhtgpu_num_ids(self._h))
+
+    def get_ids(self, first=0, n=None):
+        if n is None:
+            n = self.num_ids - first
+        out = np.empty((n, 20), dtype=np.uint8)
+        _check(lib().dhtgpu_get_ids(self._h, first, n, _p(out, _u8p)), "get_ids")
+        return out
+
+    def ids_dev(self):
+        p, s = _vp(), ctypes.c_uint64()
+        _check(lib().dhtgpu_ids_dev(self._h, ctypes.byref(p), ctypes.byref(s)), "ids_dev")
+        return p.value, s.value
+
+    # ---- K1: flat exact top-k ---------------------------------------------------
+    def topk(self, targets, k=8):
+        """findClosestNodesBatch(targets[], k): (q,k) uint32 indices (NONE padded), (q,) counts."""
+        t = _ids(targets, "targets")
+        q = t.shape[0]
+        out = np.empty((q, k), dtype=np.uint32)
+        cnt = np.empty(q, dtype=np.uint32)
+        _check(lib().dhtgpu_topk(self._h, _p(t, _u8p), q, k, _p(out, _u32p), _p(cnt, _u32p)), "topk")
+        return out, cnt
+
+    def topk_dev(self, t_planes_ptr, t_stride, q, k, out_idx_ptr=None, out_cnt_ptr=None, out_rec_ptr=None,
+                 idx_base=0, stream=None):
+        _check(lib().dhtgpu_topk_dev(self._h, t_planes_ptr, t_stride, q, k, out_idx_ptr, out_cnt_ptr,
+                                     out_rec_ptr, idx_base, stream), "topk_dev")
+
+    # ---- K1r: RoutingTable::findClosestNodes -------------------------------------
+    def find_closest(self, firsts, bucket_off, node_ids, good, targets, count=8):
+        firsts = _ids(firsts, "firsts") if len(firsts) else np.zeros((0, 20), np.uint8)
+        off = np.ascontiguousarray(bucket_off, dtype=np.uint32)
+        nodes = _ids(node_ids, "node_ids") if len(node_ids) else np.zeros((1, 20), np.uint8)
+        good = np.ascontiguousarray(good, dtype=np.uint8) if len(good) else np.zeros(1, np.uint8)
+        t = _ids(targets, "targets")
+        q = t.shape[0]
+        out = np.empty((q, count), dtype=np.uint32)
+        cnt = np.empty(q, dtype=np.uint32)
+        _check(lib().dhtgpu_find_closest(self._h, firsts.shape[0], _p(firsts, _u8p), _p(off, _u32p),
+                                         _p(nodes, _u8p), _p(good, _u8p), _p(t, _u8p), q, count,
+                                         _p(out, _u32p), _p(cnt, _u32p)), "find_closest")
+        return out, cnt
+
+    # ---- K2: classification -------------------------------------------------------
+    def classify(self, firsts, myid, buckets=True):
+        firsts = _ids(firsts, "firsts")
+        myid = np.ascontiguousarray(myid, dtype=np.uint8).reshape(20)
+        hist = np.zeros(161, dtype=np.uint64)
+        out = np.empty(max(self.num_ids, 1), dtype=np.uint8) if buckets else None
+        _check(lib().dhtgpu_classify(self._h, firsts.shape[0], _p(firsts, _u8p), _p(myid, _u8p),
+                                     _p(out, _u8p) if buckets else None, _p(hist, _u64p)), "classify")
+        return (out[: self.num_ids] if buckets else None), hist
+
+    # ---- a8: NodeCache::getCachedNodes ------------------------------------------------
+    def cached_nodes(self, targets, count=14, accept=None):
+        t = _ids(targets, "targets")
+        q = t.shape[0]
+        out = np.empty((q, count), dtype=np.uint32)
+        cnt = np.empty(q, dtype=np.uint32)
+        acc = None
+        if accept is not None:
+            acc = np.ascontiguousarray(accept, dtype=np.uint8)
+            if acc.shape[0] != self.num_ids:
+                raise ValueError("accept mask must have one byte per id")
+        _check(lib().dhtgpu_cached_nodes(self._h, _p(acc, _u8p) if acc is not None else None, _p(t, _u8p), q,
+                                         count, _p(out, _u32p), _p(cnt, _u32p)), "cached_nodes")
+        return out, cnt
+
+
+def device_count():
+    n = ctypes.c_int()
+    _check(lib().dhtgpu_device_count(ctypes.byref(n)), "device_count")
+    return n.value

@@ -1,0 +1,416 @@
+// api.hip -- the libdhtgpu C ABI (include/dhtgpu.h).  Owns device buffers and the
+// stream; converts between the boundary's 20-byte big-endian ids and the device
+// word-plane layout; never throws across the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/dhtgpu.h"
+#include "dhtgpu_internal.h"
+
+using namespace dhtgpu;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+        if (e == hipSuccess) cap = bytes;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+int map_err(hipError_t e) {
+    if (e == hipSuccess) return DHTGPU_OK;
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return DHTGPU_ENOMEM;
+    return DHTGPU_EDEVICE;
+}
+
+#define DHT_TRY(expr)                                 \
+    do {                                              \
+        hipError_t _e = (expr);                       \
+        if (_e != hipSuccess) return map_err(_e);     \
+    } while (0)
+
+uint32_t pad_q(uint32_t q) { return (q + 63) & ~63u; }
+
+}  // namespace
+
+struct dhtgpu_ctx {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;
+    DevBuf planes;          // 5 * stride u32
+    uint64_t n = 0, stride = 0;
+    bool sorted = false;
+    DevBuf staging;         // host<->device byte staging
+    DevBuf targets;         // 5 * tstride u32
+    DevBuf out_idx, out_cnt, rec, aux, aux2, aux3;
+    bool has_ids = false;
+
+    hipError_t bind() { return hipSetDevice(device); }
+
+    // upload q targets (20-byte big-endian, host) into target planes; returns stride
+    hipError_t upload_targets(const uint8_t* t20, uint32_t q, uint64_t* ts) {
+        const uint64_t s = pad_q(q);
+        hipError_t e = staging.ensure((size_t)q * 20);
+        if (e != hipSuccess) return e;
+        if ((e = targets.ensure((size_t)s * 5 * 4)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(staging.p, t20, (size_t)q * 20, hipMemcpyHostToDevice, stream)) != hipSuccess) return e;
+        if ((e = launch_pack(staging.as<uint8_t>(), q, targets.as<uint32_t>(), s, stream)) != hipSuccess) return e;
+        *ts = s;
+        return hipSuccess;
+    }
+};
+
+extern "C" {
+
+const char* dhtgpu_strerror(int code) {
+    switch (code) {
+        case DHTGPU_OK: return "ok";
+        case DHTGPU_EINVAL: return "invalid argument";
+        case DHTGPU_ENOMEM: return "device out of memory";
+        case DHTGPU_EDEVICE: return "HIP device or kernel error";
+        case DHTGPU_ENOIDS: return "no id set uploaded";
+        case DHTGPU_EUNSORTED: return "id set is not lexicographically sorted and unique";
+        case DHTGPU_ERANGE: return "size out of range";
+        default: return "unknown error";
+    }
+}
+
+int dhtgpu_device_count(int* out) {
+    if (!out) return DHTGPU_EINVAL;
+    *out = 0;
+    DHT_TRY(hipGetDeviceCount(out));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_ctx_create(int device, dhtgpu_ctx** out) {
+    if (!out) return DHTGPU_EINVAL;
+    *out = nullptr;
+    int nd = 0;
+    DHT_TRY(hipGetDeviceCount(&nd));
+    if (device < 0 || device >= nd) return DHTGPU_EINVAL;
+    auto* c = new (std::nothrow) dhtgpu_ctx;
+    if (!c) return DHTGPU_ENOMEM;
+    c->device = device;
+    hipError_t e = c->bind();
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+    }
+    if (e != hipSuccess) {
+        delete c;
+        return map_err(e);
+    }
+    *out = c;
+    return DHTGPU_OK;
+}
+
+void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
+    if (!c) return;
+    (void)c->bind();
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (DevBuf* b : {&c->planes, &c->staging, &c->targets, &c->out_idx, &c->out_cnt, &c->rec,
+                      &c->aux, &c->aux2, &c->aux3})
+        b->release();
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+void* dhtgpu_ctx_stream(dhtgpu_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+uint64_t dhtgpu_num_ids(const dhtgpu_ctx* c) { return c && c->has_ids ? c->n : 0; }
+
+static int finish_ids(dhtgpu_ctx* c, uint64_t n) {
+    // zero the padding so tile streaming reads deterministic words
+    const uint64_t s = c->stride;
+    for (int w = 0; w < 5; ++w)
+        DHT_TRY(launch_fill(c->planes.as<uint32_t>() + (uint64_t)w * s + n, s - n, 0u, c->stream));
+    DHT_TRY(c->aux.ensure(16));
+    DHT_TRY(hipMemsetAsync(c->aux.p, 0, 4, c->stream));
+    DHT_TRY(launch_check_sorted(c->planes.as<uint32_t>(), s, n, c->aux.as<uint32_t>(), c->stream));
+    uint32_t flag = 0;
+    DHT_TRY(hipMemcpyAsync(&flag, c->aux.p, 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    c->n = n;
+    c->sorted = flag == 0;
+    c->has_ids = true;
+    return DHTGPU_OK;
+}
+
+static int alloc_ids(dhtgpu_ctx* c, uint64_t n) {
+    if (n >= 0xFFFFFFFFull) return DHTGPU_ERANGE;
+    c->has_ids = false;
+    c->stride = pad_ids(n ? n : 1);
+    DHT_TRY(c->planes.ensure((size_t)c->stride * 5 * 4));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_set_ids(dhtgpu_ctx* c, const uint8_t* ids20, uint64_t n) {
+    if (!c || (!ids20 && n)) return DHTGPU_EINVAL;
+    DHT_TRY(c->bind());
+    int r = alloc_ids(c, n);
+    if (r) return r;
+    const uint64_t chunk = 1ull << 22;   // 80 MB of staging at a time
+    DHT_TRY(c->staging.ensure((size_t)std::min<uint64_t>(n ? n : 1, chunk) * 20));
+    for (uint64_t i = 0; i < n; i += chunk) {
+        const uint64_t m = std::min(chunk, n - i);
+        DHT_TRY(hipMemcpyAsync(c->staging.p, ids20 + i * 20, (size_t)m * 20, hipMemcpyHostToDevice, c->stream));
+        DHT_TRY(launch_pack(c->staging.as<uint8_t>(), m, c->planes.as<uint32_t>() + i, c->stride, c->stream));
+        DHT_TRY(hipStreamSynchronize(c->stream));   // staging is reused
+    }
+    return finish_ids(c, n);
+}
+
+int dhtgpu_gen_ids(dhtgpu_ctx* c, uint64_t seed, uint64_t start, uint64_t n) {
+    if (!c) return DHTGPU_EINVAL;
+    DHT_TRY(c->bind());
+    int r = alloc_ids(c, n);
+    if (r) return r;
+    DHT_TRY(launch_gen(seed, start, n, c->planes.as<uint32_t>(), c->stride, c->stream));
+    return finish_ids(c, n);
+}
+
+int dhtgpu_get_ids(dhtgpu_ctx* c, uint64_t first, uint64_t n, uint8_t* out20) {
+    if (!c || (!out20 && n)) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    if (first > c->n || n > c->n - first) return DHTGPU_ERANGE;
+    if (!n) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    DHT_TRY(c->staging.ensure((size_t)n * 20));
+    DHT_TRY(launch_unpack(c->planes.as<uint32_t>(), c->stride, first, n, c->staging.as<uint8_t>(), c->stream));
+    DHT_TRY(hipMemcpyAsync(out20, c->staging.p, (size_t)n * 20, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_ids_dev(dhtgpu_ctx* c, const uint32_t** planes, uint64_t* stride) {
+    if (!c || !planes || !stride) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    *planes = c->planes.as<uint32_t>();
+    *stride = c->stride;
+    return DHTGPU_OK;
+}
+
+int dhtgpu_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k,
+                    uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base,
+                    void* stream) {
+    if (!c || k == 0 || k > DHTGPU_MAX_K || (q && !tp)) return DHTGPU_EINVAL;
+    if (!out_rec && (!out_idx || !out_cnt)) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const ScanPlan p = plan_scan(c->n, q, c->num_cus);
+    if (p.splits == 1 || c->n == 0) {
+        DHT_TRY(launch_scan(c->planes.as<uint32_t>(), c->stride, c->n, p, tp, ts, q, k, out_idx,
+                            out_cnt, out_rec, idx_base, s));
+        return DHTGPU_OK;
+    }
+    // split id range: per-split candidate records, then K3 merge
+    DHT_TRY(c->rec.ensure((size_t)p.splits * q * k * 6 * 4));
+    DHT_TRY(launch_scan(c->planes.as<uint32_t>(), c->stride, c->n, p, tp, ts, q, k, nullptr,
+                        nullptr, c->rec.as<uint32_t>(), 0, s));
+    if (!out_rec) {
+        DHT_TRY(launch_merge(c->rec.as<uint32_t>(), p.splits, q, k, tp, ts, k, out_idx, out_cnt, s));
+        if (idx_base) DHT_TRY(launch_add_base(out_idx, (uint64_t)q * k, idx_base, s));
+        return DHTGPU_OK;
+    }
+    // records requested (cross-shard merge): merge locally, then re-gather records
+    DHT_TRY(c->out_idx.ensure((size_t)q * k * 4));
+    DHT_TRY(c->out_cnt.ensure((size_t)q * 4));
+    DHT_TRY(launch_merge(c->rec.as<uint32_t>(), p.splits, q, k, tp, ts, k, c->out_idx.as<uint32_t>(),
+                         c->out_cnt.as<uint32_t>(), s));
+    DHT_TRY(launch_rec_from_idx(c->out_idx.as<uint32_t>(), (uint64_t)q * k, c->planes.as<uint32_t>(),
+                                c->stride, idx_base, out_rec, s));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_merge_dev(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_t k_in,
+                     const uint32_t* tp, uint64_t ts, uint32_t k, uint32_t* out_idx,
+                     uint32_t* out_cnt, void* stream) {
+    if (!rec || !tp || !out_idx || !out_cnt || k == 0 || k > DHTGPU_MAX_K || lists == 0 || k_in == 0)
+        return DHTGPU_EINVAL;
+    if ((size_t)lists * k_in * 24 > 160 * 1024) return DHTGPU_ERANGE;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(launch_merge(rec, lists, q, k_in, tp, ts, k, out_idx, out_cnt, (hipStream_t)stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_pack_dev(const uint8_t* ids20, uint64_t n, uint32_t* planes, uint64_t stride, void* stream) {
+    if ((!ids20 || !planes) && n) return DHTGPU_EINVAL;
+    if (stride < n) return DHTGPU_EINVAL;
+    DHT_TRY(launch_pack(ids20, n, planes, stride, (hipStream_t)stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_gen_dev(uint64_t seed, uint64_t start, uint64_t n, uint32_t* planes, uint64_t stride,
+                   void* stream) {
+    if (!planes && n) return DHTGPU_EINVAL;
+    if (stride < n) return DHTGPU_EINVAL;
+    DHT_TRY(launch_gen(seed, start, n, planes, stride, (hipStream_t)stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_topk(dhtgpu_ctx* c, const uint8_t* t20, uint32_t q, uint32_t k, uint32_t* out_idx,
+                uint32_t* out_cnt) {
+    if (!c || k == 0 || k > DHTGPU_MAX_K || (q && (!t20 || !out_idx || !out_cnt))) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    uint64_t ts = 0;
+    DHT_TRY(c->upload_targets(t20, q, &ts));
+    DHT_TRY(c->aux2.ensure((size_t)q * k * 4));
+    DHT_TRY(c->aux3.ensure((size_t)q * 4));
+    int r = dhtgpu_topk_dev(c, c->targets.as<uint32_t>(), ts, q, k, c->aux2.as<uint32_t>(),
+                            c->aux3.as<uint32_t>(), nullptr, 0, c->stream);
+    if (r) return r;
+    DHT_TRY(hipMemcpyAsync(out_idx, c->aux2.p, (size_t)q * k * 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(out_cnt, c->aux3.p, (size_t)q * 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_find_closest(dhtgpu_ctx* c, uint32_t nb, const uint8_t* firsts20, const uint32_t* off,
+                        const uint8_t* node_ids20, const uint8_t* good, const uint8_t* t20,
+                        uint32_t q, uint32_t count, uint32_t* out_idx, uint32_t* out_cnt) {
+    if (!c || count == 0 || count > DHTGPU_MAX_K) return DHTGPU_EINVAL;
+    if (q && (!t20 || !out_idx || !out_cnt)) return DHTGPU_EINVAL;
+    if (nb > 256 || (nb && (!firsts20 || !off))) return DHTGPU_EINVAL;
+    if (!q) return DHTGPU_OK;
+    if (nb == 0) {   // empty table: empty result (src/routing_table.cpp:116)
+        for (uint32_t i = 0; i < q; ++i) {
+            out_cnt[i] = 0;
+            for (uint32_t r = 0; r < count; ++r) out_idx[(size_t)i * count + r] = DHTGPU_NONE;
+        }
+        return DHTGPU_OK;
+    }
+    const uint32_t nn = off[nb];
+    if (nn && (!node_ids20 || !good)) return DHTGPU_EINVAL;
+    for (uint32_t b = 0; b < nb; ++b)
+        if (off[b] > off[b + 1]) return DHTGPU_EINVAL;
+    DHT_TRY(c->bind());
+    // host snapshot -> one device blob: firsts planes | off | gcnt | node planes | good
+    const uint64_t ns = pad_q(nn ? nn : 1);
+    std::vector<uint32_t> fp((size_t)5 * nb), gcnt(nb);
+    for (uint32_t b = 0; b < nb; ++b) {
+        for (int w = 0; w < 5; ++w) {
+            const uint8_t* p = firsts20 + 20 * b + 4 * w;
+            fp[(size_t)w * nb + b] = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+        }
+        uint32_t g = 0;
+        for (uint32_t i = off[b]; i < off[b + 1]; ++i) g += good[i] != 0;
+        gcnt[b] = g;
+    }
+    const size_t o_fp = 0, o_off = o_fp + fp.size() * 4, o_g = o_off + (size_t)(nb + 1) * 4,
+                 o_np = (o_g + (size_t)nb * 4 + 15) & ~size_t(15), o_good = o_np + (size_t)ns * 5 * 4,
+                 total = o_good + nn + 16;
+    DHT_TRY(c->aux.ensure(total));
+    uint8_t* base = c->aux.as<uint8_t>();
+    DHT_TRY(hipMemcpyAsync(base + o_fp, fp.data(), fp.size() * 4, hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(hipMemcpyAsync(base + o_off, off, (size_t)(nb + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(hipMemcpyAsync(base + o_g, gcnt.data(), (size_t)nb * 4, hipMemcpyHostToDevice, c->stream));
+    if (nn) {
+        DHT_TRY(hipMemcpyAsync(base + o_good, good, nn, hipMemcpyHostToDevice, c->stream));
+        DHT_TRY(c->staging.ensure((size_t)std::max<uint64_t>(nn, q) * 20));
+        DHT_TRY(hipMemcpyAsync(c->staging.p, node_ids20, (size_t)nn * 20, hipMemcpyHostToDevice, c->stream));
+        DHT_TRY(launch_pack(c->staging.as<uint8_t>(), nn, (uint32_t*)(base + o_np), ns, c->stream));
+        DHT_TRY(hipStreamSynchronize(c->stream));   // staging reused for targets
+    }
+    uint64_t ts = 0;
+    DHT_TRY(c->upload_targets(t20, q, &ts));
+    DHT_TRY(c->aux2.ensure((size_t)q * count * 4));
+    DHT_TRY(c->aux3.ensure((size_t)q * 4));
+    DHT_TRY(launch_find_closest(nb, (const uint32_t*)(base + o_fp), (const uint32_t*)(base + o_off),
+                                (const uint32_t*)(base + o_g), (const uint32_t*)(base + o_np), ns,
+                                base + o_good, c->targets.as<uint32_t>(), ts, q, count,
+                                c->aux2.as<uint32_t>(), c->aux3.as<uint32_t>(), c->stream));
+    DHT_TRY(hipMemcpyAsync(out_idx, c->aux2.p, (size_t)q * count * 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(out_cnt, c->aux3.p, (size_t)q * 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_classify_dev(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t nb,
+                        const uint32_t* d_fp, const uint32_t* myid_words, uint8_t* out_bucket,
+                        unsigned long long* d_hist, void* stream) {
+    if (!d_fp || !myid_words || !d_hist || nb == 0 || nb > 256 || (n && !planes)) return DHTGPU_EINVAL;
+    DHT_TRY(launch_classify(planes, stride, n, nb, d_fp, myid_words, out_bucket, d_hist, (hipStream_t)stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_classify(dhtgpu_ctx* c, uint32_t nb, const uint8_t* firsts20, const uint8_t* myid20,
+                    uint8_t* out_bucket, uint64_t* hist161) {
+    if (!c || !firsts20 || !myid20 || !hist161 || nb == 0 || nb > 256) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    DHT_TRY(c->bind());
+    std::vector<uint32_t> fp((size_t)5 * nb);
+    uint32_t my[5];
+    auto be = [](const uint8_t* p) {
+        return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+    };
+    for (uint32_t b = 0; b < nb; ++b)
+        for (int w = 0; w < 5; ++w) fp[(size_t)w * nb + b] = be(firsts20 + 20 * b + 4 * w);
+    for (int w = 0; w < 5; ++w) my[w] = be(myid20 + 4 * w);
+    DHT_TRY(c->aux.ensure(fp.size() * 4 + 161 * 8 + 64));
+    uint8_t* base = c->aux.as<uint8_t>();
+    unsigned long long* d_hist = (unsigned long long*)(base + ((fp.size() * 4 + 15) & ~size_t(15)));
+    DHT_TRY(hipMemcpyAsync(base, fp.data(), fp.size() * 4, hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(hipMemsetAsync(d_hist, 0, 161 * 8, c->stream));
+    uint8_t* d_bucket = nullptr;
+    if (out_bucket && c->n) {
+        DHT_TRY(c->aux2.ensure((size_t)c->n + 16));
+        d_bucket = c->aux2.as<uint8_t>();
+    }
+    DHT_TRY(launch_classify(c->planes.as<uint32_t>(), c->stride, c->n, nb, (const uint32_t*)base, my,
+                            d_bucket, d_hist, c->stream));
+    if (d_bucket) DHT_TRY(hipMemcpyAsync(out_bucket, d_bucket, (size_t)c->n, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(hist161, d_hist, 161 * 8, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_cached_nodes(dhtgpu_ctx* c, const uint8_t* accept, const uint8_t* t20, uint32_t q,
+                        uint32_t count, uint32_t* out_idx, uint32_t* out_cnt) {
+    if (!c || count == 0 || count > DHTGPU_MAX_K || (q && (!t20 || !out_idx || !out_cnt))) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    if (!c->sorted) return DHTGPU_EUNSORTED;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    uint8_t* d_acc = nullptr;
+    if (accept && c->n) {
+        DHT_TRY(c->aux.ensure((size_t)c->n + 16));
+        d_acc = c->aux.as<uint8_t>();
+        DHT_TRY(hipMemcpyAsync(d_acc, accept, (size_t)c->n, hipMemcpyHostToDevice, c->stream));
+    }
+    uint64_t ts = 0;
+    DHT_TRY(c->upload_targets(t20, q, &ts));
+    DHT_TRY(c->aux2.ensure((size_t)q * count * 4));
+    DHT_TRY(c->aux3.ensure((size_t)q * 4));
+    DHT_TRY(launch_cached(c->planes.as<uint32_t>(), c->stride, c->n, d_acc, c->targets.as<uint32_t>(),
+                          ts, q, count, c->aux2.as<uint32_t>(), c->aux3.as<uint32_t>(), c->stream));
+    DHT_TRY(hipMemcpyAsync(out_idx, c->aux2.p, (size_t)q * count * 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(out_cnt, c->aux3.p, (size_t)q * 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    return DHTGPU_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,63 @@
+// dhtgpu_internal.h -- host-side launch entry points shared between the kernel
+// translation units and the C ABI (api.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dhtgpu {
+
+// ID-plane geometry: planes are padded to a multiple of kTile ids so that the scan
+// kernel can stream whole tiles without bounds checks.
+constexpr uint32_t kTile = 4096;
+constexpr uint32_t kScanWaves = 8;       // waves per scan workgroup
+constexpr uint32_t kScanTargets = 16;    // targets held (wave-uniform) per wave
+
+inline uint64_t pad_ids(uint64_t n) { return ((n + kTile - 1) / kTile) * kTile; }
+
+// keys.hip
+hipError_t launch_gen(uint64_t seed, uint64_t start, uint64_t n, uint32_t* planes,
+                      uint64_t stride, hipStream_t s);
+hipError_t launch_pack(const uint8_t* ids20, uint64_t n, uint32_t* planes, uint64_t stride,
+                       hipStream_t s);
+hipError_t launch_unpack(const uint32_t* planes, uint64_t stride, uint64_t first, uint64_t n,
+                         uint8_t* out20, hipStream_t s);
+hipError_t launch_fill(uint32_t* p, uint64_t n, uint32_t v, hipStream_t s);
+// sets *d_flag to 1 if ids are NOT strictly ascending (unsorted or duplicated)
+hipError_t launch_check_sorted(const uint32_t* planes, uint64_t stride, uint64_t n,
+                               uint32_t* d_flag, hipStream_t s);
+
+// scan.hip
+struct ScanPlan {
+    uint32_t blocks_x;   // target groups
+    uint32_t splits;     // id-range splits
+    uint64_t split_len;  // ids per split (multiple of kTile)
+};
+ScanPlan plan_scan(uint64_t n, uint32_t q, int num_cus);
+hipError_t launch_scan(const uint32_t* ids, uint64_t is, uint64_t n, const ScanPlan& p,
+                       const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k,
+                       uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec,
+                       uint32_t idx_base, hipStream_t s);
+hipError_t launch_merge(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_t kin,
+                        const uint32_t* tp, uint64_t ts, uint32_t k, uint32_t* out_idx,
+                        uint32_t* out_cnt, hipStream_t s);
+
+// out_idx[i] += base for valid entries
+hipError_t launch_add_base(uint32_t* idx, uint64_t m, uint32_t base, hipStream_t s);
+// rec[i] = {words of id idx[i], idx[i] + base} (DHT_NONE record for DHT_NONE)
+hipError_t launch_rec_from_idx(const uint32_t* idx, uint64_t m, const uint32_t* planes,
+                               uint64_t stride, uint32_t base, uint32_t* rec, hipStream_t s);
+
+// table.hip
+hipError_t launch_find_closest(uint32_t nb, const uint32_t* fp, const uint32_t* off,
+                               const uint32_t* gcnt, const uint32_t* np, uint64_t ns,
+                               const uint8_t* good, const uint32_t* tp, uint64_t ts, uint32_t q,
+                               uint32_t count, uint32_t* out_idx, uint32_t* out_cnt,
+                               hipStream_t s);
+hipError_t launch_classify(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t nb,
+                           const uint32_t* fp, const uint32_t* myid, uint8_t* out_bucket,
+                           unsigned long long* hist, hipStream_t s);
+hipError_t launch_cached(const uint32_t* planes, uint64_t stride, uint64_t n,
+                         const uint8_t* accept, const uint32_t* tp, uint64_t ts, uint32_t q,
+                         uint32_t count, uint32_t* out_idx, uint32_t* out_cnt, hipStream_t s);
+
+}  // namespace dhtgpu

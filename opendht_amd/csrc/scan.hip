@@ -1,0 +1,347 @@
+// scan.hip -- K1 xor_topk_scan and K3 topk_merge for gfx950.
+//
+// K1 restates std::partial_sort(ids, ids+k, ids+n, [t](a,b){ return t.xorCmp(a,b) < 0; })
+// (InfoHash::xorCmp, include/opendht/infohash.h:179-194) for a batch of
+// targets.  Design (integer compare-select; MFMA deliberately unused):
+//   * ids are streamed as the w0 word plane (4 B/id) through a double-buffered LDS
+//     tile shared by the 8 waves of a workgroup; each lane reads 16 ids per chunk with
+//     4 conflict-free ds_read_b128;
+//   * each wave owns kScanTargets targets whose w0 word and current k-th distance
+//     (threshold) are wave-uniform (SGPRs); per (id, target) pair the hot loop costs a
+//     v_xor_b32 plus half a v_min3_u32 (1.5 VALU ops), and one compare per target per
+//     16-id chunk decides whether any lane holds a candidate;
+//   * the exact top-k of each target is register-resident and lane-distributed (lane r
+//     holds rank r as {w0 distance, id index}) and is updated by ballot + shuffle
+//     insertion; ties on the w0 distance are resolved by a full 160-bit compare that
+//     reads the remaining planes (rare: < 1 in 10^3 insertions at N = 2^24);
+//   * when the batch has too few targets to fill the chip the id range is split across
+//     workgroups and the per-split lists are merged by K3.
+#include "dhtgpu_dev.h"
+#include "dhtgpu_internal.h"
+
+namespace dhtgpu {
+namespace {
+
+constexpr uint32_t WAVES = kScanWaves;
+constexpr uint32_t TILE = kTile;
+constexpr uint32_t CHUNK = 1024;       // ids per chunk per wave (16 per lane)
+
+// Is the (w0-distance-equal) entry `ei` closer to the target than candidate `ci`?
+// Full compare on words 1..4, then index (ties only for duplicated ids).
+__device__ __forceinline__ bool entry_closer_full(const uint32_t* __restrict__ ids, uint64_t is,
+                                               uint32_t ei, uint32_t ci,
+                                               const uint32_t* __restrict__ tp, uint64_t ts,
+                                               uint32_t qi) {
+    uint32_t a[DHT_W], b[DHT_W], t[DHT_W];
+    load_id(ids, is, ei, a);
+    load_id(ids, is, ci, b);
+    load_id(tp, ts, qi, t);
+    return xor_less_from(a, ei, b, ci, t, 1);
+}
+
+// Insert candidate (cd = w0 distance, ci = id index) into the lane-distributed sorted
+// list {ed, ei} of length cnt <= K.  cnt/thr are wave-uniform.
+template <uint32_t K>
+__device__ __forceinline__ void topk_insert(uint32_t& ed, uint32_t& ei, uint32_t& cnt,
+                                            uint32_t& thr, uint32_t cd, uint32_t ci,
+                                            uint32_t lane, const uint32_t* __restrict__ ids,
+                                            uint64_t is, const uint32_t* __restrict__ tp,
+                                            uint64_t ts, uint32_t qi) {
+    const bool valid = lane < cnt;
+    bool closer = valid && ed < cd;
+    if (valid && ed == cd) closer = entry_closer_full(ids, is, ei, ci, tp, ts, qi);
+    const uint32_t pos = (uint32_t)__popcll(__ballot(closer));
+    if (pos >= K) return;
+    const uint32_t ud = __shfl_up(ed, 1), ui = __shfl_up(ei, 1);
+    if (lane == pos) {
+        ed = cd;
+        ei = ci;
+    } else if (lane > pos) {
+        ed = ud;
+        ei = ui;
+    }
+    cnt = cnt + 1 < K ? cnt + 1 : K;
+    thr = cnt == K ? (uint32_t)__builtin_amdgcn_readlane((int)ed, K - 1) : DHT_NONE;
+}
+
+template <uint32_t K, uint32_t T>
+__global__ __launch_bounds__(WAVES * 64) void k_scan(
+    const uint32_t* __restrict__ ids, uint64_t is, uint64_t n, uint64_t split_len,
+    const uint32_t* __restrict__ tp, uint64_t ts, uint32_t q, uint32_t k,
+    uint32_t* __restrict__ out_idx, uint32_t* __restrict__ out_cnt, uint32_t* __restrict__ out_rec,
+    uint32_t idx_base) {
+    __shared__ uint4 tile[2][TILE / 4];
+
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t id_begin = (uint64_t)blockIdx.y * split_len;
+    const uint64_t id_end = n < id_begin + split_len ? n : id_begin + split_len;
+    const uint32_t qbase = (blockIdx.x * WAVES + wave) * T;
+
+    uint32_t t0[T], thr[T], cnt[T], ed[T], ei[T];
+#pragma unroll
+    for (uint32_t j = 0; j < T; ++j) {
+        const uint32_t qi = qbase + j < q ? qbase + j : q - 1;
+        t0[j] = __builtin_amdgcn_readfirstlane(tp[qi]);
+        thr[j] = DHT_NONE;
+        cnt[j] = 0;
+        ed[j] = DHT_NONE;
+        ei[j] = DHT_NONE;
+    }
+
+    const uint64_t ntiles = id_end > id_begin ? (id_end - id_begin + TILE - 1) / TILE : 0;
+    uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0;
+    if (ntiles) {
+        const uint4* src = reinterpret_cast<const uint4*>(ids + id_begin);
+        pf0 = src[threadIdx.x];
+        pf1 = src[threadIdx.x + WAVES * 64];
+        tile[0][threadIdx.x] = pf0;
+        tile[0][threadIdx.x + WAVES * 64] = pf1;
+    }
+    __syncthreads();
+
+    for (uint64_t t = 0; t < ntiles; ++t) {
+        const uint64_t tb = id_begin + t * TILE;
+        if (t + 1 < ntiles) {
+            const uint4* src = reinterpret_cast<const uint4*>(ids + tb + TILE);
+            pf0 = src[threadIdx.x];
+            pf1 = src[threadIdx.x + WAVES * 64];
+        }
+        const uint4* buf = tile[t & 1];
+        const uint32_t* bufw = reinterpret_cast<const uint32_t*>(buf);
+
+#pragma unroll 1
+        for (uint32_t c = 0; c < TILE / CHUNK; ++c) {
+            uint32_t x[16];
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r) {
+                const uint4 v = buf[c * (CHUNK / 4) + r * 64 + lane];
+                x[4 * r + 0] = v.x;
+                x[4 * r + 1] = v.y;
+                x[4 * r + 2] = v.z;
+                x[4 * r + 3] = v.w;
+            }
+            // ids of this chunk still inside [tb + c*CHUNK, id_end)
+            const uint64_t cbase = tb + c * CHUNK;
+            const uint32_t rem = id_end > cbase ? (uint32_t)min<uint64_t>(id_end - cbase, CHUNK) : 0;
+
+#pragma unroll
+            for (uint32_t j = 0; j < T; ++j) {
+                const uint32_t tj = t0[j];
+                uint32_t a = min(x[0] ^ tj, x[1] ^ tj);
+#pragma unroll
+                for (uint32_t s = 2; s < 16; s += 2) a = min(a, min(x[s] ^ tj, x[s + 1] ^ tj));
+                if (__ballot(a <= thr[j])) {
+                    // slow path: collect this lane's passing slots, then insert serially
+                    uint32_t lim = thr[j];
+                    if (cnt[j] < K) {
+                        // Warm-up: the K-th smallest per-lane minimum v* bounds the K-th
+                        // smallest distance of the chunk (K ids lie at or below it), so
+                        // ids above v* cannot enter the top-K; find v* by bisection.
+                        uint32_t av = DHT_NONE;
+#pragma unroll
+                        for (uint32_t s = 0; s < 16; ++s) {
+                            const uint32_t off = (s >> 2) * 256 + 4 * lane + (s & 3);
+                            if (off < rem) av = min(av, x[s] ^ tj);
+                        }
+                        const bool has = 4 * lane < rem;
+                        if ((uint32_t)__popcll(__ballot(has)) >= K) {
+                            uint32_t v = 0;
+                            for (int bit = 31; bit >= 0; --bit) {
+                                const uint32_t tryv = v | ((1u << bit) - 1u);
+                                if ((uint32_t)__popcll(__ballot(has && av <= tryv)) < K) v |= 1u << bit;
+                            }
+                            lim = min(lim, v);
+                        }
+                    }
+                    uint32_t bits = 0;
+#pragma unroll
+                    for (uint32_t s = 0; s < 16; ++s) {
+                        const uint32_t off = (s >> 2) * 256 + 4 * lane + (s & 3);
+                        bits |= (uint32_t)(((x[s] ^ tj) <= lim) && off < rem) << s;
+                    }
+                    const uint32_t qi = qbase + j < q ? qbase + j : q - 1;
+                    for (;;) {
+                        const uint64_t m = __ballot(bits != 0);
+                        if (!m) break;
+                        const uint32_t L = (uint32_t)__ffsll((long long)m) - 1;
+                        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)bits, L);
+                        const uint32_t s = (uint32_t)__ffs(b) - 1;
+                        if (lane == L) bits &= bits - 1;
+                        const uint32_t off = (s >> 2) * 256 + 4 * L + (s & 3);
+                        const uint32_t cd = bufw[c * CHUNK + off] ^ tj;
+                        if (cd <= thr[j])
+                            topk_insert<K>(ed[j], ei[j], cnt[j], thr[j], cd,
+                                           (uint32_t)(cbase + off), lane, ids, is, tp, ts, qi);
+                    }
+                }
+            }
+        }
+        if (t + 1 < ntiles) {
+            tile[(t + 1) & 1][threadIdx.x] = pf0;
+            tile[(t + 1) & 1][threadIdx.x + WAVES * 64] = pf1;
+        }
+        __syncthreads();
+    }
+
+    // write results
+#pragma unroll
+    for (uint32_t j = 0; j < T; ++j) {
+        const uint32_t qi = qbase + j;
+        if (qi >= q) continue;
+        if (out_rec) {
+            if (lane < k) {
+                uint32_t* r = out_rec + (((uint64_t)blockIdx.y * q + qi) * k + lane) * 6;
+                if (lane < cnt[j]) {
+#pragma unroll
+                    for (int w = 0; w < DHT_W; ++w) r[w] = ids[(uint64_t)w * is + ei[j]];
+                    r[5] = ei[j] + idx_base;
+                } else {
+#pragma unroll
+                    for (int w = 0; w < 6; ++w) r[w] = DHT_NONE;
+                }
+            }
+        } else {
+            if (lane < k) out_idx[(uint64_t)qi * k + lane] = lane < cnt[j] ? ei[j] + idx_base : DHT_NONE;
+            if (lane == 0) out_cnt[qi] = cnt[j] < k ? cnt[j] : k;
+        }
+    }
+}
+
+// K3: one wave per target; candidates staged in LDS as {w0^t .. w4^t, idx}; the rank
+// of each valid candidate (number of strictly closer candidates) is its output slot.
+__global__ __launch_bounds__(64) void k_merge(const uint32_t* __restrict__ rec, uint32_t lists,
+                                              uint32_t q, uint32_t kin,
+                                              const uint32_t* __restrict__ tp, uint64_t ts,
+                                              uint32_t k, uint32_t* __restrict__ out_idx,
+                                              uint32_t* __restrict__ out_cnt) {
+    extern __shared__ uint32_t sm[];
+    const uint32_t qi = blockIdx.x, lane = lane_id();
+    const uint32_t C = lists * kin;
+    uint32_t t[DHT_W];
+    load_id(tp, ts, qi, t);
+    uint32_t nvalid = 0;
+    for (uint32_t c0 = 0; c0 < C; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        bool v = false;
+        if (c < C) {
+            const uint32_t l = c / kin, r = c % kin;
+            const uint32_t* src = rec + (((uint64_t)l * q + qi) * kin + r) * 6;
+            const uint32_t idx = src[5];
+            v = idx != DHT_NONE;
+#pragma unroll
+            for (int w = 0; w < DHT_W; ++w) sm[c * 6 + w] = src[w] ^ t[w];
+            sm[c * 6 + 5] = idx;
+        }
+        nvalid += (uint32_t)__popcll(__ballot(v));
+    }
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < C; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        if (c >= C) continue;
+        uint32_t key[6];
+#pragma unroll
+        for (int w = 0; w < 6; ++w) key[w] = sm[c * 6 + w];
+        if (key[5] == DHT_NONE) continue;
+        uint32_t rank = 0;
+        for (uint32_t o = 0; o < C; ++o) {
+            const uint32_t* kk = sm + o * 6;
+            if (kk[5] == DHT_NONE) continue;
+            bool less = false, decided = false;
+#pragma unroll
+            for (int w = 0; w < 6; ++w) {
+                if (!decided && kk[w] != key[w]) {
+                    less = kk[w] < key[w];
+                    decided = true;
+                }
+            }
+            rank += less;
+        }
+        if (rank < k) out_idx[(uint64_t)qi * k + rank] = key[5];
+    }
+    const uint32_t nout = nvalid < k ? nvalid : k;
+    if (lane >= nout && lane < k) out_idx[(uint64_t)qi * k + lane] = DHT_NONE;
+    for (uint32_t r = 64 + lane; r < k; r += 64)
+        if (r >= nout) out_idx[(uint64_t)qi * k + r] = DHT_NONE;
+    if (lane == 0) out_cnt[qi] = nout;
+}
+
+__global__ __launch_bounds__(256) void k_add_base(uint32_t* __restrict__ idx, uint64_t m, uint32_t base) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < m && idx[i] != DHT_NONE) idx[i] += base;
+}
+
+__global__ __launch_bounds__(256) void k_rec_from_idx(const uint32_t* __restrict__ idx, uint64_t m,
+                                                      const uint32_t* __restrict__ planes,
+                                                      uint64_t stride, uint32_t base,
+                                                      uint32_t* __restrict__ rec) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t x = idx[i];
+#pragma unroll
+    for (int w = 0; w < DHT_W; ++w) rec[i * 6 + w] = x == DHT_NONE ? DHT_NONE : planes[(uint64_t)w * stride + x];
+    rec[i * 6 + 5] = x == DHT_NONE ? DHT_NONE : x + base;
+}
+
+template <uint32_t K>
+hipError_t launch_scan_k(const uint32_t* ids, uint64_t is, uint64_t n, const ScanPlan& p,
+                         const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k,
+                         uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec,
+                         uint32_t idx_base, hipStream_t s) {
+    dim3 grid(p.blocks_x, p.splits);
+    k_scan<K, kScanTargets><<<grid, WAVES * 64, 0, s>>>(ids, is, n, p.split_len, tp, ts, q, k,
+                                                        out_idx, out_cnt, out_rec, idx_base);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+ScanPlan plan_scan(uint64_t n, uint32_t q, int num_cus) {
+    ScanPlan p;
+    const uint32_t per_block = WAVES * kScanTargets;
+    p.blocks_x = (q + per_block - 1) / per_block;
+    const uint64_t ntiles = (n + TILE - 1) / TILE;
+    // aim for >= 2 workgroups per CU; never split below one tile per workgroup
+    const uint64_t want = (uint64_t)(num_cus > 0 ? num_cus : 256) * 2;
+    uint64_t splits = (want + p.blocks_x - 1) / p.blocks_x;
+    if (splits > ntiles) splits = ntiles ? ntiles : 1;
+    if (splits < 1) splits = 1;
+    const uint64_t tiles_per = (ntiles + splits - 1) / splits;
+    p.split_len = (tiles_per ? tiles_per : 1) * TILE;
+    p.splits = (uint32_t)((n + p.split_len - 1) / p.split_len);
+    if (p.splits == 0) p.splits = 1;
+    return p;
+}
+
+hipError_t launch_scan(const uint32_t* ids, uint64_t is, uint64_t n, const ScanPlan& p,
+                       const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k,
+                       uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec,
+                       uint32_t idx_base, hipStream_t s) {
+    if (k <= 8) return launch_scan_k<8>(ids, is, n, p, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s);
+    if (k <= 16) return launch_scan_k<16>(ids, is, n, p, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s);
+    return launch_scan_k<32>(ids, is, n, p, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s);
+}
+
+hipError_t launch_add_base(uint32_t* idx, uint64_t m, uint32_t base, hipStream_t s) {
+    if (!m) return hipSuccess;
+    k_add_base<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(idx, m, base);
+    return hipGetLastError();
+}
+
+hipError_t launch_rec_from_idx(const uint32_t* idx, uint64_t m, const uint32_t* planes,
+                               uint64_t stride, uint32_t base, uint32_t* rec, hipStream_t s) {
+    if (!m) return hipSuccess;
+    k_rec_from_idx<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(idx, m, planes, stride, base, rec);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_t kin,
+                        const uint32_t* tp, uint64_t ts, uint32_t k, uint32_t* out_idx,
+                        uint32_t* out_cnt, hipStream_t s) {
+    const size_t lds = (size_t)lists * kin * 6 * sizeof(uint32_t);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    k_merge<<<q, 64, lds, s>>>(rec, lists, q, kin, tp, ts, k, out_idx, out_cnt);
+    return hipGetLastError();
+}
+
+}  // namespace dhtgpu

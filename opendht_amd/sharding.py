@@ -1,0 +1,33 @@
+"""Multi-GPU sharding of the id set (north-star scheme).
+
+The N ids are split into contiguous ranges, one per rank.  Every rank scans its range
+for all targets and emits candidate records {w0..w4, global idx} (24 B, k per target);
+one all-gather (RCCL over xGMI on MI355X, gloo in CPU tests) exchanges them and K3
+merges world*k candidates per target into the exact global top-k.  Bit-exactness holds
+because the merge uses the same total order (XOR distance, then global index).
+"""
+import torch
+import torch.distributed as dist
+
+REC_WORDS = 6
+
+
+def shard_range(n, world, rank):
+    """Contiguous [lo, hi) share of n ids for `rank` (first n % world ranks get one more)."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def gather_records(rec, group=None):
+    """All-gather this rank's (q, k, 6) int32 candidate records -> (world, q, k, 6)."""
+    world = dist.get_world_size(group)
+    out = torch.empty((world,) + tuple(rec.shape), dtype=rec.dtype, device=rec.device)
+    dist.all_gather_into_tensor(out, rec.contiguous(), group=group)
+    return out
+
+
+def sharded_topk(local_records, merge, group=None):
+    """One sharded lookup: local_records() -> (q, k, 6) records of this rank's shard;
+    merge(gathered (world, q, k, 6)) -> final (idx, cnt)."""
+    return merge(gather_records(local_records(), group))

@@ -1,0 +1,51 @@
+"""CPU-side checks of the drop-in boundary: libdhtgpu.so loads and exports every
+entry point include/dhtgpu.h declares (no compute calls -- no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import opendht_amd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "dhtgpu.h")).read()
+    return sorted(set(re.findall(r"\b(dhtgpu_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_built():
+    assert os.path.exists(opendht_amd.LIB_PATH), "run __graft_entry__.build() first"
+
+
+def test_exports_match_header():
+    syms = header_symbols()
+    assert len(syms) >= 15
+    out = subprocess.check_output(["nm", "-D", "--defined-only", opendht_amd.LIB_PATH], text=True)
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+    assert sorted(opendht_amd.exported_symbols()) == syms
+
+
+def test_ctypes_load_and_strerror():
+    L = opendht_amd.lib()
+    for s in header_symbols():
+        assert hasattr(L, s)
+    assert L.dhtgpu_strerror(0) == b"ok"
+    assert L.dhtgpu_strerror(-5).startswith(b"id set is not")
+
+
+def test_cpp_adapter_header_compiles(tmp_path):
+    """The C++11 host adapter (include/dhtgpu.hpp) compiles as C++11 against a
+    reference-shaped mock table (tests/cpp/adapter_check.cpp)."""
+    src = os.path.join(ROOT, "tests", "cpp", "adapter_check.cpp")
+    if not os.path.exists(src):
+        pytest.skip("adapter check source absent")
+    exe = tmp_path / "adapter_check"
+    subprocess.check_call(["g++", "-std=c++11", "-Wall", "-Wextra", "-I", os.path.join(ROOT, "include"),
+                           src, "-o", str(exe), "-L", os.path.dirname(opendht_amd.LIB_PATH), "-ldhtgpu",
+                           "-Wl,-rpath," + os.path.dirname(opendht_amd.LIB_PATH)])

@@ -1,0 +1,190 @@
+"""GPU parity: libdhtgpu (HIP, gfx950) against the CPU oracle, bit-exact.
+All calls go through the C ABI (ctypes).  Marked gpu: run on the MI355X box."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import opendht_amd
+    c = opendht_amd.Context(0)
+    yield c
+    c.close()
+
+
+def check_topk(ctx, ids, targets, k):
+    ctx.set_ids(ids)
+    got, gcnt = ctx.topk(targets, k)
+    want, wcnt = O.topk(ids, targets, k)
+    assert np.array_equal(gcnt, wcnt)
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} mismatching targets, first {bad[:5]}: got {got[bad[0]]} want {want[bad[0]]}"
+
+
+def test_gen_matches_oracle(ctx):
+    ctx.gen_ids(123, 10007, start=5)
+    assert np.array_equal(ctx.get_ids(), O.gen_ids(123, 10007, start=5))
+
+
+def test_set_get_roundtrip(ctx):
+    ids = O.gen_ids(5, 4099)
+    ctx.set_ids(ids)
+    assert ctx.num_ids == 4099
+    assert np.array_equal(ctx.get_ids(), ids)
+    assert np.array_equal(ctx.get_ids(4000, 99), ids[4000:])
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 9, 100, 4096, 5000, 70001])
+@pytest.mark.parametrize("k", [1, 8, 14, 32])
+def test_topk_sizes(ctx, n, k):
+    check_topk(ctx, O.gen_ids(1000 + n, n), O.gen_ids(77, 150), k)
+
+
+@pytest.mark.parametrize("q", [1, 2, 127, 128, 129, 1000, 4097])
+def test_topk_batch_shapes(ctx, q):
+    check_topk(ctx, O.gen_ids(31, 20000), O.gen_ids(32, q), 8)
+
+
+def test_topk_targets_are_members(ctx):
+    ids = O.gen_ids(41, 30000)
+    check_topk(ctx, ids, ids[::997], 8)
+
+
+def test_topk_clustered_w0_ties(ctx):
+    """Many ids share their top 32 (even 64) bits with each other and with the
+    targets: exercises the full 160-bit tie path of the scan."""
+    ids = O.gen_ids(51, 40000)
+    ids[:20000, :4] = ids[0, :4]
+    ids[:5000, 4:8] = ids[0, 4:8]
+    ids[20000:30000, :3] = 0
+    tg = O.gen_ids(52, 300)
+    tg[:100, :4] = ids[0, :4]
+    tg[100:150, :8] = ids[0, :8]
+    tg[150:200, :3] = 0
+    check_topk(ctx, ids, tg, 8)
+    check_topk(ctx, ids, tg, 32)
+
+
+def test_topk_duplicates_tiebreak_by_index(ctx):
+    base = O.gen_ids(61, 3000)
+    ids = np.concatenate([base, base[::-1], base[:100]])
+    tg = np.concatenate([base[:50], O.gen_ids(62, 50)])
+    check_topk(ctx, ids, tg, 16)
+
+
+def test_topk_empty_set(ctx):
+    ctx.set_ids(np.zeros((0, 20), np.uint8))
+    idx, cnt = ctx.topk(O.gen_ids(1, 5), 8)
+    assert np.all(cnt == 0) and np.all(idx == 0xFFFFFFFF)
+
+
+def test_topk_2p24_sample(ctx):
+    """Cfg 2 set size (N = 2^24) with a target sample vs std::partial_sort(xorCmp)."""
+    n = 1 << 24
+    ctx.gen_ids(2024, n)
+    tg = O.gen_ids(2025, 48)
+    got, cnt = ctx.topk(tg, 8)
+    want, wcnt = O.topk(O.gen_ids(2024, n), tg, 8)
+    assert np.array_equal(cnt, wcnt) and np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("expired,cluster", [(0.0, False), (0.3, False), (0.6, False), (0.3, True)])
+def test_find_closest_vs_oracle(ctx, expired, cluster):
+    myid = O.gen_ids(99, 1)[0]
+    ids = O.gen_ids(100, 10000)
+    if cluster:
+        ids[:5000, :3] = myid[:3]
+    firsts, off, nodes = O.Table(myid).grow(ids).export()
+    rng = np.random.default_rng(7)
+    good = (rng.random(nodes.shape[0]) >= expired).astype(np.uint8)
+    tg = np.concatenate([O.gen_ids(101, 500), nodes[:40]])
+    for count in (1, 8, 14, 32):
+        got, cnt = ctx.find_closest(firsts, off, nodes, good, tg, count)
+        for qi in range(tg.shape[0]):
+            want = O.find_closest(firsts, off, nodes, good, tg[qi], count)
+            assert cnt[qi] == len(want), (count, qi)
+            assert list(got[qi, : cnt[qi]]) == list(want), (count, qi)
+            assert np.all(got[qi, cnt[qi]:] == 0xFFFFFFFF)
+
+
+def test_find_closest_empty_and_single_bucket(ctx):
+    tg = O.gen_ids(5, 3)
+    idx, cnt = ctx.find_closest(np.zeros((0, 20), np.uint8), np.zeros(1, np.uint32), [], [], tg, 8)
+    assert np.all(cnt == 0)
+    firsts, off, nodes = O.Table(O.gen_ids(6, 1)[0]).grow(O.gen_ids(7, 5)).export()
+    good = np.ones(nodes.shape[0], np.uint8)
+    idx, cnt = ctx.find_closest(firsts, off, nodes, good, tg, 8)
+    for qi in range(3):
+        assert list(idx[qi, : cnt[qi]]) == list(O.find_closest(firsts, off, nodes, good, tg[qi], 8))
+
+
+def test_classify_vs_oracle(ctx):
+    myid = O.gen_ids(1, 1)[0]
+    firsts, _, _ = O.Table(myid).grow(O.gen_ids(2, 20000)).export()
+    ids = O.gen_ids(3, 100003)
+    ids[:50, :6] = myid[:6]      # populate deep commonBits bins
+    ctx.set_ids(ids)
+    b, hist = ctx.classify(firsts, myid)
+    wb, wh = O.classify(firsts, myid, ids)
+    assert np.array_equal(b, wb)
+    assert np.array_equal(hist, wh)
+
+
+def test_cached_nodes_vs_oracle(ctx):
+    ids = O.gen_ids(21, 50000)
+    s = ids[np.lexsort(ids.T[::-1])]
+    rng = np.random.default_rng(3)
+    acc = (rng.random(s.shape[0]) < 0.7).astype(np.uint8)
+    ctx.set_ids(s)
+    tg = np.concatenate([O.gen_ids(22, 400), s[:10], s[-3:]])
+    for count in (1, 8, 14):
+        got, cnt = ctx.cached_nodes(tg, count, acc)
+        for qi in range(tg.shape[0]):
+            want = O.cached_nodes(s, acc, tg[qi], count)
+            assert list(got[qi, : cnt[qi]]) == list(want)
+
+
+def test_cached_nodes_requires_sorted(ctx):
+    import opendht_amd
+    ctx.set_ids(O.gen_ids(23, 100))
+    with pytest.raises(opendht_amd.DhtGpuError):
+        ctx.cached_nodes(O.gen_ids(1, 2), 8)
+
+
+def test_sharded_records_merge(ctx):
+    """K1 record mode + K3 merge over 3 shards == one flat top-k (the multi-GPU path
+    on one device)."""
+    import torch
+    import opendht_amd
+    ids = O.gen_ids(71, 30000)
+    tg = O.gen_ids(72, 500)
+    k = 8
+    dev = torch.device("cuda", 0)
+    tb = torch.from_numpy(tg.reshape(-1)).to(dev)
+    ts = 512
+    tp = torch.zeros(5 * ts, dtype=torch.int32, device=dev)
+    L = opendht_amd.lib()
+    assert L.dhtgpu_pack_dev(tb.data_ptr(), 500, tp.data_ptr(), ts, None) == 0
+    bounds = [0, 7000, 19000, 30000]
+    rec = torch.empty((3, 500, k, 6), dtype=torch.int32, device=dev)
+    shards = []
+    for s in range(3):
+        c = opendht_amd.Context(0)
+        c.set_ids(ids[bounds[s]:bounds[s + 1]])
+        c.topk_dev(tp.data_ptr(), ts, 500, k, None, None, rec[s].data_ptr(), bounds[s], c.stream)
+        torch.cuda.synchronize()
+        shards.append(c)
+    out = torch.empty((500, k), dtype=torch.int32, device=dev)
+    cnt = torch.empty(500, dtype=torch.int32, device=dev)
+    assert L.dhtgpu_merge_dev(rec.data_ptr(), 3, 500, k, tp.data_ptr(), ts, k, out.data_ptr(), cnt.data_ptr(),
+                              None) == 0
+    torch.cuda.synchronize()
+    want, wcnt = O.topk(ids, tg, k)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    assert np.array_equal(cnt.cpu().numpy().view(np.uint32), wcnt)
+    for c in shards:
+        c.close()
