@@ -32,9 +32,17 @@ import opendht_amd  # noqa: E402
 from opendht_amd import sharding  # noqa: E402
 
 METRIC = "queries/sec, k=8 XOR-NN over 16M 160-bit IDs; % HBM roofline at 1/2/4/8 GPUs"
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s
+# int32 VALU peak: a wave64 integer VALU op issues every 4 cycles per SIMD on gfx950
+# (16 lanes/clk/SIMD): 1024 SIMDs x 16 x 2.4 GHz = 39.3 T lane-ops/s; tools/valu_peak
+# measures 40.1 T on the box (profiles/r01_valu_peak.log).
+VALU_PEAK_TOPS = 1024 * 16 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
-OPS_PER_PAIR = 1.5   # K1 hot loop: v_xor_b32 per pair + v_min3_u32 per two pairs
+# Algorithmic VALU work per (id, target) pair: the XOR distance and the running-min
+# select, done two pairs at a time on packed top-16-bit words (v_xor_b32 + v_pk_min_u16
+# per two pairs) = 1 lane-op per pair.  (SURVEY 8(d)'s contract assumed 3 ops/pair on a
+# 64-bit lane; the packed prefilter is an algorithmic win, so frac here is measured
+# against the op count the kernel actually needs and cannot exceed 1.)
+OPS_PER_PAIR = 1.0
 
 
 def parse():
@@ -84,7 +92,9 @@ def main():
     ctx.gen_ids(a.seed, hi - lo, start=lo)          # this rank's contiguous slice of the global id stream
     ts = (a.q + 63) // 64 * 64
     tp = torch.empty(5 * ts, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    tstream = torch.cuda.Stream(dev)              # every kernel and event of the bench runs here
+    torch.cuda.set_stream(tstream)
+    stream = tstream.cuda_stream
     assert L.dhtgpu_gen_dev(a.seed + 1, 0, a.q, tp.data_ptr(), ts, stream) == 0
     out_idx = torch.empty((a.q, a.k), dtype=torch.int32, device=dev)
     out_cnt = torch.empty(a.q, dtype=torch.int32, device=dev)
