@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verify", type=int, default=16, help="targets re-checked against the oracle (rank 0)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the multi-GPU path (records + RCCL all-gather + K3 merge) even with one rank")
     return ap.parse_args()
 
 
@@ -81,7 +83,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    sharded = world > 1 or a.sharded
+    if sharded:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -98,15 +105,15 @@ def main():
     assert L.dhtgpu_gen_dev(a.seed + 1, 0, a.q, tp.data_ptr(), ts, stream) == 0
     out_idx = torch.empty((a.q, a.k), dtype=torch.int32, device=dev)
     out_cnt = torch.empty(a.q, dtype=torch.int32, device=dev)
-    rec = torch.empty((a.q, a.k, 6), dtype=torch.int32, device=dev) if world > 1 else None
-    gathered = torch.empty((world, a.q, a.k, 6), dtype=torch.int32, device=dev) if world > 1 else None
+    rec = torch.empty((a.q, a.k, 6), dtype=torch.int32, device=dev) if sharded else None
+    gathered = torch.empty((world * a.q, a.k, 6), dtype=torch.int32, device=dev) if sharded else None
 
     def step():
-        if world == 1:
+        if not sharded:
             ctx.topk_dev(tp.data_ptr(), ts, a.q, a.k, out_idx.data_ptr(), out_cnt.data_ptr(), None, 0, stream)
         else:
             ctx.topk_dev(tp.data_ptr(), ts, a.q, a.k, None, None, rec.data_ptr(), lo, stream)
-            dist.all_gather_into_tensor(gathered, rec)
+            sharding.gather_records(rec, out=gathered)
             rc = L.dhtgpu_merge_dev(gathered.data_ptr(), world, a.q, a.k, tp.data_ptr(), ts, a.k,
                                     out_idx.data_ptr(), out_cnt.data_ptr(), stream)
             assert rc == 0
@@ -114,7 +121,7 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if sharded:
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -124,13 +131,13 @@ def main():
         step()
     ev1.record()
     torch.cuda.synchronize()
-    if world > 1:
+    if sharded:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1) / a.steps
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
+    if sharded:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t.item())
     ms_per_step = wall * 1e3 / a.steps
@@ -138,7 +145,7 @@ def main():
     # scan-kernel-only time (the dominant kernel), measured live with HIP events on the
     # stream the kernel runs on: one extra timed batch with record output only
     kern_ms = ev_ms
-    if world > 1:
+    if sharded:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.steps):
@@ -166,7 +173,7 @@ def main():
             "data": "synthetic: splitmix64 ids and targets generated in HBM (SURVEY 8(d) spec)",
             "config": {"workload": f"cfg2 batched k-NN: {a.q} targets x {a.n} ids (2^{a.n.bit_length()-1}), k={a.k}",
                        "n_ids": a.n, "n_targets": a.q, "k": a.k,
-                       "parallelism": f"id-range shards x{world}" + (" + RCCL all-gather + K3 merge" if world > 1 else "")},
+                       "parallelism": f"id-range shards x{world}" + (" + RCCL all-gather + K3 merge" if sharded else "")},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
                          "frac": achieved / VALU_PEAK_TOPS, "traffic": None,
                          "kernel": "k_scan (K1 xor_topk_scan)", "kernel_ms": kern_ms,
@@ -176,6 +183,7 @@ def main():
         }
         # cpu_baseline (rank 0, N=1 only) + spot check of this run's output vs the oracle
         if world == 1 and not a.no_cpu:
+            # (in --sharded mode this also checks the merged output of the record path)
             cb, ids, tg, want = cpu_baseline(a.n, a.k, a.seed, max(a.cpu_targets, a.verify), a.cpu_threads)
             got = out_idx[: want.shape[0]].cpu().numpy().view(np.uint32)
             res["cpu_baseline"] = cb
@@ -183,7 +191,7 @@ def main():
             res["verified_exact"] = bool(np.array_equal(got, want))
         print(json.dumps(res), flush=True)
     ctx.close()
-    if world > 1:
+    if sharded:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -1,0 +1,201 @@
+/*
+ * dhtgpu.hpp -- C++11 host adapter over the libdhtgpu C ABI (dhtgpu.h).
+ *
+ * Drop-in helpers with the reference's signatures and result shapes
+ * (paths relative to the OpenDHT tree):
+ *
+ *   findClosestNodes(ctx, table, id, now, count)          <- RoutingTable::findClosestNodes
+ *       (include/opendht/routing_table.h:56, src/routing_table.cpp:110-150)
+ *   findClosestNodesBatch(ctx, table, targets, q, now, k)  new batched form (one launch)
+ *   getCachedNodes(ctx, map, id, count)                    <- NodeCache::getCachedNodes
+ *       (include/opendht/node_cache.h:31, src/node_cache.cpp:42-74)
+ *   ClosestIndex                                           flat exact k-NN over a fixed id
+ *       set: std::partial_sort(.., InfoHash::xorCmp) (include/opendht/infohash.h:179-194)
+ *
+ * The templates are written against the reference's member names only -- a table is a
+ * list of buckets with `.first` (InfoHash) and `.nodes` (list of Sp<Node>); a node has
+ * `.id`, `isGood(now)`, `isExpired()`, `isClient()`; an InfoHash exposes `data()` (20
+ * big-endian bytes) -- so they compile against dht::RoutingTable / NodeCache's map
+ * without including OpenDHT headers here.
+ *
+ * Behaviour: results are identical to the reference (same nodes, same order).  On a
+ * device error the helpers throw dhtgpu::Error; they never return different nodes.
+ * The caller (single dht_thread, src/dhtrunner.cpp:115-150) owns the Context.
+ */
+#ifndef DHTGPU_HPP
+#define DHTGPU_HPP
+
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "dhtgpu.h"
+
+namespace dhtgpu {
+
+class Error : public std::runtime_error {
+public:
+    Error(int code, const char* what)
+        : std::runtime_error(std::string("libdhtgpu: ") + what + ": " + dhtgpu_strerror(code)), code_(code) {}
+    int code() const { return code_; }
+private:
+    int code_;
+};
+
+inline void check(int code, const char* what) {
+    if (code != DHTGPU_OK) throw Error(code, what);
+}
+
+/* RAII owner of one device context. */
+class Context {
+public:
+    explicit Context(int device = 0) : ctx_(nullptr) { check(dhtgpu_ctx_create(device, &ctx_), "ctx_create"); }
+    ~Context() { dhtgpu_ctx_destroy(ctx_); }
+    Context(const Context&) = delete;
+    Context& operator=(const Context&) = delete;
+    dhtgpu_ctx* get() const { return ctx_; }
+private:
+    dhtgpu_ctx* ctx_;
+};
+
+namespace detail {
+template <class H>
+inline void put_id(std::vector<uint8_t>& out, const H& h) {
+    const uint8_t* p = h.data();
+    out.insert(out.end(), p, p + DHTGPU_HASH_LEN);
+}
+}  // namespace detail
+
+/* Snapshot of a RoutingTable at time `now`: bucket firsts, per-bucket node ranges,
+ * node ids, the isGood(now) mask, and the node handles to map indices back. */
+template <class Table, class TimePoint>
+struct TableSnapshot {
+    typedef typename std::decay<decltype(*std::declval<const Table&>().begin()->nodes.begin())>::type NodePtr;
+    std::vector<uint8_t> firsts, ids, good;
+    std::vector<uint32_t> off;
+    std::vector<NodePtr> nodes;
+
+    TableSnapshot(const Table& table, TimePoint now) {
+        for (const auto& b : table) {
+            detail::put_id(firsts, b.first);
+            off.push_back((uint32_t)nodes.size());
+            for (const auto& n : b.nodes) {
+                detail::put_id(ids, n->id);
+                good.push_back(n->isGood(now) ? 1 : 0);
+                nodes.push_back(n);
+            }
+        }
+        off.push_back((uint32_t)nodes.size());
+    }
+    uint32_t nbuckets() const { return (uint32_t)(firsts.size() / DHTGPU_HASH_LEN); }
+};
+
+/* RoutingTable::findClosestNodes for a batch of targets (one device launch). */
+template <class Table, class HashT, class TimePoint>
+std::vector<std::vector<typename TableSnapshot<Table, TimePoint>::NodePtr>>
+findClosestNodesBatch(Context& ctx, const Table& table, const HashT* targets, size_t q, TimePoint now,
+                      size_t count) {
+    typedef typename TableSnapshot<Table, TimePoint>::NodePtr NodePtr;
+    std::vector<std::vector<NodePtr>> res(q);
+    if (q == 0 || count == 0) return res;
+    if (count > DHTGPU_MAX_K) throw Error(DHTGPU_EINVAL, "findClosestNodes count > DHTGPU_MAX_K");
+    TableSnapshot<Table, TimePoint> snap(table, now);
+    std::vector<uint8_t> t;
+    t.reserve(q * DHTGPU_HASH_LEN);
+    for (size_t i = 0; i < q; ++i) detail::put_id(t, targets[i]);
+    std::vector<uint32_t> idx(q * count), cnt(q);
+    check(dhtgpu_find_closest(ctx.get(), snap.nbuckets(), snap.firsts.data(), snap.off.data(),
+                              snap.ids.empty() ? nullptr : snap.ids.data(),
+                              snap.good.empty() ? nullptr : snap.good.data(), t.data(), (uint32_t)q,
+                              (uint32_t)count, idx.data(), cnt.data()),
+          "find_closest");
+    for (size_t i = 0; i < q; ++i) {
+        res[i].reserve(cnt[i]);
+        for (uint32_t r = 0; r < cnt[i]; ++r) res[i].push_back(snap.nodes[idx[i * count + r]]);
+    }
+    return res;
+}
+
+/* Drop-in for RoutingTable::findClosestNodes(id, now, count). */
+template <class Table, class HashT, class TimePoint>
+std::vector<typename TableSnapshot<Table, TimePoint>::NodePtr>
+findClosestNodes(Context& ctx, const Table& table, const HashT& id, TimePoint now, size_t count = 8) {
+    return std::move(findClosestNodesBatch(ctx, table, &id, 1, now, count)[0]);
+}
+
+/* Drop-in for NodeCache::getCachedNodes over one address family's map
+ * (std::map<InfoHash, std::weak_ptr<Node>>, already lexicographically sorted).
+ * Accepted = lock() succeeds && !isExpired() && !isClient(); walk order preserved. */
+template <class NodeMap, class HashT>
+void getCachedNodesRaw(Context& ctx, const NodeMap& map, const HashT* targets, size_t q, size_t count,
+                  std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>>& locked,
+                  std::vector<std::vector<uint32_t>>& out) {
+    std::vector<uint8_t> ids, accept;
+    ids.reserve(map.size() * DHTGPU_HASH_LEN);
+    locked.clear();
+    for (const auto& kv : map) {
+        detail::put_id(ids, kv.first);
+        auto n = kv.second.lock();
+        accept.push_back(n && !n->isExpired() && !n->isClient() ? 1 : 0);
+        locked.push_back(n);
+    }
+    check(dhtgpu_set_ids(ctx.get(), ids.empty() ? nullptr : ids.data(), map.size()), "set_ids");
+    std::vector<uint8_t> t;
+    for (size_t i = 0; i < q; ++i) detail::put_id(t, targets[i]);
+    std::vector<uint32_t> idx(q * count), cnt(q);
+    out.assign(q, std::vector<uint32_t>());
+    if (q == 0) return;
+    check(dhtgpu_cached_nodes(ctx.get(), accept.empty() ? nullptr : accept.data(), t.data(), (uint32_t)q,
+                              (uint32_t)count, idx.data(), cnt.data()),
+          "cached_nodes");
+    for (size_t i = 0; i < q; ++i) out[i].assign(idx.begin() + i * count, idx.begin() + i * count + cnt[i]);
+}
+
+template <class NodeMap, class HashT>
+std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>>
+getCachedNodes(Context& ctx, const NodeMap& map, const HashT& id, size_t count) {
+    std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>> locked, res;
+    std::vector<std::vector<uint32_t>> out;
+    getCachedNodesRaw(ctx, map, &id, 1, count, locked, out);
+    for (uint32_t i : out[0]) res.push_back(locked[i]);
+    return res;
+}
+
+/* Flat exact k-NN over a fixed id set kept resident in HBM (the batched
+ * findClosestNodesBatch(targets[], k) of the north star): upload once, query many. */
+class ClosestIndex {
+public:
+    explicit ClosestIndex(Context& ctx) : ctx_(ctx) {}
+    template <class HashT>
+    void assign(const HashT* ids, size_t n) {
+        std::vector<uint8_t> b;
+        b.reserve(n * DHTGPU_HASH_LEN);
+        for (size_t i = 0; i < n; ++i) detail::put_id(b, ids[i]);
+        check(dhtgpu_set_ids(ctx_.get(), b.empty() ? nullptr : b.data(), n), "set_ids");
+    }
+    /* out[i] = indices of the k ids closest to targets[i], ascending by XOR distance */
+    template <class HashT>
+    std::vector<std::vector<uint32_t>> query(const HashT* targets, size_t q, size_t k) const {
+        std::vector<uint8_t> t;
+        t.reserve(q * DHTGPU_HASH_LEN);
+        for (size_t i = 0; i < q; ++i) detail::put_id(t, targets[i]);
+        std::vector<uint32_t> idx(q * k), cnt(q);
+        std::vector<std::vector<uint32_t>> res(q);
+        if (q == 0) return res;
+        check(dhtgpu_topk(ctx_.get(), t.data(), (uint32_t)q, (uint32_t)k, idx.data(), cnt.data()), "topk");
+        for (size_t i = 0; i < q; ++i) res[i].assign(idx.begin() + i * k, idx.begin() + i * k + cnt[i]);
+        return res;
+    }
+private:
+    Context& ctx_;
+};
+
+}  // namespace dhtgpu
+
+#endif /* DHTGPU_HPP */

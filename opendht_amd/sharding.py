@@ -19,12 +19,15 @@ def shard_range(n, world, rank):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def gather_records(rec, group=None):
-    """All-gather this rank's (q, k, 6) int32 candidate records -> (world, q, k, 6)."""
+def gather_records(rec, group=None, out=None):
+    """All-gather this rank's (q, k, 6) int32 candidate records -> (world, q, k, 6).
+    `out` may be a preallocated (world*q, k, 6) buffer (the concatenated form every
+    backend accepts); list l of the result is rank l's shard."""
     world = dist.get_world_size(group)
-    out = torch.empty((world,) + tuple(rec.shape), dtype=rec.dtype, device=rec.device)
+    if out is None:
+        out = torch.empty((world * rec.shape[0],) + tuple(rec.shape[1:]), dtype=rec.dtype, device=rec.device)
     dist.all_gather_into_tensor(out, rec.contiguous(), group=group)
-    return out
+    return out.view((world,) + tuple(rec.shape))
 
 
 def sharded_topk(local_records, merge, group=None):

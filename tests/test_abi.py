@@ -45,7 +45,16 @@ def test_cpp_adapter_header_compiles(tmp_path):
     src = os.path.join(ROOT, "tests", "cpp", "adapter_check.cpp")
     if not os.path.exists(src):
         pytest.skip("adapter check source absent")
-    exe = tmp_path / "adapter_check"
-    subprocess.check_call(["g++", "-std=c++11", "-Wall", "-Wextra", "-I", os.path.join(ROOT, "include"),
-                           src, "-o", str(exe), "-L", os.path.dirname(opendht_amd.LIB_PATH), "-ldhtgpu",
-                           "-Wl,-rpath," + os.path.dirname(opendht_amd.LIB_PATH)])
+    exe = build_adapter_check(str(tmp_path / "adapter_check"))
+    assert subprocess.check_output([exe], text=True).strip() == "built"
+
+
+def build_adapter_check(exe):
+    src = os.path.join(ROOT, "tests", "cpp", "adapter_check.cpp")
+    libdir = os.path.dirname(opendht_amd.LIB_PATH)
+    odir = os.path.join(ROOT, "oracle")
+    subprocess.check_call(["make", "-s", "-C", odir])
+    subprocess.check_call(["g++", "-std=c++11", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                           src, "-o", exe, "-L", libdir, "-ldhtgpu", "-L", odir, "-loracle",
+                           "-Wl,-rpath," + libdir, "-Wl,-rpath," + odir])
+    return exe

@@ -188,3 +188,14 @@ def test_sharded_records_merge(ctx):
     assert np.array_equal(cnt.cpu().numpy().view(np.uint32), wcnt)
     for c in shards:
         c.close()
+
+
+def test_cpp_adapter_on_gpu(tmp_path):
+    """The C++11 drop-in adapter (include/dhtgpu.hpp) over reference-shaped types returns
+    the same nodes, in the same order, as the oracle restatements."""
+    import subprocess
+    from test_abi import build_adapter_check
+    exe = build_adapter_check(str(tmp_path / "adapter_check"))
+    out = subprocess.run([exe, "--run"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "0 mismatches" in out.stdout
