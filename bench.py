@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verify", type=int, default=16, help="targets re-checked against the oracle (rank 0)")
+    ap.add_argument("--algo", choices=["index", "scan"], default="index",
+                    help="index: K4 bucket-index build + K5 trie-descent query, rebuilt inside every step; "
+                         "scan: K1 brute-force streaming scan")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU path (records + RCCL all-gather + K3 merge) even with one rank")
     return ap.parse_args()
@@ -108,11 +111,18 @@ def main():
     rec = torch.empty((a.q, a.k, 6), dtype=torch.int32, device=dev) if sharded else None
     gathered = torch.empty((world * a.q, a.k, 6), dtype=torch.int32, device=dev) if sharded else None
 
+    def local(out_i, out_c, out_r, base):
+        if a.algo == "index":
+            ctx.index_build(stream)          # the index is rebuilt from the raw id planes every step
+            ctx.index_topk_dev(tp.data_ptr(), ts, a.q, a.k, out_i, out_c, out_r, base, stream)
+        else:
+            ctx.topk_dev(tp.data_ptr(), ts, a.q, a.k, out_i, out_c, out_r, base, stream)
+
     def step():
         if not sharded:
-            ctx.topk_dev(tp.data_ptr(), ts, a.q, a.k, out_idx.data_ptr(), out_cnt.data_ptr(), None, 0, stream)
+            local(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0)
         else:
-            ctx.topk_dev(tp.data_ptr(), ts, a.q, a.k, None, None, rec.data_ptr(), lo, stream)
+            local(None, None, rec.data_ptr(), lo)
             sharding.gather_records(rec, out=gathered)
             rc = L.dhtgpu_merge_dev(gathered.data_ptr(), world, a.q, a.k, tp.data_ptr(), ts, a.k,
                                     out_idx.data_ptr(), out_cnt.data_ptr(), stream)
@@ -149,7 +159,7 @@ def main():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.steps):
-            ctx.topk_dev(tp.data_ptr(), ts, a.q, a.k, None, None, rec.data_ptr(), lo, stream)
+            local(None, None, rec.data_ptr(), lo)
         e1.record()
         torch.cuda.synchronize()
         kern_ms = e0.elapsed_time(e1) / a.steps

@@ -102,6 +102,21 @@ int dhtgpu_pack_dev(const uint8_t* ids20_be, uint64_t n, uint32_t* planes, uint6
 int dhtgpu_gen_dev(uint64_t seed, uint64_t start, uint64_t n, uint32_t* planes, uint64_t stride,
                    void* stream);
 
+/* ---- K4/K5: bucket index + trie-descent exact top-k (same results as dhtgpu_topk) ---- */
+/* Build (or rebuild) the index over the context's id set: a counting sort of the ids by
+ * their top B = clamp(log2(n) - 4, 1, 24) bits into 32-byte records plus a 2^B + 1 entry
+ * prefix directory.  Stream-ordered (NULL = the context stream); no host sync. */
+int dhtgpu_index_build(dhtgpu_ctx* ctx, void* stream);
+/* Exact top-k via the index: identical output to dhtgpu_topk_dev -- final indices +
+ * counts, or (out_rec != NULL) candidate records for dhtgpu_merge_dev; idx offset by
+ * idx_base.  Needs a built index (DHTGPU_ENOIDS otherwise). */
+int dhtgpu_index_topk_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
+                          uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec,
+                          uint32_t idx_base, void* stream);
+/* Host form: builds the index if the id set changed since the last build, then queries. */
+int dhtgpu_index_topk(dhtgpu_ctx* ctx, const uint8_t* targets20_be, uint32_t q, uint32_t k,
+                      uint32_t* out_idx, uint32_t* out_cnt);
+
 /* ---- K1r: RoutingTable::findClosestNodes over a table snapshot ------------------ */
 /* Snapshot: nb buckets in list order with firsts20[nb*20] (Bucket::first),
  * bucket_off[nb+1] (bucket b owns nodes [off[b], off[b+1]) of node_ids20), and

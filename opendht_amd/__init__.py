@@ -80,6 +80,10 @@ def lib():
                                  _vp], ctypes.c_int),
         "dhtgpu_cached_nodes": ([_vp, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p],
                                 ctypes.c_int),
+        "dhtgpu_index_build": ([_vp, _vp], ctypes.c_int),
+        "dhtgpu_index_topk_dev": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp,
+                                   ctypes.c_uint32, _vp], ctypes.c_int),
+        "dhtgpu_index_topk": ([_vp, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -95,7 +99,7 @@ def exported_symbols():
             "dhtgpu_ctx_stream", "dhtgpu_set_ids", "dhtgpu_gen_ids", "dhtgpu_num_ids", "dhtgpu_get_ids",
             "dhtgpu_ids_dev", "dhtgpu_topk", "dhtgpu_topk_dev", "dhtgpu_merge_dev", "dhtgpu_pack_dev",
             "dhtgpu_gen_dev", "dhtgpu_find_closest", "dhtgpu_classify", "dhtgpu_classify_dev",
-            "dhtgpu_cached_nodes"]
+            "dhtgpu_cached_nodes", "dhtgpu_index_build", "dhtgpu_index_topk_dev", "dhtgpu_index_topk"]
 
 
 def _ids(a, name="ids"):
@@ -179,6 +183,23 @@ class Context:
         cnt = np.empty(q, dtype=np.uint32)
         _check(lib().dhtgpu_topk(self._h, _p(t, _u8p), q, k, _p(out, _u32p), _p(cnt, _u32p)), "topk")
         return out, cnt
+
+    def index_topk(self, targets, k=8):
+        """Same result as topk() through the K4/K5 bucket index (built on first use)."""
+        t = _ids(targets, "targets")
+        q = t.shape[0]
+        out = np.empty((q, k), dtype=np.uint32)
+        cnt = np.empty(q, dtype=np.uint32)
+        _check(lib().dhtgpu_index_topk(self._h, _p(t, _u8p), q, k, _p(out, _u32p), _p(cnt, _u32p)), "index_topk")
+        return out, cnt
+
+    def index_build(self, stream=None):
+        _check(lib().dhtgpu_index_build(self._h, stream), "index_build")
+
+    def index_topk_dev(self, t_planes_ptr, t_stride, q, k, out_idx_ptr=None, out_cnt_ptr=None, out_rec_ptr=None,
+                       idx_base=0, stream=None):
+        _check(lib().dhtgpu_index_topk_dev(self._h, t_planes_ptr, t_stride, q, k, out_idx_ptr, out_cnt_ptr,
+                                           out_rec_ptr, idx_base, stream), "index_topk_dev")
 
     def topk_dev(self, t_planes_ptr, t_stride, q, k, out_idx_ptr=None, out_cnt_ptr=None, out_rec_ptr=None,
                  idx_base=0, stream=None):

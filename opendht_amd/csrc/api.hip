@@ -63,6 +63,9 @@ struct dhtgpu_ctx {
     DevBuf targets;         // 5 * tstride u32
     DevBuf out_idx, out_cnt, rec, aux, aux2, aux3;
     bool has_ids = false;
+    DevBuf index;           // K4 workspace: records | directory | cursor | block sums
+    uint32_t index_B = 0;
+    bool index_valid = false;
 
     hipError_t bind() { return hipSetDevice(device); }
 
@@ -129,7 +132,7 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
     (void)c->bind();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->planes, &c->staging, &c->targets, &c->out_idx, &c->out_cnt, &c->rec,
-                      &c->aux, &c->aux2, &c->aux3})
+                      &c->aux, &c->aux2, &c->aux3, &c->index})
         b->release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -159,6 +162,7 @@ static int finish_ids(dhtgpu_ctx* c, uint64_t n) {
 static int alloc_ids(dhtgpu_ctx* c, uint64_t n) {
     if (n >= 0xFFFFFFFFull) return DHTGPU_ERANGE;
     c->has_ids = false;
+    c->index_valid = false;
     c->stride = pad_ids(n ? n : 1);
     DHT_TRY(c->planes.ensure((size_t)c->stride * 5 * 4));
     return DHTGPU_OK;
@@ -282,6 +286,65 @@ int dhtgpu_topk(dhtgpu_ctx* c, const uint8_t* t20, uint32_t q, uint32_t k, uint3
     DHT_TRY(c->aux3.ensure((size_t)q * 4));
     int r = dhtgpu_topk_dev(c, c->targets.as<uint32_t>(), ts, q, k, c->aux2.as<uint32_t>(),
                             c->aux3.as<uint32_t>(), nullptr, 0, c->stream);
+    if (r) return r;
+    DHT_TRY(hipMemcpyAsync(out_idx, c->aux2.p, (size_t)q * k * 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(out_cnt, c->aux3.p, (size_t)q * 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_index_build(dhtgpu_ctx* c, void* stream) {
+    if (!c) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    DHT_TRY(c->bind());
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const uint32_t B = index_bits(c->n);
+    DHT_TRY(c->index.ensure(index_bytes(c->n, B)));
+    DHT_TRY(launch_index_build(c->planes.as<uint32_t>(), c->stride, c->n, B, c->index.p, s));
+    c->index_B = B;
+    c->index_valid = true;
+    return DHTGPU_OK;
+}
+
+int dhtgpu_index_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k,
+                          uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base,
+                          void* stream) {
+    if (!c || k == 0 || k > DHTGPU_MAX_K || (q && !tp)) return DHTGPU_EINVAL;
+    if (!out_rec && (!out_idx || !out_cnt)) return DHTGPU_EINVAL;
+    if (!c->has_ids || !c->index_valid) return DHTGPU_ENOIDS;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (out_rec) {   // candidate records for a cross-shard merge
+        DHT_TRY(c->out_idx.ensure((size_t)q * k * 4));
+        DHT_TRY(c->out_cnt.ensure((size_t)q * 4));
+        DHT_TRY(launch_index_query(c->index.p, c->n, c->index_B, tp, ts, q, k, c->out_idx.as<uint32_t>(),
+                                   c->out_cnt.as<uint32_t>(), s));
+        DHT_TRY(launch_rec_from_idx(c->out_idx.as<uint32_t>(), (uint64_t)q * k, c->planes.as<uint32_t>(),
+                                    c->stride, idx_base, out_rec, s));
+        return DHTGPU_OK;
+    }
+    DHT_TRY(launch_index_query(c->index.p, c->n, c->index_B, tp, ts, q, k, out_idx, out_cnt, s));
+    if (idx_base) DHT_TRY(launch_add_base(out_idx, (uint64_t)q * k, idx_base, s));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_index_topk(dhtgpu_ctx* c, const uint8_t* t20, uint32_t q, uint32_t k, uint32_t* out_idx,
+                      uint32_t* out_cnt) {
+    if (!c || k == 0 || k > DHTGPU_MAX_K || (q && (!t20 || !out_idx || !out_cnt))) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    if (!c->index_valid) {
+        int r = dhtgpu_index_build(c, c->stream);
+        if (r) return r;
+    }
+    uint64_t ts = 0;
+    DHT_TRY(c->upload_targets(t20, q, &ts));
+    DHT_TRY(c->aux2.ensure((size_t)q * k * 4));
+    DHT_TRY(c->aux3.ensure((size_t)q * 4));
+    int r = dhtgpu_index_topk_dev(c, c->targets.as<uint32_t>(), ts, q, k, c->aux2.as<uint32_t>(),
+                                  c->aux3.as<uint32_t>(), nullptr, 0, c->stream);
     if (r) return r;
     DHT_TRY(hipMemcpyAsync(out_idx, c->aux2.p, (size_t)q * k * 4, hipMemcpyDeviceToHost, c->stream));
     DHT_TRY(hipMemcpyAsync(out_cnt, c->aux3.p, (size_t)q * 4, hipMemcpyDeviceToHost, c->stream));

@@ -17,12 +17,14 @@ def ctx():
 
 
 def check_topk(ctx, ids, targets, k):
+    """K1 (scan) and K4/K5 (bucket index) both bit-exact vs std::partial_sort(xorCmp)."""
     ctx.set_ids(ids)
-    got, gcnt = ctx.topk(targets, k)
     want, wcnt = O.topk(ids, targets, k)
-    assert np.array_equal(gcnt, wcnt)
-    bad = np.nonzero((got != want).any(axis=1))[0]
-    assert bad.size == 0, f"{bad.size} mismatching targets, first {bad[:5]}: got {got[bad[0]]} want {want[bad[0]]}"
+    for name, fn in (("scan", ctx.topk), ("index", ctx.index_topk)):
+        got, gcnt = fn(targets, k)
+        assert np.array_equal(gcnt, wcnt), name
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, f"{name}: {bad.size} mismatching targets, first {bad[:5]}: got {got[bad[0]]} want {want[bad[0]]}"
 
 
 def test_gen_matches_oracle(ctx):
@@ -69,6 +71,24 @@ def test_topk_clustered_w0_ties(ctx):
     check_topk(ctx, ids, tg, 32)
 
 
+def test_index_adversarial_clusters(ctx):
+    """Huge buckets (tens of thousands of ids sharing 40+ leading bits), a lone far id,
+    targets inside/outside the clusters: exercises the index's take-child-and-descend
+    iteration and its large-range selection."""
+    ids = O.gen_ids(81, 60000)
+    ids[:30000, :5] = 0x5A            # one big cluster (40 shared bits)
+    ids[30000:45000, :3] = 0x00       # a second, 24-bit cluster
+    ids[45000:45003, :6] = 0x5A       # 3 ids deeper inside the first cluster
+    tg = O.gen_ids(82, 400)
+    tg[:100, :5] = 0x5A
+    tg[100:150, :7] = 0x5A
+    tg[150:200, :2] = 0x00
+    tg[200:220, 0] = 0x5B
+    check_topk(ctx, ids, tg, 8)
+    check_topk(ctx, ids, tg, 32)
+    check_topk(ctx, ids[:5], tg, 8)
+
+
 def test_topk_duplicates_tiebreak_by_index(ctx):
     base = O.gen_ids(61, 3000)
     ids = np.concatenate([base, base[::-1], base[:100]])
@@ -87,9 +107,21 @@ def test_topk_2p24_sample(ctx):
     n = 1 << 24
     ctx.gen_ids(2024, n)
     tg = O.gen_ids(2025, 48)
-    got, cnt = ctx.topk(tg, 8)
     want, wcnt = O.topk(O.gen_ids(2024, n), tg, 8)
-    assert np.array_equal(cnt, wcnt) and np.array_equal(got, want)
+    for fn in (ctx.topk, ctx.index_topk):
+        got, cnt = fn(tg, 8)
+        assert np.array_equal(cnt, wcnt) and np.array_equal(got, want)
+
+
+def test_index_vs_scan_full_batch(ctx):
+    """Full cfg-2 batch (65,536 targets x 2^24 ids): the two independent GPU algorithms
+    agree on every target (a size-independent cross-check; the oracle covers samples)."""
+    ctx.gen_ids(2024, 1 << 24)
+    tg = O.gen_ids(2025, 65536)
+    a, ca = ctx.topk(tg, 8)
+    b, cb = ctx.index_topk(tg, 8)
+    assert np.array_equal(ca, cb) and np.array_equal(a, b)
+    assert np.all(ca == 8)
 
 
 @pytest.mark.parametrize("expired,cluster", [(0.0, False), (0.3, False), (0.6, False), (0.3, True)])

@@ -1,0 +1,5 @@
+set -o pipefail
+OUT=gpurun_out/r01f; mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 --algo index > $OUT/bench_index.log 2>&1 && tail -1 $OUT/bench_index.log | cut -c1-400 &&
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu --algo index > $OUT/kt.log 2>&1 && echo kt-ok
