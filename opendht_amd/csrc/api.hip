@@ -318,13 +318,13 @@ int dhtgpu_index_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     if (out_rec) {   // candidate records for a cross-shard merge
         DHT_TRY(c->out_idx.ensure((size_t)q * k * 4));
         DHT_TRY(c->out_cnt.ensure((size_t)q * 4));
-        DHT_TRY(launch_index_query(c->index.p, c->n, c->index_B, tp, ts, q, k, c->out_idx.as<uint32_t>(),
+        DHT_TRY(launch_index_query(c->index.p, c->n, c->index_B, c->planes.as<uint32_t>(), c->stride, tp, ts, q, k, c->out_idx.as<uint32_t>(),
                                    c->out_cnt.as<uint32_t>(), s));
         DHT_TRY(launch_rec_from_idx(c->out_idx.as<uint32_t>(), (uint64_t)q * k, c->planes.as<uint32_t>(),
                                     c->stride, idx_base, out_rec, s));
         return DHTGPU_OK;
     }
-    DHT_TRY(launch_index_query(c->index.p, c->n, c->index_B, tp, ts, q, k, out_idx, out_cnt, s));
+    DHT_TRY(launch_index_query(c->index.p, c->n, c->index_B, c->planes.as<uint32_t>(), c->stride, tp, ts, q, k, out_idx, out_cnt, s));
     if (idx_base) DHT_TRY(launch_add_base(out_idx, (uint64_t)q * k, idx_base, s));
     return DHTGPU_OK;
 }
