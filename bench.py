@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--algo", choices=["index", "scan"], default="index",
                     help="index: K4 bucket-index build + K5 trie-descent query, rebuilt inside every step; "
                          "scan: K1 brute-force streaming scan")
+    ap.add_argument("--no-scan", action="store_true", help="skip the reference K1 scan measurement (index algo)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU path (records + RCCL all-gather + K3 merge) even with one rank")
     return ap.parse_args()
@@ -152,22 +153,62 @@ def main():
     wall = float(t.item())
     ms_per_step = wall * 1e3 / a.steps
 
-    # scan-kernel-only time (the dominant kernel), measured live with HIP events on the
-    # stream the kernel runs on: one extra timed batch with record output only
-    kern_ms = ev_ms
-    if sharded:
+    n_local = hi - lo
+
+    def ev_time(fn, reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(a.steps):
-            local(None, None, rec.data_ptr(), lo)
+        for _ in range(reps):
+            fn()
         e1.record()
         torch.cuda.synchronize()
-        kern_ms = e0.elapsed_time(e1) / a.steps
+        return e0.elapsed_time(e1) / reps
 
-    if rank == 0:
-        n_local = hi - lo
+    reps = max(3, min(a.steps, 20))
+    if a.algo == "index":
+        # per-kernel device times of the index build (HIP events between its kernels, on
+        # the bench stream) and of the query kernel alone
+        phases = [ctx.index_build_timed(stream) for _ in range(reps)]
+        ph = [sum(p[i] for p in phases) / reps for i in range(4)]
+        q_ms = ev_time(lambda: ctx.index_topk_dev(tp.data_ptr(), ts, a.q, a.k, out_idx.data_ptr(),
+                                                  out_cnt.data_ptr(), None, 0, stream), reps)
+        kern = {"k_p0_hist": (ph[0], 4 * n_local), "k_p0_scans": (ph[1], 0),
+                "k_p1_scatter": (ph[2], 12 * n_local), "k_p2_buckets": (ph[3], 16 * n_local),
+                "k_query": (q_ms, a.q * (20 + a.k * 4))}
+        dom = max(kern, key=lambda k: kern[k][0])
+        dom_ms, dom_bytes = kern[dom]
+        step_bytes = n_local * (4 + 8) + a.q * (20 + a.k * 4)
+        roof = {"bound": "hbm", "achieved": dom_bytes / (dom_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                "kernel": dom, "kernel_ms": dom_ms, "alg_bytes_per_launch": dom_bytes,
+                "kernels_ms": {k: v[0] for k, v in kern.items()},
+                "step_alg_bytes": step_bytes,
+                "step_hbm_frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        extra = {"query_only_qps": a.q / (q_ms * 1e-3), "index_build_ms": sum(ph)}
+    else:
+        kern_ms = ev_ms
+        if sharded:
+            kern_ms = ev_time(lambda: local(None, None, rec.data_ptr(), lo), reps)
         pairs = a.q * n_local
         achieved = OPS_PER_PAIR * pairs / (kern_ms * 1e-3) / 1e12
+        roof = {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
+                "frac": achieved / VALU_PEAK_TOPS, "traffic": None,
+                "kernel": "k_scan (K1 xor_topk_scan)", "kernel_ms": kern_ms,
+                "ops_per_pair": OPS_PER_PAIR, "pairs_per_launch": pairs,
+                "hbm_alg_bytes_per_launch": n_local * 20 + a.q * 20 + a.q * a.k * 4}
+        extra = {}
+    if a.algo == "index" and not a.no_scan and not sharded:
+        # the north-star brute-force scan (K1) on the same inputs, for reference
+        sc_ms = ev_time(lambda: ctx.topk_dev(tp.data_ptr(), ts, a.q, a.k, out_idx.data_ptr(), out_cnt.data_ptr(),
+                                             None, 0, stream), 3)
+        ach = OPS_PER_PAIR * a.q * n_local / (sc_ms * 1e-3) / 1e12
+        extra["scan_k1"] = {"qps": a.q / (sc_ms * 1e-3), "kernel_ms": sc_ms, "bound": "valu",
+                            "achieved_TOPs": ach, "peak_TOPs": VALU_PEAK_TOPS, "frac": ach / VALU_PEAK_TOPS}
+        # restore the index-path output for the verification below
+        step()
+        torch.cuda.synchronize()
+
+    if rank == 0:
         res = {
             "metric": METRIC,
             "value": a.q / (ms_per_step * 1e-3),
@@ -182,15 +223,11 @@ def main():
             "dtype": "u32",
             "data": "synthetic: splitmix64 ids and targets generated in HBM (SURVEY 8(d) spec)",
             "config": {"workload": f"cfg2 batched k-NN: {a.q} targets x {a.n} ids (2^{a.n.bit_length()-1}), k={a.k}",
-                       "n_ids": a.n, "n_targets": a.q, "k": a.k,
+                       "n_ids": a.n, "n_targets": a.q, "k": a.k, "algo": a.algo,
                        "parallelism": f"id-range shards x{world}" + (" + RCCL all-gather + K3 merge" if sharded else "")},
-            "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
-                         "frac": achieved / VALU_PEAK_TOPS, "traffic": None,
-                         "kernel": "k_scan (K1 xor_topk_scan)", "kernel_ms": kern_ms,
-                         "ops_per_pair": OPS_PER_PAIR, "pairs_per_launch": pairs,
-                         "hbm_alg_bytes_per_launch": n_local * 20 + a.q * 20 + a.q * a.k * 4,
-                         "hbm_frac": (n_local * 20 + a.q * 20 + a.q * a.k * 4) / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+            "roofline": roof,
         }
+        res.update(extra)
         # cpu_baseline (rank 0, N=1 only) + spot check of this run's output vs the oracle
         if world == 1 and not a.no_cpu:
             # (in --sharded mode this also checks the merged output of the record path)

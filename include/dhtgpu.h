@@ -107,6 +107,10 @@ int dhtgpu_gen_dev(uint64_t seed, uint64_t start, uint64_t n, uint32_t* planes, 
  * their top B = clamp(log2(n) - 4, 1, 24) bits into 32-byte records plus a 2^B + 1 entry
  * prefix directory.  Stream-ordered (NULL = the context stream); no host sync. */
 int dhtgpu_index_build(dhtgpu_ctx* ctx, void* stream);
+/* Diagnostics: the same build with HIP events between its kernels; synchronises and
+ * returns per-phase device milliseconds ms4 = {P0 histogram, P0 scans, P1 partition
+ * scatter, P2 bucket gather}. */
+int dhtgpu_index_build_timed(dhtgpu_ctx* ctx, void* stream, float* ms4);
 /* Exact top-k via the index: identical output to dhtgpu_topk_dev -- final indices +
  * counts, or (out_rec != NULL) candidate records for dhtgpu_merge_dev; idx offset by
  * idx_base.  Needs a built index (DHTGPU_ENOIDS otherwise). */

@@ -84,6 +84,7 @@ def lib():
         "dhtgpu_index_topk_dev": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp,
                                    ctypes.c_uint32, _vp], ctypes.c_int),
         "dhtgpu_index_topk": ([_vp, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p], ctypes.c_int),
+        "dhtgpu_index_build_timed": ([_vp, _vp, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -99,7 +100,8 @@ def exported_symbols():
             "dhtgpu_ctx_stream", "dhtgpu_set_ids", "dhtgpu_gen_ids", "dhtgpu_num_ids", "dhtgpu_get_ids",
             "dhtgpu_ids_dev", "dhtgpu_topk", "dhtgpu_topk_dev", "dhtgpu_merge_dev", "dhtgpu_pack_dev",
             "dhtgpu_gen_dev", "dhtgpu_find_closest", "dhtgpu_classify", "dhtgpu_classify_dev",
-            "dhtgpu_cached_nodes", "dhtgpu_index_build", "dhtgpu_index_topk_dev", "dhtgpu_index_topk"]
+            "dhtgpu_cached_nodes", "dhtgpu_index_build", "dhtgpu_index_topk_dev", "dhtgpu_index_topk",
+            "dhtgpu_index_build_timed"]
 
 
 def _ids(a, name="ids"):
@@ -195,6 +197,13 @@ class Context:
 
     def index_build(self, stream=None):
         _check(lib().dhtgpu_index_build(self._h, stream), "index_build")
+
+    def index_build_timed(self, stream=None):
+        """Build with HIP events between kernels; returns device ms per phase:
+        (P0 histogram, P0 scans, P1 partition scatter, P2 bucket gather)."""
+        ms = (ctypes.c_float * 4)()
+        _check(lib().dhtgpu_index_build_timed(self._h, stream, ms), "index_build_timed")
+        return tuple(ms)
 
     def index_topk_dev(self, t_planes_ptr, t_stride, q, k, out_idx_ptr=None, out_cnt_ptr=None, out_rec_ptr=None,
                        idx_base=0, stream=None):

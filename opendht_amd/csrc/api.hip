@@ -306,6 +306,25 @@ int dhtgpu_index_build(dhtgpu_ctx* c, void* stream) {
     return DHTGPU_OK;
 }
 
+int dhtgpu_index_build_timed(dhtgpu_ctx* c, void* stream, float* ms4) {
+    if (!c || !ms4) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    DHT_TRY(c->bind());
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const uint32_t B = index_bits(c->n);
+    DHT_TRY(c->index.ensure(index_bytes(c->n, B)));
+    hipEvent_t ev[5];
+    for (int i = 0; i < 5; ++i) DHT_TRY(hipEventCreate(&ev[i]));
+    hipError_t e = launch_index_build(c->planes.as<uint32_t>(), c->stride, c->n, B, c->index.p, s, ev);
+    if (e == hipSuccess) e = hipEventSynchronize(ev[4]);
+    for (int i = 0; e == hipSuccess && i < 4; ++i) e = hipEventElapsedTime(&ms4[i], ev[i], ev[i + 1]);
+    for (int i = 0; i < 5; ++i) (void)hipEventDestroy(ev[i]);
+    DHT_TRY(e);
+    c->index_B = B;
+    c->index_valid = true;
+    return DHTGPU_OK;
+}
+
 int dhtgpu_index_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k,
                           uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base,
                           void* stream) {

@@ -63,8 +63,9 @@ hipError_t launch_cached(const uint32_t* planes, uint64_t stride, uint64_t n,
 // index.hip: K4 bucket index (counting sort by the top B bits) + K5 trie-descent k-NN
 uint32_t index_bits(uint64_t n);
 size_t index_bytes(uint64_t n, uint32_t B);
+// ev (nullable): 5 events recorded before/between/after the build's kernels
 hipError_t launch_index_build(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t B, void* ws,
-                              hipStream_t s);
+                              hipStream_t s, hipEvent_t* ev = nullptr);
 hipError_t launch_index_query(const void* ws, uint64_t n, uint32_t B, const uint32_t* planes, uint64_t stride,
                               const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k, uint32_t* out_idx,
                               uint32_t* out_cnt, hipStream_t s);

@@ -356,7 +356,7 @@ static void index_layout(void* ws, uint64_t n, uint32_t B, uint2*& pairs, uint32
 }
 
 hipError_t launch_index_build(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t B, void* ws,
-                              hipStream_t s) {
+                              hipStream_t s, hipEvent_t* ev) {
     (void)stride;
     uint32_t b1, b2;
     index_split(n, B, b1, b2);
@@ -374,21 +374,27 @@ hipError_t launch_index_build(const uint32_t* planes, uint64_t stride, uint64_t 
         (void)hipFuncSetAttribute((const void*)k_p2_buckets, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
         attr_set = true;
     }
+    if (ev) (void)hipEventRecord(ev[0], s);
     if (n) {
         k_p0_hist<<<nblk, kBlk, np * 4, s>>>(planes, n, b1, nblk, H);
+        if (ev) (void)hipEventRecord(ev[1], s);
         k_p0_rowscan<<<(uint32_t)np, 1024, 0, s>>>(H, nblk, pcount);
     } else {
+        if (ev) (void)hipEventRecord(ev[1], s);
         hipError_t e = hipMemsetAsync(pcount, 0, np * 4, s);
         if (e != hipSuccess) return e;
     }
     k_p0_scan<<<1, 1024, 0, s>>>(pcount, (uint32_t)np, pstart, n);
+    if (ev) (void)hipEventRecord(ev[2], s);
     if (n) k_p1_scatter<<<nblk, kBlk, np * 8, s>>>(planes, n, b1, nblk, H, pstart, tmp);
+    if (ev) (void)hipEventRecord(ev[3], s);
     // LDS: fixed part + a permutation sized ~3x the average partition (cap: 160 KB)
     const uint32_t fixed = ((2u << b2) + 1024) * 4;
     uint64_t cap = 3 * ((n >> b1) + 1) + 1024;
     if (cap > (kLdsMax - fixed) / 4) cap = (kLdsMax - fixed) / 4;
     k_p2_buckets<<<(uint32_t)np, kP2Blk, fixed + (uint32_t)cap * 4, s>>>(tmp, pstart, b1, b2, (uint32_t)cap, dir,
                                                                         pairs, n);
+    if (ev) (void)hipEventRecord(ev[4], s);
     return hipGetLastError();
 }
 
