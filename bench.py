@@ -6,16 +6,24 @@ node ids, k = 8, exact (bit-identical to std::partial_sort over InfoHash::xorCmp
 One step = one batched lookup of all targets against the whole id set.  Ids and
 targets are generated in HBM before timing (synthetic splitmix64 stream).
 
-Multi-GPU (one process per GPU, torch.distributed over RCCL): the id set is range-
-sharded across ranks; every rank scans its shard for all targets (K1, record mode),
-the per-rank candidate lists (q x k x 24 B) are exchanged with one RCCL all-gather over
-xGMI, and K3 merges them into the exact global top-k.  Total work is fixed as N grows
-("scaling": "strong").
+Algorithms (--algo):
+  index  K4 bucket-index build + K5 trie-descent query; the index is REBUILT from the raw
+         id planes inside every timed step (default)
+  scan   K1 brute-force streaming scan (the north-star kernel design)
+
+Multi-GPU (one process per GPU, torch.distributed over RCCL; --route):
+  prefix     (default for a power-of-two world) ids AND targets are partitioned by their
+             top log2(N) bits; each rank answers only its own targets from its own shard.
+             If every shard holds >= k ids, a target's top-k provably lies in its own
+             prefix subtree, so the data path needs no collective; the setup checks the
+             minimum shard size with one all-reduce and refuses otherwise.
+  broadcast  ids range-sharded, all targets on every rank, per-rank candidate records
+             exchanged by one RCCL all-gather, merged by K3 (SURVEY §8(e) north-star scheme).
+Total work is fixed as N grows ("scaling": "strong").
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
-import ctypes
 import json
 import os
 import sys
@@ -37,7 +45,7 @@ METRIC = "queries/sec, k=8 XOR-NN over 16M 160-bit IDs; % HBM roofline at 1/2/4/
 # measures 40.1 T on the box (profiles/r01_valu_peak.log).
 VALU_PEAK_TOPS = 1024 * 16 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
-# Algorithmic VALU work per (id, target) pair: the XOR distance and the running-min
+# Algorithmic VALU work per (id, target) pair in K1: the XOR distance and the running-min
 # select, done two pairs at a time on packed top-16-bit words (v_xor_b32 + v_pk_min_u16
 # per two pairs) = 1 lane-op per pair.  (SURVEY 8(d)'s contract assumed 3 ops/pair on a
 # 64-bit lane; the packed prefilter is an algorithmic win, so frac here is measured
@@ -51,35 +59,40 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=1 << 24, help="node ids (total over all ranks)")
-    ap.add_argument("--q", type=int, default=65536, help="targets per step")
+    ap.add_argument("--q", type=int, default=65536, help="targets per step (total over all ranks)")
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--algo", choices=["index", "scan"], default="index")
+    ap.add_argument("--route", choices=["auto", "prefix", "broadcast"], default="auto")
+    ap.add_argument("--sharded", action="store_true",
+                    help="use the multi-GPU code path (and its collectives) even with one rank")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="prefix route only: run rank --simulate-rank of a world of this size on one GPU")
+    ap.add_argument("--simulate-rank", type=int, default=0)
     ap.add_argument("--cpu-targets", type=int, default=256, help="cpu_baseline sample (targets)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--verify", type=int, default=16, help="targets re-checked against the oracle (rank 0)")
-    ap.add_argument("--algo", choices=["index", "scan"], default="index",
-                    help="index: K4 bucket-index build + K5 trie-descent query, rebuilt inside every step; "
-                         "scan: K1 brute-force streaming scan")
     ap.add_argument("--no-scan", action="store_true", help="skip the reference K1 scan measurement (index algo)")
-    ap.add_argument("--sharded", action="store_true",
-                    help="run the multi-GPU path (records + RCCL all-gather + K3 merge) even with one rank")
+    ap.add_argument("--verify", type=int, default=16, help="targets re-checked against the oracle (rank 0)")
     return ap.parse_args()
 
 
-def cpu_baseline(n, k, seed, nt, threads):
-    """Oracle (std::partial_sort with the restated InfoHash::xorCmp) on the host cores,
-    over a bounded target sample of the same workload."""
+def oracle():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O
-    ids = O.gen_ids(seed, n)
-    tg = O.gen_ids(seed + 1, nt)
+    return O
+
+
+def cpu_baseline(ids, tg, k, threads):
+    """Oracle (std::partial_sort with the restated InfoHash::xorCmp) on the host cores,
+    over a bounded target sample of the same workload."""
+    O = oracle()
     t0 = time.perf_counter()
     out, _ = O.topk(ids, tg, k, threads=threads)
     dt = time.perf_counter() - t0
-    return {"value": nt / dt, "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": f"{nt} targets x {n} ids, k={k}, std::partial_sort(xorCmp) per target, "
-                      f"{threads} threads, {dt:.2f} s wall"}, ids, tg, out
+    return {"value": tg.shape[0] / dt, "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{tg.shape[0]} targets x {ids.shape[0]} ids, k={k}, std::partial_sort(xorCmp) per target, "
+                      f"{threads} threads, {dt:.2f} s wall"}, out
 
 
 def main():
@@ -87,8 +100,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    sharded = world > 1 or a.sharded
-    if sharded:
+    pow2 = lambda g: g > 0 and (g & (g - 1)) == 0
+    route = a.route
+    if route == "auto":
+        route = "prefix" if (a.algo == "index" and pow2(world)) else "broadcast"
+    if a.simulate_world:
+        assert world == 1 and route == "prefix" and pow2(a.simulate_world)
+    use_dist = world > 1 or a.sharded
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", "0")
@@ -96,43 +115,67 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    L = opendht_amd.lib()
-
-    lo, hi = sharding.shard_range(a.n, world, rank)
-    ctx = opendht_amd.Context(local)
-    ctx.gen_ids(a.seed, hi - lo, start=lo)          # this rank's contiguous slice of the global id stream
-    ts = (a.q + 63) // 64 * 64
-    tp = torch.empty(5 * ts, dtype=torch.int32, device=dev)
     tstream = torch.cuda.Stream(dev)              # every kernel and event of the bench runs here
     torch.cuda.set_stream(tstream)
     stream = tstream.cuda_stream
-    assert L.dhtgpu_gen_dev(a.seed + 1, 0, a.q, tp.data_ptr(), ts, stream) == 0
-    out_idx = torch.empty((a.q, a.k), dtype=torch.int32, device=dev)
-    out_cnt = torch.empty(a.q, dtype=torch.int32, device=dev)
-    rec = torch.empty((a.q, a.k, 6), dtype=torch.int32, device=dev) if sharded else None
-    gathered = torch.empty((world * a.q, a.k, 6), dtype=torch.int32, device=dev) if sharded else None
+    L = opendht_amd.lib()
+    ctx = opendht_amd.Context(local)
 
-    def local(out_i, out_c, out_r, base):
+    G, R = (a.simulate_world, a.simulate_rank) if a.simulate_world else (world, rank)
+    pbits = G.bit_length() - 1 if route == "prefix" else 0
+    ts_all = (a.q + 63) // 64 * 64
+    tp_all = torch.empty(5 * ts_all, dtype=torch.int32, device=dev)
+    assert L.dhtgpu_gen_dev(a.seed + 1, 0, a.q, tp_all.data_ptr(), ts_all, stream) == 0
+    if route == "prefix":
+        if pbits:
+            ctx.gen_ids_prefix(a.seed, a.n, pbits, R)         # this rank's prefix shard, global indices
+            tp = torch.empty_like(tp_all)
+            tgidx = torch.empty(ts_all, dtype=torch.int32, device=dev)
+            q_local = ctx.select_prefix_dev(tp_all.data_ptr(), ts_all, a.q, pbits, R, tp.data_ptr(), ts_all,
+                                            tgidx.data_ptr(), stream)
+        else:                                                 # one shard: the whole set
+            ctx.gen_ids(a.seed, a.n)
+            tp, q_local, tgidx = tp_all, a.q, None
+        ts = ts_all
+        shard_min = torch.tensor([ctx.num_ids], dtype=torch.int64, device=dev)
+        if use_dist:
+            dist.all_reduce(shard_min, op=dist.ReduceOp.MIN)
+        if int(shard_min.item()) < a.k:
+            raise SystemExit("prefix route needs >= k ids per shard; rerun with --route broadcast")
+        n_local = ctx.num_ids
+        lo = 0
+    else:
+        lo, hi = sharding.shard_range(a.n, world, rank)
+        ctx.gen_ids(a.seed, hi - lo, start=lo)      # this rank's contiguous slice of the global id stream
+        tp, ts, q_local, tgidx = tp_all, ts_all, a.q, None
+        n_local = hi - lo
+    collective = use_dist and route == "broadcast"
+    qk = max(q_local, 1)
+    out_idx = torch.empty((qk, a.k), dtype=torch.int32, device=dev)
+    out_cnt = torch.empty(qk, dtype=torch.int32, device=dev)
+    rec = torch.empty((a.q, a.k, 6), dtype=torch.int32, device=dev) if collective else None
+    gathered = torch.empty((world * a.q, a.k, 6), dtype=torch.int32, device=dev) if collective else None
+
+    def local_lookup(out_i, out_c, out_r, base):
         if a.algo == "index":
             ctx.index_build(stream)          # the index is rebuilt from the raw id planes every step
-            ctx.index_topk_dev(tp.data_ptr(), ts, a.q, a.k, out_i, out_c, out_r, base, stream)
+            ctx.index_topk_dev(tp.data_ptr(), ts, q_local, a.k, out_i, out_c, out_r, base, stream)
         else:
-            ctx.topk_dev(tp.data_ptr(), ts, a.q, a.k, out_i, out_c, out_r, base, stream)
+            ctx.topk_dev(tp.data_ptr(), ts, q_local, a.k, out_i, out_c, out_r, base, stream)
 
     def step():
-        if not sharded:
-            local(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0)
+        if not collective:
+            local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0)
         else:
-            local(None, None, rec.data_ptr(), lo)
+            local_lookup(None, None, rec.data_ptr(), lo)
             sharding.gather_records(rec, out=gathered)
-            rc = L.dhtgpu_merge_dev(gathered.data_ptr(), world, a.q, a.k, tp.data_ptr(), ts, a.k,
-                                    out_idx.data_ptr(), out_cnt.data_ptr(), stream)
-            assert rc == 0
+            assert L.dhtgpu_merge_dev(gathered.data_ptr(), world, a.q, a.k, tp.data_ptr(), ts, a.k,
+                                      out_idx.data_ptr(), out_cnt.data_ptr(), stream) == 0
 
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    if sharded:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -142,18 +185,19 @@ def main():
         step()
     ev1.record()
     torch.cuda.synchronize()
-    if sharded:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1) / a.steps
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if sharded:
+    if use_dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t.item())
     ms_per_step = wall * 1e3 / a.steps
-
-    n_local = hi - lo
+    # outputs of the last timed step (for the verification below)
+    got_idx = out_idx[:q_local].cpu().numpy().view(np.uint32).copy()
+    got_tg = tgidx[:q_local].cpu().numpy().view(np.uint32).copy() if tgidx is not None else np.arange(q_local)
 
     def ev_time(fn, reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -170,48 +214,47 @@ def main():
         # the bench stream) and of the query kernel alone
         phases = [ctx.index_build_timed(stream) for _ in range(reps)]
         ph = [sum(p[i] for p in phases) / reps for i in range(4)]
-        q_ms = ev_time(lambda: ctx.index_topk_dev(tp.data_ptr(), ts, a.q, a.k, out_idx.data_ptr(),
+        q_ms = ev_time(lambda: ctx.index_topk_dev(tp.data_ptr(), ts, q_local, a.k, out_idx.data_ptr(),
                                                   out_cnt.data_ptr(), None, 0, stream), reps)
         kern = {"k_p0_hist": (ph[0], 4 * n_local), "k_p0_scans": (ph[1], 0),
                 "k_p1_scatter": (ph[2], 12 * n_local), "k_p2_buckets": (ph[3], 16 * n_local),
-                "k_query": (q_ms, a.q * (20 + a.k * 4))}
+                "k_query": (q_ms, q_local * (20 + a.k * 4))}
         dom = max(kern, key=lambda k: kern[k][0])
         dom_ms, dom_bytes = kern[dom]
-        step_bytes = n_local * (4 + 8) + a.q * (20 + a.k * 4)
+        step_bytes = n_local * (4 + 8) + q_local * (20 + a.k * 4)
         roof = {"bound": "hbm", "achieved": dom_bytes / (dom_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                 "kernel": dom, "kernel_ms": dom_ms, "alg_bytes_per_launch": dom_bytes,
                 "kernels_ms": {k: v[0] for k, v in kern.items()},
                 "step_alg_bytes": step_bytes,
                 "step_hbm_frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS}
-        extra = {"query_only_qps": a.q / (q_ms * 1e-3), "index_build_ms": sum(ph)}
+        extra = {"query_only_qps_per_gpu": q_local / (q_ms * 1e-3), "index_build_ms": sum(ph)}
     else:
         kern_ms = ev_ms
-        if sharded:
-            kern_ms = ev_time(lambda: local(None, None, rec.data_ptr(), lo), reps)
-        pairs = a.q * n_local
+        if collective:
+            kern_ms = ev_time(lambda: local_lookup(None, None, rec.data_ptr(), lo), reps)
+        pairs = q_local * n_local
         achieved = OPS_PER_PAIR * pairs / (kern_ms * 1e-3) / 1e12
         roof = {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
                 "frac": achieved / VALU_PEAK_TOPS, "traffic": None,
                 "kernel": "k_scan (K1 xor_topk_scan)", "kernel_ms": kern_ms,
                 "ops_per_pair": OPS_PER_PAIR, "pairs_per_launch": pairs,
-                "hbm_alg_bytes_per_launch": n_local * 20 + a.q * 20 + a.q * a.k * 4}
+                "hbm_alg_bytes_per_launch": n_local * 20 + q_local * 20 + q_local * a.k * 4}
         extra = {}
-    if a.algo == "index" and not a.no_scan and not sharded:
+    if a.algo == "index" and not a.no_scan and world == 1 and not a.simulate_world:
         # the north-star brute-force scan (K1) on the same inputs, for reference
-        sc_ms = ev_time(lambda: ctx.topk_dev(tp.data_ptr(), ts, a.q, a.k, out_idx.data_ptr(), out_cnt.data_ptr(),
-                                             None, 0, stream), 3)
-        ach = OPS_PER_PAIR * a.q * n_local / (sc_ms * 1e-3) / 1e12
-        extra["scan_k1"] = {"qps": a.q / (sc_ms * 1e-3), "kernel_ms": sc_ms, "bound": "valu",
+        sc_ms = ev_time(lambda: ctx.topk_dev(tp.data_ptr(), ts, q_local, a.k, out_idx.data_ptr(),
+                                             out_cnt.data_ptr(), None, 0, stream), 3)
+        ach = OPS_PER_PAIR * q_local * n_local / (sc_ms * 1e-3) / 1e12
+        extra["scan_k1"] = {"qps": q_local / (sc_ms * 1e-3), "kernel_ms": sc_ms, "bound": "valu",
                             "achieved_TOPs": ach, "peak_TOPs": VALU_PEAK_TOPS, "frac": ach / VALU_PEAK_TOPS}
-        # restore the index-path output for the verification below
-        step()
-        torch.cuda.synchronize()
 
     if rank == 0:
+        par = {"prefix": f"prefix-routed shards x{G} (top {pbits} id bits; no data-path collective)",
+               "broadcast": f"id-range shards x{world}" + (" + RCCL all-gather + K3 merge" if collective else "")}[route]
         res = {
             "metric": METRIC,
-            "value": a.q / (ms_per_step * 1e-3),
+            "value": (a.q if not a.simulate_world else q_local) / (ms_per_step * 1e-3),
             "unit": "queries/s",
             "n_gpus": world,
             "steps": a.steps,
@@ -223,22 +266,31 @@ def main():
             "dtype": "u32",
             "data": "synthetic: splitmix64 ids and targets generated in HBM (SURVEY 8(d) spec)",
             "config": {"workload": f"cfg2 batched k-NN: {a.q} targets x {a.n} ids (2^{a.n.bit_length()-1}), k={a.k}",
-                       "n_ids": a.n, "n_targets": a.q, "k": a.k, "algo": a.algo,
-                       "parallelism": f"id-range shards x{world}" + (" + RCCL all-gather + K3 merge" if sharded else "")},
+                       "n_ids": a.n, "n_targets": a.q, "k": a.k, "algo": a.algo, "route": route,
+                       "ids_per_gpu": n_local, "targets_per_gpu": q_local, "parallelism": par},
             "roofline": roof,
         }
+        if a.simulate_world:
+            res["simulated"] = f"rank {R} of {G} on one GPU; value = this rank's targets / its step time"
         res.update(extra)
-        # cpu_baseline (rank 0, N=1 only) + spot check of this run's output vs the oracle
-        if world == 1 and not a.no_cpu:
-            # (in --sharded mode this also checks the merged output of the record path)
-            cb, ids, tg, want = cpu_baseline(a.n, a.k, a.seed, max(a.cpu_targets, a.verify), a.cpu_threads)
-            got = out_idx[: want.shape[0]].cpu().numpy().view(np.uint32)
-            res["cpu_baseline"] = cb
-            res["verified_targets"] = int(want.shape[0])
-            res["verified_exact"] = bool(np.array_equal(got, want))
+        # spot check of this run's output against the oracle (rank 0), and the cpu_baseline
+        # leg (rank 0, N = 1 only)
+        if not a.no_cpu and (a.verify or world == 1):
+            O = oracle()
+            ids = O.gen_ids(a.seed, a.n)
+            nv = min(q_local, max(a.verify, a.cpu_targets if world == 1 else 0))
+            tg_all = O.gen_ids(a.seed + 1, a.q)
+            tg = tg_all[got_tg[:nv]]
+            if world == 1 and not a.simulate_world:
+                cb, want = cpu_baseline(ids, tg, a.k, a.cpu_threads)
+                res["cpu_baseline"] = cb
+            else:
+                want, _ = O.topk(ids, tg, a.k, threads=a.cpu_threads)
+            res["verified_targets"] = int(nv)
+            res["verified_exact"] = bool(np.array_equal(got_idx[:nv], want))
         print(json.dumps(res), flush=True)
     ctx.close()
-    if sharded:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -67,6 +67,12 @@ int dhtgpu_set_ids(dhtgpu_ctx* ctx, const uint8_t* ids20_be, uint64_t n);
 /* Generate n synthetic ids directly in HBM: splitmix64 stream,
  * id i = BE(x(3g)) || BE(x(3g+1)) || top4(BE(x(3g+2))), g = start + i. */
 int dhtgpu_gen_ids(dhtgpu_ctx* ctx, uint64_t seed, uint64_t start, uint64_t n);
+/* Multi-GPU prefix routing: generate the stream [start, start+n) and keep
+ * only the ids whose top pbits bits equal pval, in stream order.  Every result index of
+ * the context then refers to the GLOBAL stream (start + i); get_ids/classify use shard
+ * order.  pbits <= 16. */
+int dhtgpu_gen_ids_prefix(dhtgpu_ctx* ctx, uint64_t seed, uint64_t start, uint64_t n, uint32_t pbits,
+                          uint32_t pval);
 uint64_t dhtgpu_num_ids(const dhtgpu_ctx* ctx);
 /* Read back ids [first, first+n) as 20-byte big-endian. */
 int dhtgpu_get_ids(dhtgpu_ctx* ctx, uint64_t first, uint64_t n, uint8_t* out20_be);
@@ -94,6 +100,13 @@ int dhtgpu_topk_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride
 int dhtgpu_merge_dev(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_t k_in,
                      const uint32_t* t_planes, uint64_t t_stride, uint32_t k,
                      uint32_t* out_idx, uint32_t* out_cnt, void* stream);
+
+/* Device planes -> the ids whose top pbits bits equal pval, compacted in order into
+ * out_planes (out_stride >= count) with out_gidx[j] = original index (nullable);
+ * *out_count = number selected.  Synchronises (setup-time helper). */
+int dhtgpu_select_prefix_dev(dhtgpu_ctx* ctx, const uint32_t* planes, uint64_t stride, uint64_t n,
+                             uint32_t pbits, uint32_t pval, uint32_t* out_planes, uint64_t out_stride,
+                             uint32_t* out_gidx, uint64_t* out_count, void* stream);
 
 /* Convert 20-byte big-endian ids (device) into word planes (device). */
 int dhtgpu_pack_dev(const uint8_t* ids20_be, uint64_t n, uint32_t* planes, uint64_t stride,

@@ -85,6 +85,10 @@ def lib():
                                    ctypes.c_uint32, _vp], ctypes.c_int),
         "dhtgpu_index_topk": ([_vp, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p], ctypes.c_int),
         "dhtgpu_index_build_timed": ([_vp, _vp, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+        "dhtgpu_gen_ids_prefix": ([_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                   ctypes.c_uint32], ctypes.c_int),
+        "dhtgpu_select_prefix_dev": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                      _vp, ctypes.c_uint64, _vp, _u64p, _vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -101,7 +105,7 @@ def exported_symbols():
             "dhtgpu_ids_dev", "dhtgpu_topk", "dhtgpu_topk_dev", "dhtgpu_merge_dev", "dhtgpu_pack_dev",
             "dhtgpu_gen_dev", "dhtgpu_find_closest", "dhtgpu_classify", "dhtgpu_classify_dev",
             "dhtgpu_cached_nodes", "dhtgpu_index_build", "dhtgpu_index_topk_dev", "dhtgpu_index_topk",
-            "dhtgpu_index_build_timed"]
+            "dhtgpu_index_build_timed", "dhtgpu_gen_ids_prefix", "dhtgpu_select_prefix_dev"]
 
 
 def _ids(a, name="ids"):
@@ -159,6 +163,18 @@ class Context:
 
     def gen_ids(self, seed, n, start=0):
         _check(lib().dhtgpu_gen_ids(self._h, seed, start, n), "gen_ids")
+
+    def gen_ids_prefix(self, seed, n, pbits, pval, start=0):
+        """Keep the ids of the stream [start, start+n) whose top pbits bits == pval
+        (a prefix shard); result indices refer to the global stream."""
+        _check(lib().dhtgpu_gen_ids_prefix(self._h, seed, start, n, pbits, pval), "gen_ids_prefix")
+
+    def select_prefix_dev(self, planes_ptr, stride, n, pbits, pval, out_planes_ptr, out_stride, out_gidx_ptr=None,
+                          stream=None):
+        cnt = ctypes.c_uint64()
+        _check(lib().dhtgpu_select_prefix_dev(self._h, planes_ptr, stride, n, pbits, pval, out_planes_ptr, out_stride,
+                                              out_gidx_ptr, ctypes.byref(cnt), stream), "select_prefix_dev")
+        return cnt.value
 
     @property
     def num_ids(self):

@@ -63,7 +63,9 @@ struct dhtgpu_ctx {
     DevBuf targets;         // 5 * tstride u32
     DevBuf out_idx, out_cnt, rec, aux, aux2, aux3;
     bool has_ids = false;
-    DevBuf index;           // K4 workspace: records | directory | cursor | block sums
+    DevBuf gidx;            // shard -> global index map (dhtgpu_gen_ids_prefix), else unused
+    bool has_gidx = false;
+    DevBuf index;           // K4 workspace: entries | directory | partition scratch
     uint32_t index_B = 0;
     bool index_valid = false;
 
@@ -132,7 +134,7 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
     (void)c->bind();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->planes, &c->staging, &c->targets, &c->out_idx, &c->out_cnt, &c->rec,
-                      &c->aux, &c->aux2, &c->aux3, &c->index})
+                      &c->aux, &c->aux2, &c->aux3, &c->index, &c->gidx})
         b->release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -163,6 +165,7 @@ static int alloc_ids(dhtgpu_ctx* c, uint64_t n) {
     if (n >= 0xFFFFFFFFull) return DHTGPU_ERANGE;
     c->has_ids = false;
     c->index_valid = false;
+    c->has_gidx = false;
     c->stride = pad_ids(n ? n : 1);
     DHT_TRY(c->planes.ensure((size_t)c->stride * 5 * 4));
     return DHTGPU_OK;
@@ -191,6 +194,56 @@ int dhtgpu_gen_ids(dhtgpu_ctx* c, uint64_t seed, uint64_t start, uint64_t n) {
     if (r) return r;
     DHT_TRY(launch_gen(seed, start, n, c->planes.as<uint32_t>(), c->stride, c->stream));
     return finish_ids(c, n);
+}
+
+int dhtgpu_gen_ids_prefix(dhtgpu_ctx* c, uint64_t seed, uint64_t start, uint64_t n, uint32_t pbits,
+                          uint32_t pval) {
+    if (!c || pbits > 16 || (pbits < 32 && pval >= (1u << pbits))) return DHTGPU_EINVAL;
+    if (n >= 0xFFFFFFFFull || start + n > 0xFFFFFFFFull) return DHTGPU_ERANGE;
+    DHT_TRY(c->bind());
+    // the whole stream is generated into scratch, then the shard is compacted in order
+    const uint64_t gs = pad_ids(n ? n : 1);
+    DHT_TRY(c->staging.ensure((size_t)gs * 5 * 4));
+    uint32_t* gen = c->staging.as<uint32_t>();
+    DHT_TRY(launch_gen(seed, start, n, gen, gs, c->stream));
+    DHT_TRY(c->aux.ensure((size_t)select_scratch_words(n) * 4 + 16));
+    unsigned long long* d_total = reinterpret_cast<unsigned long long*>(c->aux.as<uint8_t>());
+    uint32_t* scratch = reinterpret_cast<uint32_t*>(c->aux.as<uint8_t>() + 8);
+    DHT_TRY(launch_select_prefix(gen, gs, n, pbits, pval, scratch, d_total, nullptr, 0, nullptr, 0, c->stream));
+    unsigned long long m = 0;
+    DHT_TRY(hipMemcpyAsync(&m, d_total, 8, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    int r = alloc_ids(c, m);
+    if (r) return r;
+    DHT_TRY(c->gidx.ensure((size_t)(m ? m : 1) * 4));
+    DHT_TRY(launch_select_prefix(gen, gs, n, pbits, pval, scratch, d_total, c->planes.as<uint32_t>(), c->stride,
+                                 c->gidx.as<uint32_t>(), start, c->stream));
+    r = finish_ids(c, m);
+    if (r) return r;
+    c->has_gidx = true;
+    return DHTGPU_OK;
+}
+
+int dhtgpu_select_prefix_dev(dhtgpu_ctx* c, const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t pbits,
+                             uint32_t pval, uint32_t* out_planes, uint64_t out_stride, uint32_t* out_gidx,
+                             uint64_t* out_count, void* stream) {
+    if (!c || !out_count || pbits > 16 || (pbits < 32 && pval >= (1u << pbits))) return DHTGPU_EINVAL;
+    if (n && (!planes || !out_planes)) return DHTGPU_EINVAL;
+    DHT_TRY(c->bind());
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    DHT_TRY(c->aux.ensure((size_t)select_scratch_words(n) * 4 + 16));
+    unsigned long long* d_total = reinterpret_cast<unsigned long long*>(c->aux.as<uint8_t>());
+    uint32_t* scratch = reinterpret_cast<uint32_t*>(c->aux.as<uint8_t>() + 8);
+    DHT_TRY(launch_select_prefix(planes, stride, n, pbits, pval, scratch, d_total, nullptr, 0, nullptr, 0, s));
+    unsigned long long m = 0;
+    DHT_TRY(hipMemcpyAsync(&m, d_total, 8, hipMemcpyDeviceToHost, s));
+    DHT_TRY(hipStreamSynchronize(s));
+    if (m > out_stride) return DHTGPU_ERANGE;
+    DHT_TRY(launch_select_prefix(planes, stride, n, pbits, pval, scratch, d_total, out_planes, out_stride, out_gidx,
+                                 0, s));
+    DHT_TRY(hipStreamSynchronize(s));
+    *out_count = m;
+    return DHTGPU_OK;
 }
 
 int dhtgpu_get_ids(dhtgpu_ctx* c, uint64_t first, uint64_t n, uint8_t* out20) {
@@ -224,27 +277,35 @@ int dhtgpu_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, 
     DHT_TRY(c->bind());
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     const ScanPlan p = plan_scan(c->n, q, c->num_cus);
-    if (p.splits == 1 || c->n == 0) {
+    const uint32_t* gidx = c->has_gidx ? c->gidx.as<uint32_t>() : nullptr;
+    if ((p.splits == 1 || c->n == 0) && !gidx) {   // one pass writes the final form directly
         DHT_TRY(launch_scan(c->planes.as<uint32_t>(), c->stride, c->n, p, tp, ts, q, k, out_idx,
                             out_cnt, out_rec, idx_base, s));
         return DHTGPU_OK;
     }
-    // split id range: per-split candidate records, then K3 merge
-    DHT_TRY(c->rec.ensure((size_t)p.splits * q * k * 6 * 4));
-    DHT_TRY(launch_scan(c->planes.as<uint32_t>(), c->stride, c->n, p, tp, ts, q, k, nullptr,
-                        nullptr, c->rec.as<uint32_t>(), 0, s));
-    if (!out_rec) {
-        DHT_TRY(launch_merge(c->rec.as<uint32_t>(), p.splits, q, k, tp, ts, k, out_idx, out_cnt, s));
-        if (idx_base) DHT_TRY(launch_add_base(out_idx, (uint64_t)q * k, idx_base, s));
-        return DHTGPU_OK;
+    // local indices (merged over id-range splits when the batch is too small to fill
+    // the chip), then mapped to global indices or turned into candidate records
+    uint32_t* li = out_idx;
+    uint32_t* lc = out_cnt;
+    if (out_rec) {
+        DHT_TRY(c->out_idx.ensure((size_t)q * k * 4));
+        DHT_TRY(c->out_cnt.ensure((size_t)q * 4));
+        li = c->out_idx.as<uint32_t>();
+        lc = c->out_cnt.as<uint32_t>();
     }
-    // records requested (cross-shard merge): merge locally, then re-gather records
-    DHT_TRY(c->out_idx.ensure((size_t)q * k * 4));
-    DHT_TRY(c->out_cnt.ensure((size_t)q * 4));
-    DHT_TRY(launch_merge(c->rec.as<uint32_t>(), p.splits, q, k, tp, ts, k, c->out_idx.as<uint32_t>(),
-                         c->out_cnt.as<uint32_t>(), s));
-    DHT_TRY(launch_rec_from_idx(c->out_idx.as<uint32_t>(), (uint64_t)q * k, c->planes.as<uint32_t>(),
-                                c->stride, idx_base, out_rec, s));
+    if (p.splits == 1 || c->n == 0) {
+        DHT_TRY(launch_scan(c->planes.as<uint32_t>(), c->stride, c->n, p, tp, ts, q, k, li, lc, nullptr, 0, s));
+    } else {
+        DHT_TRY(c->rec.ensure((size_t)p.splits * q * k * 6 * 4));
+        DHT_TRY(launch_scan(c->planes.as<uint32_t>(), c->stride, c->n, p, tp, ts, q, k, nullptr, nullptr,
+                            c->rec.as<uint32_t>(), 0, s));
+        DHT_TRY(launch_merge(c->rec.as<uint32_t>(), p.splits, q, k, tp, ts, k, li, lc, s));
+    }
+    if (out_rec)
+        DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
+                                    out_rec, s));
+    else
+        DHT_TRY(launch_map_idx(li, (uint64_t)q * k, gidx, idx_base, s));
     return DHTGPU_OK;
 }
 
@@ -334,17 +395,22 @@ int dhtgpu_index_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     if (!q) return DHTGPU_OK;
     DHT_TRY(c->bind());
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const uint32_t* gidx = c->has_gidx ? c->gidx.as<uint32_t>() : nullptr;
+    uint32_t* li = out_idx;
+    uint32_t* lc = out_cnt;
     if (out_rec) {   // candidate records for a cross-shard merge
         DHT_TRY(c->out_idx.ensure((size_t)q * k * 4));
         DHT_TRY(c->out_cnt.ensure((size_t)q * 4));
-        DHT_TRY(launch_index_query(c->index.p, c->n, c->index_B, c->planes.as<uint32_t>(), c->stride, tp, ts, q, k, c->out_idx.as<uint32_t>(),
-                                   c->out_cnt.as<uint32_t>(), s));
-        DHT_TRY(launch_rec_from_idx(c->out_idx.as<uint32_t>(), (uint64_t)q * k, c->planes.as<uint32_t>(),
-                                    c->stride, idx_base, out_rec, s));
-        return DHTGPU_OK;
+        li = c->out_idx.as<uint32_t>();
+        lc = c->out_cnt.as<uint32_t>();
     }
-    DHT_TRY(launch_index_query(c->index.p, c->n, c->index_B, c->planes.as<uint32_t>(), c->stride, tp, ts, q, k, out_idx, out_cnt, s));
-    if (idx_base) DHT_TRY(launch_add_base(out_idx, (uint64_t)q * k, idx_base, s));
+    DHT_TRY(launch_index_query(c->index.p, c->n, c->index_B, c->planes.as<uint32_t>(), c->stride, tp, ts, q, k,
+                               li, lc, s));
+    if (out_rec)
+        DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
+                                    out_rec, s));
+    else
+        DHT_TRY(launch_map_idx(li, (uint64_t)q * k, gidx, idx_base, s));
     return DHTGPU_OK;
 }
 
@@ -489,6 +555,8 @@ int dhtgpu_cached_nodes(dhtgpu_ctx* c, const uint8_t* accept, const uint8_t* t20
     DHT_TRY(c->aux3.ensure((size_t)q * 4));
     DHT_TRY(launch_cached(c->planes.as<uint32_t>(), c->stride, c->n, d_acc, c->targets.as<uint32_t>(),
                           ts, q, count, c->aux2.as<uint32_t>(), c->aux3.as<uint32_t>(), c->stream));
+    if (c->has_gidx)
+        DHT_TRY(launch_map_idx(c->aux2.as<uint32_t>(), (uint64_t)q * count, c->gidx.as<uint32_t>(), 0, c->stream));
     DHT_TRY(hipMemcpyAsync(out_idx, c->aux2.p, (size_t)q * count * 4, hipMemcpyDeviceToHost, c->stream));
     DHT_TRY(hipMemcpyAsync(out_cnt, c->aux3.p, (size_t)q * 4, hipMemcpyDeviceToHost, c->stream));
     DHT_TRY(hipStreamSynchronize(c->stream));

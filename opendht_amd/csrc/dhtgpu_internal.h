@@ -26,6 +26,15 @@ hipError_t launch_fill(uint32_t* p, uint64_t n, uint32_t v, hipStream_t s);
 hipError_t launch_check_sorted(const uint32_t* planes, uint64_t stride, uint64_t n,
                                uint32_t* d_flag, hipStream_t s);
 
+// ids whose top pbits bits equal pval, compacted in index order (out == nullptr: count
+// only).  scratch: select_scratch_words(n) u32; *d_total = number selected; gidx[j] =
+// gbase + original index of the j-th selected id (nullable).
+hipError_t launch_select_prefix(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t pbits,
+                                uint32_t pval, uint32_t* scratch, unsigned long long* d_total,
+                                uint32_t* out, uint64_t out_stride, uint32_t* gidx, uint64_t gbase,
+                                hipStream_t s);
+uint64_t select_scratch_words(uint64_t n);
+
 // scan.hip
 struct ScanPlan {
     uint32_t blocks_x;   // target groups
@@ -41,11 +50,13 @@ hipError_t launch_merge(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_
                         const uint32_t* tp, uint64_t ts, uint32_t k, uint32_t* out_idx,
                         uint32_t* out_cnt, hipStream_t s);
 
-// out_idx[i] += base for valid entries
-hipError_t launch_add_base(uint32_t* idx, uint64_t m, uint32_t base, hipStream_t s);
-// rec[i] = {words of id idx[i], idx[i] + base} (DHT_NONE record for DHT_NONE)
+// valid idx[i] -> gidx ? gidx[idx[i]] : idx[i] + base
+hipError_t launch_map_idx(uint32_t* idx, uint64_t m, const uint32_t* gidx, uint32_t base, hipStream_t s);
+// rec[i] = {words of id idx[i], global index} (DHT_NONE record for DHT_NONE); the global
+// index is gidx[idx[i]] when gidx != nullptr, else idx[i] + base
 hipError_t launch_rec_from_idx(const uint32_t* idx, uint64_t m, const uint32_t* planes,
-                               uint64_t stride, uint32_t base, uint32_t* rec, hipStream_t s);
+                               uint64_t stride, uint32_t base, const uint32_t* gidx, uint32_t* rec,
+                               hipStream_t s);
 
 // table.hip
 hipError_t launch_find_closest(uint32_t nb, const uint32_t* fp, const uint32_t* off,

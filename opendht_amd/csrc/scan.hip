@@ -363,21 +363,23 @@ __global__ __launch_bounds__(64) void k_merge(const uint32_t* __restrict__ rec, 
     if (lane == 0) out_cnt[qi] = nout;
 }
 
-__global__ __launch_bounds__(256) void k_add_base(uint32_t* __restrict__ idx, uint64_t m, uint32_t base) {
+__global__ __launch_bounds__(256) void k_map_idx(uint32_t* __restrict__ idx, uint64_t m,
+                                                 const uint32_t* __restrict__ gidx, uint32_t base) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < m && idx[i] != DHT_NONE) idx[i] += base;
+    if (i < m && idx[i] != DHT_NONE) idx[i] = gidx ? gidx[idx[i]] : idx[i] + base;
 }
 
 __global__ __launch_bounds__(256) void k_rec_from_idx(const uint32_t* __restrict__ idx, uint64_t m,
                                                       const uint32_t* __restrict__ planes,
                                                       uint64_t stride, uint32_t base,
+                                                      const uint32_t* __restrict__ gidx,
                                                       uint32_t* __restrict__ rec) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= m) return;
     const uint32_t x = idx[i];
 #pragma unroll
     for (int w = 0; w < DHT_W; ++w) rec[i * 6 + w] = x == DHT_NONE ? DHT_NONE : planes[(uint64_t)w * stride + x];
-    rec[i * 6 + 5] = x == DHT_NONE ? DHT_NONE : x + base;
+    rec[i * 6 + 5] = x == DHT_NONE ? DHT_NONE : (gidx ? gidx[x] : x + base);
 }
 
 template <uint32_t K>
@@ -419,16 +421,17 @@ hipError_t launch_scan(const uint32_t* ids, uint64_t is, uint64_t n, const ScanP
     return launch_scan_k<32>(ids, is, n, p, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s);
 }
 
-hipError_t launch_add_base(uint32_t* idx, uint64_t m, uint32_t base, hipStream_t s) {
-    if (!m) return hipSuccess;
-    k_add_base<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(idx, m, base);
+hipError_t launch_map_idx(uint32_t* idx, uint64_t m, const uint32_t* gidx, uint32_t base, hipStream_t s) {
+    if (!m || (!gidx && !base)) return hipSuccess;
+    k_map_idx<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(idx, m, gidx, base);
     return hipGetLastError();
 }
 
 hipError_t launch_rec_from_idx(const uint32_t* idx, uint64_t m, const uint32_t* planes,
-                               uint64_t stride, uint32_t base, uint32_t* rec, hipStream_t s) {
+                               uint64_t stride, uint32_t base, const uint32_t* gidx, uint32_t* rec,
+                               hipStream_t s) {
     if (!m) return hipSuccess;
-    k_rec_from_idx<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(idx, m, planes, stride, base, rec);
+    k_rec_from_idx<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(idx, m, planes, stride, base, gidx, rec);
     return hipGetLastError();
 }
 

@@ -231,3 +231,41 @@ def test_cpp_adapter_on_gpu(tmp_path):
     out = subprocess.run([exe, "--run"], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "0 mismatches" in out.stdout
+
+
+@pytest.mark.parametrize("pbits,pval", [(0, 0), (1, 1), (3, 5)])
+def test_prefix_shard_matches_global_topk(ctx, pbits, pval):
+    """Prefix routing: a shard holding the ids with top-pbits == pval answers
+    every target carrying that prefix exactly like the full set, with global indices."""
+    n = 120000
+    ids = O.gen_ids(91, n)
+    tg = O.gen_ids(92, 3000)
+    top = lambda a: (a[:, 0].astype(np.uint32) >> (8 - pbits)) if pbits else np.zeros(a.shape[0], np.uint32)
+    mine = tg[top(tg) == pval]
+    assert mine.shape[0] > 0
+    ctx.gen_ids_prefix(91, n, pbits, pval)
+    shard = ids[top(ids) == pval]
+    assert ctx.num_ids == shard.shape[0]
+    assert np.array_equal(ctx.get_ids(), shard)
+    want, wcnt = O.topk(ids, mine, 8)
+    for fn in (ctx.topk, ctx.index_topk):
+        got, cnt = fn(mine, 8)
+        assert np.array_equal(cnt, wcnt) and np.array_equal(got, want)
+
+
+def test_select_prefix_dev(ctx):
+    import torch
+    n, stride = 50000, 50048
+    dev = torch.device("cuda", 0)
+    planes = torch.empty(5 * stride, dtype=torch.int32, device=dev)
+    import opendht_amd
+    assert opendht_amd.lib().dhtgpu_gen_dev(5, 0, n, planes.data_ptr(), stride, None) == 0
+    out = torch.empty(5 * stride, dtype=torch.int32, device=dev)
+    gidx = torch.empty(stride, dtype=torch.int32, device=dev)
+    m = ctx.select_prefix_dev(planes.data_ptr(), stride, n, 2, 3, out.data_ptr(), stride, gidx.data_ptr())
+    ids = O.gen_ids(5, n)
+    sel = np.nonzero((ids[:, 0] >> 6) == 3)[0]
+    assert m == sel.size
+    assert np.array_equal(gidx[:m].cpu().numpy().view(np.uint32), sel.astype(np.uint32))
+    words = out.view(5, stride)[:, :m].cpu().numpy().view(np.uint32).T
+    assert np.array_equal(words, ids[sel].view(">u4").reshape(-1, 5).astype(np.uint32))
