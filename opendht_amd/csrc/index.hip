@@ -40,18 +40,19 @@ constexpr int kBlk = 256;
 //       a scatter path instead.)
 // Ranks come from LDS atomics, so order inside a bucket is arbitrary; queries rank
 // candidates by (distance, index), so results do not depend on it.
-constexpr uint32_t kP1Tile = 8192;   // ids per P0/P1 block (256 threads x 32)
+constexpr uint32_t kP1Tile = 8192;   // minimum ids per P0/P1 block (256 threads x 32); grown so nblk <= 2048
 constexpr int kP2Blk = 1024;
+constexpr int kP2Per = 16;          // entries per thread per batch: a ~16K partition is one batch
 constexpr uint32_t kLdsMax = 160 * 1024;
 
 __global__ __launch_bounds__(kBlk) void k_p0_hist(const uint32_t* __restrict__ w0, uint64_t n, uint32_t b1,
-                                                 uint32_t nblk, uint32_t* __restrict__ H) {
+                                                 uint32_t nblk, uint32_t tile, uint32_t* __restrict__ H) {
     extern __shared__ uint32_t sh[];
     const uint32_t nbin = 1u << b1, shift = 32 - b1;
     for (uint32_t i = threadIdx.x; i < nbin; i += kBlk) sh[i] = 0;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * kP1Tile;
-    const uint32_t cnt = (uint32_t)(n - base < kP1Tile ? n - base : kP1Tile);
+    const uint64_t base = (uint64_t)blockIdx.x * tile;
+    const uint32_t cnt = (uint32_t)(n - base < tile ? n - base : tile);
     for (uint32_t e = threadIdx.x * 4; e < cnt; e += kBlk * 4) {
         if (e + 3 < cnt) {
             const uint4 v = *reinterpret_cast<const uint4*>(w0 + base + e);
@@ -88,6 +89,28 @@ __device__ uint32_t block_scan_inplace(uint32_t* __restrict__ a, uint32_t len, u
     return carry;
 }
 
+// exclusive scan of `len` values in place by a block of NT threads; returns the total
+template <int NT>
+__device__ uint32_t block_scan_nt(uint32_t* __restrict__ a, uint32_t len, uint32_t* scr) {
+    uint32_t carry = 0;
+    for (uint32_t b = 0; b < len; b += NT) {
+        const uint32_t i = b + threadIdx.x;
+        const uint32_t v = i < len ? a[i] : 0;
+        scr[threadIdx.x] = v;
+        __syncthreads();
+        for (uint32_t o = 1; o < (uint32_t)NT; o <<= 1) {
+            const uint32_t x = threadIdx.x >= o ? scr[threadIdx.x - o] : 0;
+            __syncthreads();
+            scr[threadIdx.x] += x;
+            __syncthreads();
+        }
+        if (i < len) a[i] = carry + scr[threadIdx.x] - v;
+        carry += scr[NT - 1];
+        __syncthreads();
+    }
+    return carry;
+}
+
 __global__ __launch_bounds__(1024) void k_p0_rowscan(uint32_t* __restrict__ H, uint32_t nblk,
                                                     uint32_t* __restrict__ pcount) {
     __shared__ uint32_t scr[1024];
@@ -104,35 +127,73 @@ __global__ __launch_bounds__(1024) void k_p0_scan(uint32_t* __restrict__ pcount,
     if (threadIdx.x == 0) pstart[nbin] = (uint32_t)n;
 }
 
+// P1: the block's tile is counting-sorted by partition in LDS first, so that every
+// partition run is then written to HBM contiguously by consecutive lanes (runs are
+// short -- tile / 2^b1 entries -- and scattered 8-byte stores would leave partial lines).
+constexpr uint32_t kP1Stage = 8192;   // entries staged in LDS per round (64 KB)
+
 __global__ __launch_bounds__(kBlk) void k_p1_scatter(const uint32_t* __restrict__ w0, uint64_t n, uint32_t b1,
-                                                    uint32_t nblk, const uint32_t* __restrict__ H,
+                                                    uint32_t nblk, uint32_t tile, const uint32_t* __restrict__ H,
                                                     const uint32_t* __restrict__ pstart,
                                                     uint2* __restrict__ tmp) {
-    extern __shared__ uint32_t sh[];   // [rank counters 2^b1 | base 2^b1]
+    extern __shared__ uint32_t sh[];   // [gbase 2^b1 | lcnt 2^b1 | loff 2^b1 | scan scratch kBlk | stage]
     const uint32_t nbin = 1u << b1, shift = 32 - b1;
-    uint32_t* cnt = sh;
-    uint32_t* bb = sh + nbin;
-    for (uint32_t i = threadIdx.x; i < nbin; i += kBlk) {
-        cnt[i] = 0;
-        bb[i] = pstart[i] + H[(uint64_t)i * nblk + blockIdx.x];
-    }
-    __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * kP1Tile;
-    const uint32_t m = (uint32_t)(n - base < kP1Tile ? n - base : kP1Tile);
-    for (uint32_t e = threadIdx.x * 4; e < m; e += kBlk * 4) {
-        uint32_t v[4];
-        if (e + 3 < m) {
-            const uint4 x = *reinterpret_cast<const uint4*>(w0 + base + e);
-            v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-        } else {
-            for (uint32_t f = 0; f < 4; ++f) v[f] = e + f < m ? w0[base + e + f] : 0;
+    uint32_t* gbase = sh;
+    uint32_t* lcnt = sh + nbin;
+    uint32_t* loff = sh + 2 * nbin;
+    uint32_t* scr = sh + 3 * nbin;
+    uint2* stage = reinterpret_cast<uint2*>(scr + kBlk);
+    for (uint32_t i = threadIdx.x; i < nbin; i += kBlk) gbase[i] = pstart[i] + H[(uint64_t)i * nblk + blockIdx.x];
+    const uint64_t base0 = (uint64_t)blockIdx.x * tile;
+    const uint32_t mt = (uint32_t)(n - base0 < tile ? n - base0 : tile);
+    constexpr uint32_t PER = kP1Stage / kBlk;   // 32 ids per thread per round
+    for (uint32_t r0 = 0; r0 < mt; r0 += kP1Stage) {
+        const uint32_t m = mt - r0 < kP1Stage ? mt - r0 : kP1Stage;
+        const uint64_t base = base0 + r0;
+        for (uint32_t i = threadIdx.x; i < nbin; i += kBlk) lcnt[i] = 0;
+        __syncthreads();
+        // ids base + 4*threadIdx.x + 1024*e + f  (coalesced 16-B loads, all issued first)
+        uint32_t v[PER];
+#pragma unroll
+        for (uint32_t e = 0; e < PER / 4; ++e) {
+            const uint32_t j = e * 4 * kBlk + 4 * threadIdx.x;
+            if (j + 3 < m) {
+                const uint4 x = *reinterpret_cast<const uint4*>(w0 + base + j);
+                v[4 * e] = x.x; v[4 * e + 1] = x.y; v[4 * e + 2] = x.z; v[4 * e + 3] = x.w;
+            } else {
+#pragma unroll
+                for (uint32_t f = 0; f < 4; ++f) v[4 * e + f] = j + f < m ? w0[base + j + f] : 0;
+            }
         }
 #pragma unroll
-        for (uint32_t f = 0; f < 4; ++f) {
-            if (e + f >= m) break;
-            const uint32_t d = v[f] >> shift;
-            tmp[bb[d] + atomicAdd(cnt + d, 1u)] = make_uint2(v[f], (uint32_t)(base + e + f));
+        for (uint32_t e = 0; e < PER; ++e) {
+            const uint32_t j = (e / 4) * 4 * kBlk + 4 * threadIdx.x + (e % 4);
+            if (j < m) atomicAdd(lcnt + (v[e] >> shift), 1u);
         }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nbin; i += kBlk) loff[i] = lcnt[i];
+        __syncthreads();
+        block_scan_nt<kBlk>(loff, nbin, scr);
+        for (uint32_t i = threadIdx.x; i < nbin; i += kBlk) lcnt[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t e = 0; e < PER; ++e) {
+            const uint32_t j = (e / 4) * 4 * kBlk + 4 * threadIdx.x + (e % 4);
+            if (j < m) {
+                const uint32_t d = v[e] >> shift;
+                stage[loff[d] + atomicAdd(lcnt + d, 1u)] = make_uint2(v[e], (uint32_t)(base + j));
+            }
+        }
+        __syncthreads();
+        // write out in partition order: consecutive lanes -> consecutive addresses of a run
+        for (uint32_t j = threadIdx.x; j < m; j += kBlk) {
+            const uint2 e = stage[j];
+            const uint32_t d = e.x >> shift;
+            tmp[gbase[d] + (j - loff[d])] = e;
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nbin; i += kBlk) gbase[i] += lcnt[i];
+        __syncthreads();
     }
 }
 
@@ -140,21 +201,33 @@ __global__ __launch_bounds__(kP2Blk) void k_p2_buckets(const uint2* __restrict__
                                                       const uint32_t* __restrict__ pstart, uint32_t b1,
                                                       uint32_t b2, uint32_t perm_cap, uint32_t* __restrict__ dir,
                                                       uint2* __restrict__ pairs, uint64_t n) {
-    extern __shared__ uint32_t sh[];   // [cnt 2^b2 | offsets 2^b2 | scan scratch 1024 | perm]
+    extern __shared__ uint32_t sh[];   // [cnt 2^b2 | offsets 2^b2 | scan scratch kP2Blk | perm]
     const uint32_t p = blockIdx.x;
     const uint32_t nsub = 1u << b2, shift = 32 - b1 - b2, mask = nsub - 1u;
     uint32_t* cnt = sh;
     uint32_t* off = sh + nsub;
     uint32_t* scr = sh + 2 * nsub;
-    uint32_t* perm = scr + 1024;
+    uint32_t* perm = scr + kP2Blk;
     const uint32_t lo = pstart[p], hi = pstart[p + 1], m = hi - lo;
+    constexpr uint32_t BATCH = kP2Blk * kP2Per;
     for (uint32_t i = threadIdx.x; i < nsub; i += kP2Blk) cnt[i] = 0;
     __syncthreads();
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += kP2Blk) atomicAdd(cnt + ((tmp[i].x >> shift) & mask), 1u);
+    // histogram: each thread keeps kP2Per loads in flight per batch
+    for (uint32_t b = 0; b < m; b += BATCH) {
+        uint32_t key[kP2Per];
+#pragma unroll
+        for (int e = 0; e < kP2Per; ++e) {
+            const uint32_t j = b + e * kP2Blk + threadIdx.x;
+            key[e] = j < m ? tmp[lo + j].x : 0;
+        }
+#pragma unroll
+        for (int e = 0; e < kP2Per; ++e)
+            if (b + e * kP2Blk + threadIdx.x < m) atomicAdd(cnt + ((key[e] >> shift) & mask), 1u);
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nsub; i += kP2Blk) off[i] = cnt[i];
     __syncthreads();
-    block_scan_inplace(off, nsub, scr);
+    block_scan_nt<kP2Blk>(off, nsub, scr);
     for (uint32_t i = threadIdx.x; i < nsub; i += kP2Blk) {
         dir[((uint64_t)p << b2) + i] = lo + off[i];
         cnt[i] = 0;
@@ -162,19 +235,54 @@ __global__ __launch_bounds__(kP2Blk) void k_p2_buckets(const uint2* __restrict__
     if (p == gridDim.x - 1 && threadIdx.x == 0) dir[(uint64_t)gridDim.x << b2] = (uint32_t)n;
     __syncthreads();
     if (m <= perm_cap) {
-        // bucket permutation in LDS, then a gather (reads inside the partition's L2-resident
-        // slice) with coalesced writes
-        for (uint32_t j = threadIdx.x; j < m; j += kP2Blk) {
-            const uint32_t s = (tmp[lo + j].x >> shift) & mask;
-            perm[off[s] + atomicAdd(cnt + s, 1u)] = j;
+        // bucket permutation in LDS, then a gather (reads inside the partition's slice)
+        // with coalesced writes
+        for (uint32_t b = 0; b < m; b += BATCH) {
+            uint32_t key[kP2Per];
+#pragma unroll
+            for (int e = 0; e < kP2Per; ++e) {
+                const uint32_t j = b + e * kP2Blk + threadIdx.x;
+                key[e] = j < m ? tmp[lo + j].x : 0;
+            }
+#pragma unroll
+            for (int e = 0; e < kP2Per; ++e) {
+                const uint32_t j = b + e * kP2Blk + threadIdx.x;
+                if (j < m) {
+                    const uint32_t sb = (key[e] >> shift) & mask;
+                    perm[off[sb] + atomicAdd(cnt + sb, 1u)] = j;
+                }
+            }
         }
         __syncthreads();
-        for (uint32_t j = threadIdx.x; j < m; j += kP2Blk) pairs[lo + j] = tmp[lo + perm[j]];
+        for (uint32_t b = 0; b < m; b += BATCH) {
+            uint2 v[kP2Per];
+#pragma unroll
+            for (int e = 0; e < kP2Per; ++e) {
+                const uint32_t j = b + e * kP2Blk + threadIdx.x;
+                v[e] = j < m ? tmp[lo + perm[j]] : make_uint2(0, 0);
+            }
+#pragma unroll
+            for (int e = 0; e < kP2Per; ++e) {
+                const uint32_t j = b + e * kP2Blk + threadIdx.x;
+                if (j < m) pairs[lo + j] = v[e];
+            }
+        }
     } else {
-        for (uint32_t i = lo + threadIdx.x; i < hi; i += kP2Blk) {
-            const uint2 a = tmp[i];
-            const uint32_t s = (a.x >> shift) & mask;
-            pairs[lo + off[s] + atomicAdd(cnt + s, 1u)] = a;
+        for (uint32_t b = 0; b < m; b += BATCH) {
+            uint2 v[kP2Per];
+#pragma unroll
+            for (int e = 0; e < kP2Per; ++e) {
+                const uint32_t j = b + e * kP2Blk + threadIdx.x;
+                v[e] = j < m ? tmp[lo + j] : make_uint2(0, 0);
+            }
+#pragma unroll
+            for (int e = 0; e < kP2Per; ++e) {
+                const uint32_t j = b + e * kP2Blk + threadIdx.x;
+                if (j < m) {
+                    const uint32_t sb = (v[e].x >> shift) & mask;
+                    pairs[lo + off[sb] + atomicAdd(cnt + sb, 1u)] = v[e];
+                }
+            }
         }
     }
 }
@@ -212,28 +320,52 @@ __device__ __forceinline__ Cand load_cand(const uint2* __restrict__ pairs, uint3
 }
 
 // Append the `take` closest ids of bucket entries [lo, hi) (ascending) to the
-// lane-distributed result list at slots [base, base + take).
+// lane-distributed result list at slots [base, base + take).  `wl` is this wave's
+// 64-entry LDS scratch (u64).
 __device__ void select_range(const uint2* __restrict__ pairs, uint32_t lo, uint32_t hi,
                              const uint32_t* __restrict__ planes, uint64_t stride, const uint32_t* t,
-                             uint32_t take, uint32_t base, uint32_t lane, uint32_t& res) {
+                             uint32_t take, uint32_t base, uint32_t lane, uint32_t& res,
+                             unsigned long long* wl) {
     const uint32_t m = hi - lo;
     if (m <= 64) {
+        // packed key (w0 distance << 32 | idx); rank = number of smaller keys, read from LDS
         const Cand mine = lane < m ? load_cand(pairs, lo + lane, t[0]) : cand_none();
-        uint32_t rank = 0;
-        for (uint32_t o = 0; o < m; ++o) {
-            const Cand other = cand_readlane(mine, o);
-            if (other.d0 < mine.d0) ++rank;
-            else if (other.d0 == mine.d0 && o != lane && lane < m) rank += cand_less(other, mine, planes, stride, t);
+        const unsigned long long key = ((unsigned long long)mine.d0 << 32) | mine.idx;
+        wl[lane] = key;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        uint32_t rank = 0, eq = 0;
+        uint32_t o = 0;
+        for (; o + 4 <= m; o += 4) {
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const unsigned long long ko = wl[o + u];
+                rank += ko < key;
+                eq += (uint32_t)(ko >> 32) == mine.d0;
+            }
         }
-        const bool keep = lane < m && rank < take;
-        uint64_t km = __ballot(keep);
-        while (km) {
-            const uint32_t l = (uint32_t)__ffsll((long long)km) - 1;
-            km &= km - 1;
-            const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rank, l);
-            const uint32_t id = (uint32_t)__builtin_amdgcn_readlane((int)mine.idx, l);
-            if (lane == base + r) res = id;
+        for (; o < m; ++o) {
+            const unsigned long long ko = wl[o];
+            rank += ko < key;
+            eq += (uint32_t)(ko >> 32) == mine.d0;
         }
+        if (__ballot(lane < m && eq > 1)) {
+            // equal w0 distances (rare): exact rank by the full 160-bit key
+            rank = 0;
+            for (uint32_t q2 = 0; q2 < m; ++q2) {
+                const unsigned long long ko = wl[q2];
+                const Cand other{(uint32_t)(ko >> 32), (uint32_t)ko};
+                if (lane < m && q2 != lane) rank += cand_less(other, mine, planes, stride, t);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // route: the candidate of rank r (< take) goes to result slot base + r
+        uint32_t* slot = reinterpret_cast<uint32_t*>(wl);
+        if (lane < m && rank < take) slot[base + rank] = mine.idx;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        if (lane >= base && lane < base + take) res = slot[lane];
+        __builtin_amdgcn_wave_barrier();
         return;
     }
     // large range (clustered inputs): running lane-distributed top-`take` list
@@ -267,8 +399,11 @@ __global__ __launch_bounds__(256) void k_query(const uint2* __restrict__ pairs, 
                                               uint64_t stride, const uint32_t* __restrict__ tp, uint64_t ts,
                                               uint32_t q, uint32_t k, uint32_t* __restrict__ out_idx,
                                               uint32_t* __restrict__ out_cnt) {
+    __shared__ unsigned long long wls[4 * 64];
     const uint32_t lane = lane_id();
-    const uint32_t qi = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const uint32_t wv = threadIdx.x >> 6;
+    unsigned long long* wl = wls + 64 * wv;
+    const uint32_t qi = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
     if (qi >= q) return;
     uint32_t t[DHT_W];
 #pragma unroll
@@ -297,7 +432,7 @@ __global__ __launch_bounds__(256) void k_query(const uint2* __restrict__ pairs, 
         const uint32_t tlo = (uint32_t)__builtin_amdgcn_readlane((int)lo, x - 1);
         const uint32_t thi = (uint32_t)__builtin_amdgcn_readlane((int)hi, x - 1);
         if (lp == B || thi - tlo <= 64) {
-            select_range(pairs, tlo, thi, planes, stride, t, need, got, lane, res);
+            select_range(pairs, tlo, thi, planes, stride, t, need, got, lane, res, wl);
             got += need;
             break;
         }
@@ -305,7 +440,7 @@ __global__ __launch_bounds__(256) void k_query(const uint2* __restrict__ pairs, 
         // whole (every id in it is closer than the rest), continue in the sibling subtree
         const uint32_t clo = (uint32_t)__builtin_amdgcn_readlane((int)lo, x);
         const uint32_t chi = (uint32_t)__builtin_amdgcn_readlane((int)hi, x);
-        if (chi > clo) select_range(pairs, clo, chi, planes, stride, t, chi - clo, got, lane, res);
+        if (chi > clo) select_range(pairs, clo, chi, planes, stride, t, chi - clo, got, lane, res, wl);
         got += chi - clo;
         p0 ^= 0x80000000u >> lp;
         L = lp + 1;
@@ -326,19 +461,25 @@ uint32_t index_bits(uint64_t n) {
 }
 
 static void index_split(uint64_t n, uint32_t B, uint32_t& b1, uint32_t& b2) {
-    // partitions of ~2^14 ids so that a partition's bucket permutation fits LDS
+    // partitions of ~2^14 ids: one register batch of a 1024-thread pass-2 block, and an
+    // LDS permutation of <= 84 KB; b1, b2 <= 12 keep every LDS histogram within 32 KB
     uint32_t lg = 0;
     while (lg < 63 && (1ull << lg) < n) ++lg;
     int x = (int)lg - 14;
-    if (x < (int)B - 12) x = (int)B - 12;   // b2 <= 12
+    if (x < (int)B - 12) x = (int)B - 12;
     if (x > 12) x = 12;
-    if (x < 1) x = 1;
     if (x > (int)B) x = (int)B;
+    if (x < 1) x = 1;   // B >= 1 (index_bits)
     b1 = (uint32_t)x;
     b2 = B - b1;
 }
 
-static uint32_t p1_blocks(uint64_t n) { return (uint32_t)((n + kP1Tile - 1) / kP1Tile); }
+static uint32_t p1_tile(uint64_t n) {
+    uint64_t t = kP1Tile;
+    while ((n + t - 1) / t > 2048) t += kP1Tile;
+    return (uint32_t)t;
+}
+static uint32_t p1_blocks(uint64_t n) { return (uint32_t)((n + p1_tile(n) - 1) / p1_tile(n)); }
 
 // workspace: pairs (n x 8 B) | dir (2^B + 1) | tmp (n x 8 B) | H | pcount | pstart
 size_t index_bytes(uint64_t n, uint32_t B) {
@@ -372,11 +513,12 @@ hipError_t launch_index_build(const uint32_t* planes, uint64_t stride, uint64_t 
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k_p2_buckets, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
+        (void)hipFuncSetAttribute((const void*)k_p1_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
         attr_set = true;
     }
     if (ev) (void)hipEventRecord(ev[0], s);
     if (n) {
-        k_p0_hist<<<nblk, kBlk, np * 4, s>>>(planes, n, b1, nblk, H);
+        k_p0_hist<<<nblk, kBlk, np * 4, s>>>(planes, n, b1, nblk, p1_tile(n), H);
         if (ev) (void)hipEventRecord(ev[1], s);
         k_p0_rowscan<<<(uint32_t)np, 1024, 0, s>>>(H, nblk, pcount);
     } else {
@@ -386,11 +528,14 @@ hipError_t launch_index_build(const uint32_t* planes, uint64_t stride, uint64_t 
     }
     k_p0_scan<<<1, 1024, 0, s>>>(pcount, (uint32_t)np, pstart, n);
     if (ev) (void)hipEventRecord(ev[2], s);
-    if (n) k_p1_scatter<<<nblk, kBlk, np * 8, s>>>(planes, n, b1, nblk, H, pstart, tmp);
+    if (n)
+        k_p1_scatter<<<nblk, kBlk, (3 * np + kBlk) * 4 + kP1Stage * 8, s>>>(planes, n, b1, nblk, p1_tile(n), H,
+                                                                          pstart, tmp);
     if (ev) (void)hipEventRecord(ev[3], s);
-    // LDS: fixed part + a permutation sized ~3x the average partition (cap: 160 KB)
-    const uint32_t fixed = ((2u << b2) + 1024) * 4;
-    uint64_t cap = 3 * ((n >> b1) + 1) + 1024;
+    // LDS: fixed part + a permutation sized 1.25x the average partition + 512 (several
+    // blocks per CU); larger partitions (clustered inputs) take the scatter path
+    const uint32_t fixed = ((2u << b2) + kP2Blk) * 4;
+    uint64_t cap = (n >> b1) + (n >> b1) / 4 + 512;
     if (cap > (kLdsMax - fixed) / 4) cap = (kLdsMax - fixed) / 4;
     k_p2_buckets<<<(uint32_t)np, kP2Blk, fixed + (uint32_t)cap * 4, s>>>(tmp, pstart, b1, b2, (uint32_t)cap, dir,
                                                                         pairs, n);
