@@ -7,9 +7,13 @@ One step = one batched lookup of all targets against the whole id set.  Ids and
 targets are generated in HBM before timing (synthetic splitmix64 stream).
 
 Algorithms (--algo):
+  batch  K6 per-batch target-prefix filter (default): every step streams the raw id word
+         plane w0 once, keeps the ids sharing a level-Lm prefix with some target of the
+         batch, and answers each target exactly from its complete prefix subtree in LDS
   index  K4 bucket-index build + K5 trie-descent query; the index is REBUILT from the raw
-         id planes inside every timed step (default)
+         id planes inside every timed step
   scan   K1 brute-force streaming scan (the north-star kernel design)
+Nothing is cached between steps in any algorithm.
 
 Multi-GPU (one process per GPU, torch.distributed over RCCL; --route):
   prefix     (default for a power-of-two world) ids AND targets are partitioned by their
@@ -62,7 +66,7 @@ def parse():
     ap.add_argument("--q", type=int, default=65536, help="targets per step (total over all ranks)")
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--seed", type=int, default=2024)
-    ap.add_argument("--algo", choices=["index", "scan"], default="index")
+    ap.add_argument("--algo", choices=["batch", "index", "scan"], default="batch")
     ap.add_argument("--route", choices=["auto", "prefix", "broadcast"], default="auto")
     ap.add_argument("--sharded", action="store_true",
                     help="use the multi-GPU code path (and its collectives) even with one rank")
@@ -103,7 +107,7 @@ def main():
     pow2 = lambda g: g > 0 and (g & (g - 1)) == 0
     route = a.route
     if route == "auto":
-        route = "prefix" if (a.algo == "index" and pow2(world)) else "broadcast"
+        route = "prefix" if (a.algo in ("index", "batch") and pow2(world)) else "broadcast"
     if a.simulate_world:
         assert world == 1 and route == "prefix" and pow2(a.simulate_world)
     use_dist = world > 1 or a.sharded
@@ -157,7 +161,9 @@ def main():
     gathered = torch.empty((world * a.q, a.k, 6), dtype=torch.int32, device=dev) if collective else None
 
     def local_lookup(out_i, out_c, out_r, base):
-        if a.algo == "index":
+        if a.algo == "batch":
+            ctx.batch_topk_dev(tp.data_ptr(), ts, q_local, a.k, out_i, out_c, out_r, base, stream)
+        elif a.algo == "index":
             ctx.index_build(stream)          # the index is rebuilt from the raw id planes every step
             ctx.index_topk_dev(tp.data_ptr(), ts, q_local, a.k, out_i, out_c, out_r, base, stream)
         else:
@@ -209,7 +215,30 @@ def main():
         return e0.elapsed_time(e1) / reps
 
     reps = max(3, min(a.steps, 20))
-    if a.algo == "index":
+    if a.algo == "batch":
+        # per-kernel device times (HIP events between F1..F4 on the bench stream)
+        runs = [ctx.batch_topk_timed(tp.data_ptr(), ts, q_local, a.k, out_idx.data_ptr(), out_cnt.data_ptr(), stream)
+                for _ in range(reps)]
+        ph = [sum(r[0][i] for r in runs) / reps for i in range(4)]
+        n_fb, surv = runs[-1][1], runs[-1][2]
+        kern = {"k_f1_targets": (ph[0], 12 * q_local),
+                "k_f2_filter": (ph[1], 4 * n_local + 8 * surv),
+                "k_f3_answer": (ph[2], 8 * surv + q_local * (8 + 16 + 4 * a.k + 4)),
+                "k_f4_fallback": (ph[3], 0)}
+        dom = max(kern, key=lambda k: kern[k][0])
+        dom_ms, dom_bytes = kern[dom]
+        step_bytes = sum(v[1] for v in kern.values())
+        roof = {"bound": "hbm", "achieved": dom_bytes / (dom_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                "kernel": dom, "kernel_ms": dom_ms, "alg_bytes_per_launch": dom_bytes,
+                "kernels_ms": {k: v[0] for k, v in kern.items()},
+                "step_alg_bytes": step_bytes,
+                "step_hbm_frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                # SURVEY 8(d) contract bytes (every id read whole, 20 B) and their time at peak
+                "contract_bytes": n_local * 20 + q_local * 20 + q_local * a.k * 4,
+                "contract_floor_ms": (n_local * 20 + q_local * 20 + q_local * a.k * 4) / HBM_PEAK_GBS / 1e6}
+        extra = {"survivors": surv, "survivor_frac": surv / max(n_local, 1), "fallback_targets": n_fb}
+    elif a.algo == "index":
         # per-kernel device times of the index build (HIP events between its kernels, on
         # the bench stream) and of the query kernel alone
         phases = [ctx.index_build_timed(stream) for _ in range(reps)]
@@ -241,7 +270,7 @@ def main():
                 "ops_per_pair": OPS_PER_PAIR, "pairs_per_launch": pairs,
                 "hbm_alg_bytes_per_launch": n_local * 20 + q_local * 20 + q_local * a.k * 4}
         extra = {}
-    if a.algo == "index" and not a.no_scan and world == 1 and not a.simulate_world:
+    if a.algo != "scan" and not a.no_scan and world == 1 and not a.simulate_world:
         # the north-star brute-force scan (K1) on the same inputs, for reference
         sc_ms = ev_time(lambda: ctx.topk_dev(tp.data_ptr(), ts, q_local, a.k, out_idx.data_ptr(),
                                              out_cnt.data_ptr(), None, 0, stream), 3)

@@ -134,6 +134,26 @@ int dhtgpu_index_topk_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_
 int dhtgpu_index_topk(dhtgpu_ctx* ctx, const uint8_t* targets20_be, uint32_t q, uint32_t k,
                       uint32_t* out_idx, uint32_t* out_cnt);
 
+/* ---- K6: per-batch target-prefix filter + exact top-k (same results as dhtgpu_topk) ---- */
+/* Nothing persists between calls: each call streams the id word plane w0 once, keeps only
+ * the ids that share the batch targets' level-Lm prefixes (Lm ~ log2(n / 4k)), and answers
+ * every target from its complete prefix subtree in LDS; targets whose subtree holds fewer
+ * than min(k, n) ids take an exact brute-force pass.  Same output forms as
+ * dhtgpu_topk_dev.  DHTGPU_ERANGE when n > 2^28 or q > 2^22 (use dhtgpu_index_topk_dev).
+ * Stream-ordered, no host sync. */
+int dhtgpu_batch_topk_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
+                          uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec,
+                          uint32_t idx_base, void* stream);
+/* Diagnostics: the same call with HIP events between its kernels; synchronises and returns
+ * per-phase device milliseconds ms4 = {F1 mark targets, F2 filter ids, F3 answer,
+ * F4 fallback} and (nullable) stats2 = {targets answered by the fallback, surviving ids}. */
+int dhtgpu_batch_topk_timed(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
+                            uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, void* stream, float* ms4,
+                            uint32_t* stats2);
+/* Host form (synchronous). */
+int dhtgpu_batch_topk(dhtgpu_ctx* ctx, const uint8_t* targets20_be, uint32_t q, uint32_t k,
+                      uint32_t* out_idx, uint32_t* out_cnt);
+
 /* ---- K1r: RoutingTable::findClosestNodes over a table snapshot ------------------ */
 /* Snapshot: nb buckets in list order with firsts20[nb*20] (Bucket::first),
  * bucket_off[nb+1] (bucket b owns nodes [off[b], off[b+1]) of node_ids20), and

@@ -89,6 +89,11 @@ def lib():
                                    ctypes.c_uint32], ctypes.c_int),
         "dhtgpu_select_prefix_dev": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                       _vp, ctypes.c_uint64, _vp, _u64p, _vp], ctypes.c_int),
+        "dhtgpu_batch_topk_dev": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp,
+                                   ctypes.c_uint32, _vp], ctypes.c_int),
+        "dhtgpu_batch_topk_timed": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp,
+                                     ctypes.POINTER(ctypes.c_float), _u32p], ctypes.c_int),
+        "dhtgpu_batch_topk": ([_vp, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -105,7 +110,8 @@ def exported_symbols():
             "dhtgpu_ids_dev", "dhtgpu_topk", "dhtgpu_topk_dev", "dhtgpu_merge_dev", "dhtgpu_pack_dev",
             "dhtgpu_gen_dev", "dhtgpu_find_closest", "dhtgpu_classify", "dhtgpu_classify_dev",
             "dhtgpu_cached_nodes", "dhtgpu_index_build", "dhtgpu_index_topk_dev", "dhtgpu_index_topk",
-            "dhtgpu_index_build_timed", "dhtgpu_gen_ids_prefix", "dhtgpu_select_prefix_dev"]
+            "dhtgpu_index_build_timed", "dhtgpu_gen_ids_prefix", "dhtgpu_select_prefix_dev",
+            "dhtgpu_batch_topk_dev", "dhtgpu_batch_topk_timed", "dhtgpu_batch_topk"]
 
 
 def _ids(a, name="ids"):
@@ -225,6 +231,29 @@ class Context:
                        idx_base=0, stream=None):
         _check(lib().dhtgpu_index_topk_dev(self._h, t_planes_ptr, t_stride, q, k, out_idx_ptr, out_cnt_ptr,
                                            out_rec_ptr, idx_base, stream), "index_topk_dev")
+
+    def batch_topk(self, targets, k=8):
+        """Same result as topk() through the K6 per-batch target-prefix filter."""
+        t = _ids(targets, "targets")
+        q = t.shape[0]
+        out = np.empty((q, k), dtype=np.uint32)
+        cnt = np.empty(q, dtype=np.uint32)
+        _check(lib().dhtgpu_batch_topk(self._h, _p(t, _u8p), q, k, _p(out, _u32p), _p(cnt, _u32p)), "batch_topk")
+        return out, cnt
+
+    def batch_topk_dev(self, t_planes_ptr, t_stride, q, k, out_idx_ptr=None, out_cnt_ptr=None, out_rec_ptr=None,
+                       idx_base=0, stream=None):
+        _check(lib().dhtgpu_batch_topk_dev(self._h, t_planes_ptr, t_stride, q, k, out_idx_ptr, out_cnt_ptr,
+                                           out_rec_ptr, idx_base, stream), "batch_topk_dev")
+
+    def batch_topk_timed(self, t_planes_ptr, t_stride, q, k, out_idx_ptr, out_cnt_ptr, stream=None):
+        """One K6 call with HIP events between its kernels; returns (device ms per phase
+        (F1 mark targets, F2 filter ids, F3 answer, F4 fallback), fallback targets, survivors)."""
+        ms = (ctypes.c_float * 4)()
+        st = (ctypes.c_uint32 * 2)()
+        _check(lib().dhtgpu_batch_topk_timed(self._h, t_planes_ptr, t_stride, q, k, out_idx_ptr, out_cnt_ptr,
+                                             stream, ms, st), "batch_topk_timed")
+        return tuple(ms), int(st[0]), int(st[1])
 
     def topk_dev(self, t_planes_ptr, t_stride, q, k, out_idx_ptr=None, out_cnt_ptr=None, out_rec_ptr=None,
                  idx_base=0, stream=None):

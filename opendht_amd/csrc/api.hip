@@ -68,6 +68,8 @@ struct dhtgpu_ctx {
     DevBuf index;           // K4 workspace: entries | directory | partition scratch
     uint32_t index_B = 0;
     bool index_valid = false;
+    DevBuf batch;           // K6 workspace; its 64 KB bitmap head is all-zero between calls
+    bool batch_clean = false;
 
     hipError_t bind() { return hipSetDevice(device); }
 
@@ -134,7 +136,7 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
     (void)c->bind();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->planes, &c->staging, &c->targets, &c->out_idx, &c->out_cnt, &c->rec,
-                      &c->aux, &c->aux2, &c->aux3, &c->index, &c->gidx})
+                      &c->aux, &c->aux2, &c->aux3, &c->index, &c->gidx, &c->batch})
         b->release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -430,6 +432,84 @@ int dhtgpu_index_topk(dhtgpu_ctx* c, const uint8_t* t20, uint32_t q, uint32_t k,
     DHT_TRY(c->aux3.ensure((size_t)q * 4));
     int r = dhtgpu_index_topk_dev(c, c->targets.as<uint32_t>(), ts, q, k, c->aux2.as<uint32_t>(),
                                   c->aux3.as<uint32_t>(), nullptr, 0, c->stream);
+    if (r) return r;
+    DHT_TRY(hipMemcpyAsync(out_idx, c->aux2.p, (size_t)q * k * 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(out_cnt, c->aux3.p, (size_t)q * 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    return DHTGPU_OK;
+}
+
+static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k, uint32_t* out_idx,
+                     uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base, hipStream_t s, hipEvent_t* ev) {
+    if (!batch_supported(c->n, q, k)) return DHTGPU_ERANGE;
+    const size_t need = batch_bytes(c->n, q, k);
+    if (need > c->batch.cap) c->batch_clean = false;
+    DHT_TRY(c->batch.ensure(need));
+    if (!c->batch_clean) DHT_TRY(hipMemsetAsync(c->batch.p, 0, 65536 + 256, s));
+    c->batch_clean = false;   // re-established below once every launch went through
+    const uint32_t* gidx = c->has_gidx ? c->gidx.as<uint32_t>() : nullptr;
+    uint32_t* li = out_idx;
+    uint32_t* lc = out_cnt;
+    if (out_rec) {   // local indices first, then candidate records for a cross-shard merge
+        DHT_TRY(c->out_idx.ensure((size_t)q * k * 4));
+        DHT_TRY(c->out_cnt.ensure((size_t)q * 4));
+        li = c->out_idx.as<uint32_t>();
+        lc = c->out_cnt.as<uint32_t>();
+    }
+    DHT_TRY(launch_batch_topk(c->batch.p, c->planes.as<uint32_t>(), c->stride, c->n, tp, ts, q, k,
+                              out_rec ? nullptr : gidx, out_rec ? 0u : idx_base, li, lc, s, ev));
+    if (out_rec)
+        DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
+                                    out_rec, s));
+    c->batch_clean = true;
+    return DHTGPU_OK;
+}
+
+int dhtgpu_batch_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k,
+                          uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base,
+                          void* stream) {
+    if (!c || k == 0 || k > DHTGPU_MAX_K || (q && !tp)) return DHTGPU_EINVAL;
+    if (!out_rec && (!out_idx || !out_cnt)) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    return batch_run(c, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base,
+                     stream ? (hipStream_t)stream : c->stream, nullptr);
+}
+
+int dhtgpu_batch_topk_timed(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k,
+                            uint32_t* out_idx, uint32_t* out_cnt, void* stream, float* ms4, uint32_t* stats2) {
+    if (!c || !ms4 || k == 0 || k > DHTGPU_MAX_K || !q || !tp || !out_idx || !out_cnt) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    DHT_TRY(c->bind());
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipEvent_t ev[5];
+    for (int i = 0; i < 5; ++i) DHT_TRY(hipEventCreate(&ev[i]));
+    int r = batch_run(c, tp, ts, q, k, out_idx, out_cnt, nullptr, 0, s, ev);
+    hipError_t e = r ? hipSuccess : hipEventSynchronize(ev[4]);
+    for (int i = 0; !r && e == hipSuccess && i < 4; ++i) e = hipEventElapsedTime(&ms4[i], ev[i], ev[i + 1]);
+    for (int i = 0; i < 5; ++i) (void)hipEventDestroy(ev[i]);
+    if (r) return r;
+    DHT_TRY(e);
+    if (stats2) {
+        DHT_TRY(hipMemcpyAsync(stats2, batch_stats(c->batch.p), 8, hipMemcpyDeviceToHost, s));
+        DHT_TRY(hipStreamSynchronize(s));
+    }
+    return DHTGPU_OK;
+}
+
+int dhtgpu_batch_topk(dhtgpu_ctx* c, const uint8_t* t20, uint32_t q, uint32_t k, uint32_t* out_idx,
+                      uint32_t* out_cnt) {
+    if (!c || k == 0 || k > DHTGPU_MAX_K || (q && (!t20 || !out_idx || !out_cnt))) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    uint64_t ts = 0;
+    DHT_TRY(c->upload_targets(t20, q, &ts));
+    DHT_TRY(c->aux2.ensure((size_t)q * k * 4));
+    DHT_TRY(c->aux3.ensure((size_t)q * 4));
+    int r = batch_run(c, c->targets.as<uint32_t>(), ts, q, k, c->aux2.as<uint32_t>(), c->aux3.as<uint32_t>(),
+                      nullptr, 0, c->stream, nullptr);
     if (r) return r;
     DHT_TRY(hipMemcpyAsync(out_idx, c->aux2.p, (size_t)q * k * 4, hipMemcpyDeviceToHost, c->stream));
     DHT_TRY(hipMemcpyAsync(out_cnt, c->aux3.p, (size_t)q * 4, hipMemcpyDeviceToHost, c->stream));

@@ -11,6 +11,7 @@
 
 #define DHT_W 5
 #define DHT_NONE 0xFFFFFFFFu
+#define DHTGPU_MAX_K_DEV 32u   // = DHTGPU_MAX_K of include/dhtgpu.h
 
 namespace dhtgpu {
 

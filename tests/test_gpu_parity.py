@@ -17,10 +17,11 @@ def ctx():
 
 
 def check_topk(ctx, ids, targets, k):
-    """K1 (scan) and K4/K5 (bucket index) both bit-exact vs std::partial_sort(xorCmp)."""
+    """K1 (scan), K4/K5 (bucket index) and K6 (batch prefix filter) all bit-exact vs
+    std::partial_sort(xorCmp)."""
     ctx.set_ids(ids)
     want, wcnt = O.topk(ids, targets, k)
-    for name, fn in (("scan", ctx.topk), ("index", ctx.index_topk)):
+    for name, fn in (("scan", ctx.topk), ("index", ctx.index_topk), ("batch", ctx.batch_topk)):
         got, gcnt = fn(targets, k)
         assert np.array_equal(gcnt, wcnt), name
         bad = np.nonzero((got != want).any(axis=1))[0]
@@ -108,7 +109,7 @@ def test_topk_2p24_sample(ctx):
     ctx.gen_ids(2024, n)
     tg = O.gen_ids(2025, 48)
     want, wcnt = O.topk(O.gen_ids(2024, n), tg, 8)
-    for fn in (ctx.topk, ctx.index_topk):
+    for fn in (ctx.topk, ctx.index_topk, ctx.batch_topk):
         got, cnt = fn(tg, 8)
         assert np.array_equal(cnt, wcnt) and np.array_equal(got, want)
 
@@ -122,6 +123,8 @@ def test_index_vs_scan_full_batch(ctx):
     b, cb = ctx.index_topk(tg, 8)
     assert np.array_equal(ca, cb) and np.array_equal(a, b)
     assert np.all(ca == 8)
+    c, cc = ctx.batch_topk(tg, 8)
+    assert np.array_equal(ca, cc) and np.array_equal(a, c)
 
 
 @pytest.mark.parametrize("expired,cluster", [(0.0, False), (0.3, False), (0.6, False), (0.3, True)])
@@ -248,7 +251,7 @@ def test_prefix_shard_matches_global_topk(ctx, pbits, pval):
     assert ctx.num_ids == shard.shape[0]
     assert np.array_equal(ctx.get_ids(), shard)
     want, wcnt = O.topk(ids, mine, 8)
-    for fn in (ctx.topk, ctx.index_topk):
+    for fn in (ctx.topk, ctx.index_topk, ctx.batch_topk):
         got, cnt = fn(mine, 8)
         assert np.array_equal(cnt, wcnt) and np.array_equal(got, want)
 
@@ -269,3 +272,72 @@ def test_select_prefix_dev(ctx):
     assert np.array_equal(gidx[:m].cpu().numpy().view(np.uint32), sel.astype(np.uint32))
     words = out.view(5, stride)[:, :m].cpu().numpy().view(np.uint32).T
     assert np.array_equal(words, ids[sel].view(">u4").reshape(-1, 5).astype(np.uint32))
+
+
+@pytest.mark.parametrize("n,q", [(20000, 200000), (300000, 64), (1 << 20, 70000)])
+def test_batch_filter_regimes(ctx, n, q):
+    """K6 across its regimes: nearly every id survives the filter (q >> 2^Lm), very few
+    survive (q small), and the cfg-2 shape scaled down; checked on a target sample vs the
+    oracle and on the whole batch vs the K1 scan."""
+    ids = O.gen_ids(300 + q, n)
+    tg = O.gen_ids(301 + q, q)
+    ctx.set_ids(ids)
+    got, cnt = ctx.batch_topk(tg, 8)
+    sc, scnt = ctx.topk(tg, 8)
+    assert np.array_equal(cnt, scnt) and np.array_equal(got, sc)
+    sample = np.arange(0, q, max(1, q // 300))
+    want, wcnt = O.topk(ids, tg[sample], 8)
+    assert np.array_equal(got[sample], want) and np.array_equal(cnt[sample], wcnt)
+
+
+def test_batch_clustered_targets_and_fallback(ctx):
+    """All targets inside one prefix partition; sparse subtrees that force the exact
+    brute-force fallback (subtree smaller than k); repeated calls (the prefix bitmap
+    must be all-zero again after every call)."""
+    ids = O.gen_ids(401, 50000)
+    tg = O.gen_ids(402, 3000)
+    tg[:, :2] = 0xA7                     # 16 shared leading bits: one partition
+    ctx.set_ids(ids)
+    for k in (8, 32):
+        got, cnt = ctx.batch_topk(tg, k)
+        want, wcnt = O.topk(ids, tg, k)
+        assert np.array_equal(cnt, wcnt) and np.array_equal(got, want)
+    # ids confined to a narrow prefix: most targets' level-Lm subtrees are empty
+    ids2 = O.gen_ids(403, 40000)
+    ids2[:, 0] = 0x3C
+    tg2 = np.concatenate([O.gen_ids(404, 200), ids2[:50]])
+    check_topk(ctx, ids2, tg2, 8)
+    check_topk(ctx, ids, tg[:100], 14)    # a different batch on the first set again
+
+
+def test_batch_records_merge(ctx):
+    """K6 record mode over 3 id shards + K3 merge == one flat top-k."""
+    import torch
+    import opendht_amd
+    ids = O.gen_ids(501, 90000)
+    q, k = 700, 8
+    tg = O.gen_ids(502, q)
+    dev = torch.device("cuda", 0)
+    ts = 704
+    tp = torch.zeros(5 * ts, dtype=torch.int32, device=dev)
+    L = opendht_amd.lib()
+    assert L.dhtgpu_pack_dev(torch.from_numpy(tg.reshape(-1)).to(dev).data_ptr(), q, tp.data_ptr(), ts, None) == 0
+    bounds = [0, 20000, 61000, 90000]
+    rec = torch.empty((3, q, k, 6), dtype=torch.int32, device=dev)
+    shards = []
+    for s in range(3):
+        c = opendht_amd.Context(0)
+        c.set_ids(ids[bounds[s]:bounds[s + 1]])
+        c.batch_topk_dev(tp.data_ptr(), ts, q, k, None, None, rec[s].data_ptr(), bounds[s], c.stream)
+        torch.cuda.synchronize()
+        shards.append(c)
+    out = torch.empty((q, k), dtype=torch.int32, device=dev)
+    cnt = torch.empty(q, dtype=torch.int32, device=dev)
+    assert L.dhtgpu_merge_dev(rec.data_ptr(), 3, q, k, tp.data_ptr(), ts, k, out.data_ptr(), cnt.data_ptr(),
+                              None) == 0
+    torch.cuda.synchronize()
+    want, wcnt = O.topk(ids, tg, k)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    assert np.array_equal(cnt.cpu().numpy().view(np.uint32), wcnt)
+    for c in shards:
+        c.close()
