@@ -441,8 +441,8 @@ int dhtgpu_index_topk(dhtgpu_ctx* c, const uint8_t* t20, uint32_t q, uint32_t k,
 
 static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k, uint32_t* out_idx,
                      uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base, hipStream_t s, hipEvent_t* ev) {
-    if (!batch_supported(c->n, q, k)) return DHTGPU_ERANGE;
-    const size_t need = batch_bytes(c->n, q, k);
+    if (!batch_supported(c->n, q, k, c->num_cus)) return DHTGPU_ERANGE;
+    const size_t need = batch_bytes(c->n, q, k, c->num_cus);
     if (need > c->batch.cap) c->batch_clean = false;
     DHT_TRY(c->batch.ensure(need));
     if (!c->batch_clean) DHT_TRY(hipMemsetAsync(c->batch.p, 0, 65536 + 256, s));
@@ -457,7 +457,7 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
         lc = c->out_cnt.as<uint32_t>();
     }
     DHT_TRY(launch_batch_topk(c->batch.p, c->planes.as<uint32_t>(), c->stride, c->n, tp, ts, q, k,
-                              out_rec ? nullptr : gidx, out_rec ? 0u : idx_base, li, lc, s, ev));
+                              out_rec ? nullptr : gidx, out_rec ? 0u : idx_base, li, lc, c->num_cus, s, ev));
     if (out_rec)
         DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
                                     out_rec, s));

@@ -34,6 +34,7 @@
 #include "dhtgpu_internal.h"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace dhtgpu {
 namespace {
@@ -41,16 +42,11 @@ namespace {
 constexpr int kF1Threads = 256;
 constexpr int kF1Per = 4;
 constexpr uint32_t kF1Chunk = kF1Threads * kF1Per;   // targets per F1 block
-constexpr int kF2Threads = 1024;
-constexpr int kF2Per = 32;
-constexpr uint32_t kF2Chunk = kF2Threads * kF2Per;   // ids per F2 block (kept in registers)
-constexpr int kF3Threads = 1024;
-constexpr uint32_t kF3Cap = 8192;                    // survivors per partition staged in LDS
-constexpr int kF3Per = kF3Cap / kF3Threads;
+constexpr int kF3Threads = 256;
+constexpr uint32_t kF3Cap = 4096;                    // survivors per partition staged in LDS
 constexpr int kF4Threads = 256;
 constexpr uint32_t kMaxLm = 19;                      // 2^19-bit bitmap = 64 KB of LDS in F2
 constexpr uint32_t kMaxSubBits = 11;                 // F3 sub-prefix histogram <= 2048 bins
-constexpr uint32_t kMaxBlk2 = 8192;                  // F2 blocks (n <= 2^28)
 constexpr uint32_t kMaxBlk1 = 4096;                  // F1 blocks (q <= 2^22)
 constexpr uint32_t kLdsMax = 160 * 1024;
 
@@ -119,7 +115,7 @@ __global__ __launch_bounds__(kF1Threads) void k_f1_targets(const uint32_t* __res
     uint32_t* hist = sh;
     uint32_t* wsum = sh + np + 1;
     for (uint32_t i = threadIdx.x; i <= np; i += kF1Threads) hist[i] = 0;
-    if (blockIdx.x == 0 && threadIdx.x < 2) fb_count[threadIdx.x] = 0;   // fallback count, survivor count
+    if (blockIdx.x == 0 && threadIdx.x < 4) fb_count[threadIdx.x] = 0;   // fallback, survivors, runs
     __syncthreads();
     const uint32_t base = blockIdx.x * kF1Chunk;
     const uint32_t m = q - base < kF1Chunk ? q - base : kF1Chunk;
@@ -148,61 +144,155 @@ __global__ __launch_bounds__(kF1Threads) void k_f1_targets(const uint32_t* __res
 }
 
 // ---- F2: stream w0, keep ids in marked subtrees, partition them ----------------------
-__global__ __launch_bounds__(kF2Threads) void k_f2_filter(const uint32_t* __restrict__ w0, uint64_t n, uint32_t Lm,
-                                                         uint32_t b1, const uint32_t* __restrict__ bitmap,
-                                                         uint32_t nwords, uint32_t* __restrict__ tab2,
-                                                         uint32_t nblk2, uint2* __restrict__ ireg) {
-    extern __shared__ uint32_t sh[];   // bm[nwords] | hist[np + 1] | wsum
-    const uint32_t np = 1u << b1;
-    uint32_t* bm = sh;
-    uint32_t* hist = sh + nwords;
-    uint32_t* wsum = hist + np + 1;
-    const uint64_t base = (uint64_t)blockIdx.x * kF2Chunk;
-    const uint32_t m = (uint32_t)(n - base < kF2Chunk ? n - base : kF2Chunk);
-    // id loads first (16 B per lane, all in flight), then the bitmap copy
-    uint32_t v[kF2Per];
-#pragma unroll
-    for (int e = 0; e < kF2Per / 4; ++e) {
-        const uint32_t j = e * 4 * kF2Threads + 4 * threadIdx.x;
-        if (j + 3 < m) {
-            const uint4 x = *reinterpret_cast<const uint4*>(w0 + base + j);
-            v[4 * e] = x.x; v[4 * e + 1] = x.y; v[4 * e + 2] = x.z; v[4 * e + 3] = x.w;
-        } else {
-#pragma unroll
-            for (int f = 0; f < 4; ++f) v[4 * e + f] = j + f < m ? w0[base + j + f] : 0u;
-        }
-    }
-    if ((nwords & 3) == 0) {
-        for (uint32_t i = threadIdx.x * 4; i < nwords; i += kF2Threads * 4)
-            *reinterpret_cast<uint4*>(bm + i) = *reinterpret_cast<const uint4*>(bitmap + i);
-    } else {
-        for (uint32_t i = threadIdx.x; i < nwords; i += kF2Threads) bm[i] = bitmap[i];
-    }
+// Persistent: one workgroup per CU, each owning a contiguous id range streamed in chunks
+// of kF2Step ids (the next chunk's loads are in flight while the current one is
+// filtered).  Survivors are appended to an LDS stage; when the stage could overflow (and
+// at the end) it is flushed as one RUN: counting-sorted by partition (top b1 bits) and
+// written contiguously at a region offset taken from a global cursor, with the run's
+// per-partition {start, count} written to tabr[p * max_runs + run].
+constexpr int kF2Threads = 1024;
+constexpr uint32_t kF2Sub = 4 * kF2Threads;          // ids per sub-step (one uint4 per thread)
+constexpr uint32_t kF2Step = 4 * kF2Sub;             // ids per chunk
+constexpr uint32_t kStage = 11264;                   // LDS stage entries (88 KB)
+
+__host__ __device__ inline uint32_t f2_fixed_words(uint32_t nwords, uint32_t np) {
+    return (36 + nwords + np + 1 + 17 + 3) & ~3u;
+}
+
+struct F2Args {
+    const uint32_t* w0; uint64_t n; uint64_t per_blk;
+    uint32_t Lm, b1;
+    const uint32_t* bitmap; uint32_t nwords;
+    uint32_t* tabr; uint32_t max_runs; uint32_t* rbase;
+    uint2* ireg; uint32_t* ctr;   // ctr[1] = survivor cursor, ctr[2] = run count
+    uint32_t stage;               // LDS stage capacity (entries, <= kStage)
+    uint32_t dbg;                 // experiment switches (0 in production)
+    uint32_t lim;                 // last 16-B aligned word offset loadable inside the plane allocation
+};
+
+__device__ void f2_flush(const F2Args& a, uint32_t cnt, const uint2* stage, uint32_t* hist, uint32_t* wsum,
+                         uint32_t* misc) {
+    const uint32_t np = 1u << a.b1;
     for (uint32_t i = threadIdx.x; i <= np; i += kF2Threads) hist[i] = 0;
     __syncthreads();
-    uint32_t rk[kF2Per];
-#pragma unroll
-    for (int e = 0; e < kF2Per; ++e) {
-        const uint32_t j = (e / 4) * 4 * kF2Threads + 4 * threadIdx.x + (e % 4);
-        rk[e] = DHT_NONE;
-        if (j < m) {
-            const uint32_t pre = top_bits(v[e], Lm);
-            if ((bm[pre >> 5] >> (pre & 31)) & 1u) rk[e] = atomicAdd(hist + top_bits(v[e], b1), 1u);
-        }
+    for (uint32_t j = threadIdx.x; j < cnt; j += kF2Threads) atomicAdd(hist + top_bits(stage[j].x, a.b1), 1u);
+    __syncthreads();
+    scan_lds<kF2Threads>(hist, np, wsum);
+    if (threadIdx.x == 0) {
+        hist[np] = cnt;
+        misc[3] = atomicAdd(a.ctr + 2, 1u);
+        misc[4] = atomicAdd(a.ctr + 1, cnt);
     }
     __syncthreads();
-    const uint32_t tot = scan_lds<kF2Threads>(hist, np, wsum);
-    hist[np] = tot;
-    __syncthreads();
+    const uint32_t run = misc[3], off = misc[4];
+    if (a.dbg & 2) { __syncthreads(); return; }
     for (uint32_t p = threadIdx.x; p < np; p += kF2Threads)
-        tab2[(uint64_t)p * nblk2 + blockIdx.x] = (hist[p] << 16) | (hist[p + 1] - hist[p]);
+        a.tabr[(uint64_t)p * a.max_runs + run] = (hist[p] << 16) | (hist[p + 1] - hist[p]);
+    if (threadIdx.x == 0) a.rbase[run] = off;
+    __syncthreads();
+    // order inside a partition is free: the running offsets hand out the slots
+    for (uint32_t j = threadIdx.x; j < cnt; j += kF2Threads) {
+        const uint2 e = stage[j];
+        a.ireg[(uint64_t)off + atomicAdd(hist + top_bits(e.x, a.b1), 1u)] = e;
+    }
+    __syncthreads();
+}
+
+// Loads are unconditional 16-B loads (no data-dependent branches, so every load of the
+// ring stays in flight): addresses past the id range are clamped into the plane
+// allocation and their words are masked by the caller's range test.
+constexpr uint32_t kRing = 8;
+__device__ __forceinline__ uint4 f2_load1(const uint32_t* __restrict__ w0, uint32_t c, uint32_t lim) {
+    uint32_t j = c + 4 * threadIdx.x;
+    j = j < lim ? j : lim;
+    return *reinterpret_cast<const uint4*>(w0 + j);
+}
+
+__global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
+    extern __shared__ uint32_t sh[];   // (32 spare) | misc[8] | bm[nwords] | hist[np + 1] | wsum[17] | stage
+    const uint32_t np = 1u << a.b1;
+    uint32_t* misc = sh + 28;
+    uint32_t* bm = sh + 36;
+    uint32_t* hist = bm + a.nwords;
+    uint32_t* wsum = hist + np + 1;
+    uint2* stage = reinterpret_cast<uint2*>(sh + f2_fixed_words(a.nwords, np));
+    const uint64_t lo64 = (uint64_t)blockIdx.x * a.per_blk;
+    if (lo64 >= a.n) return;
+    const uint32_t lo = (uint32_t)lo64;
+    const uint32_t hi = (uint32_t)(lo64 + a.per_blk < a.n ? lo64 + a.per_blk : a.n);
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t sh_lm = 32 - a.Lm;   // Lm >= 1 here is not guaranteed: handled by lm_mask
+    const uint32_t lm_mask = a.Lm ? 0xFFFFFFFFu : 0u;
+    // the prefix bitmap first (its loads would otherwise wait behind the id ring); indices
+    // past the end are clamped, so a clamped lane rewrites a word with its own value
+    if ((a.nwords & 3) == 0) {
+        for (uint32_t i0 = 0; i0 < a.nwords; i0 += kF2Threads * 16) {
+            uint4 t[4];
+            uint32_t ic[4];
 #pragma unroll
-    for (int e = 0; e < kF2Per; ++e) {
-        if (rk[e] != DHT_NONE) {
-            const uint32_t j = (e / 4) * 4 * kF2Threads + 4 * threadIdx.x + (e % 4);
-            ireg[base + hist[top_bits(v[e], b1)] + rk[e]] = make_uint2(v[e], (uint32_t)(base + j));
+            for (uint32_t r = 0; r < 4; ++r) {
+                const uint32_t i = i0 + (r * kF2Threads + threadIdx.x) * 4;
+                ic[r] = i < a.nwords ? i : a.nwords - 4;
+                t[r] = *reinterpret_cast<const uint4*>(a.bitmap + ic[r]);
+            }
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r) *reinterpret_cast<uint4*>(bm + ic[r]) = t[r];
+        }
+    } else {
+        for (uint32_t i = threadIdx.x; i < a.nwords; i += kF2Threads) bm[i] = a.bitmap[i];
+    }
+    // ring of kRing sub-steps (one 16-B load per lane each) in flight: 128 KB per CU
+    uint4 ring[kRing];
+#pragma unroll
+    for (uint32_t r = 0; r < kRing; ++r) ring[r] = f2_load1(a.w0, lo + r * kF2Sub, a.lim);
+    if (threadIdx.x < 3) misc[threadIdx.x] = 0;
+    __syncthreads();
+    // Stage fill `cnt` is block-uniform.  Sub-step s reserves slots with one LDS atomic per
+    // wave on counter misc[s % 3]; after the sub-step's barrier every wave adds that
+    // counter to cnt.  The counter of sub-step s + 1 is zeroed during sub-step s (before
+    // its barrier), when every read of its previous use (sub-step s - 2) is complete.
+    uint32_t cnt = 0, s3 = 0;
+    for (uint32_t c0 = lo; c0 < hi; c0 += kRing * kF2Sub) {
+#pragma unroll
+        for (uint32_t r = 0; r < kRing; ++r) {
+            const uint32_t sb = c0 + r * kF2Sub;
+            if (sb < hi) {   // block-uniform
+                if (cnt > a.stage - kF2Sub) {
+                    f2_flush(a, cnt, stage, hist, wsum, misc);
+                    cnt = 0;
+                }
+                const uint32_t j0 = sb + 4 * threadIdx.x;
+                const uint32_t v4[4] = {ring[r].x, ring[r].y, ring[r].z, ring[r].w};
+                uint64_t bal[4];
+                uint32_t tot = 0;
+#pragma unroll
+                for (uint32_t f = 0; f < 4; ++f) {
+                    const uint32_t pre = (v4[f] & lm_mask) >> (sh_lm & 31);
+                    bool sv = j0 + f < hi && ((bm[pre >> 5] >> (pre & 31)) & 1u);
+                    if (a.dbg & 1) sv = (v4[f] & 0xFFFFF) == 0x12345;
+                    bal[f] = __ballot(sv);
+                    tot += (uint32_t)__popcll(bal[f]);
+                }
+                const uint32_t s3n = s3 == 2 ? 0u : s3 + 1;
+                uint32_t base = 0;
+                if (lane == 0 && tot) base = atomicAdd(misc + s3, tot);
+                if (threadIdx.x == 0) misc[s3n] = 0;
+                uint32_t pos = cnt + __builtin_amdgcn_readfirstlane(base);
+#pragma unroll
+                for (uint32_t f = 0; f < 4; ++f) {
+                    const uint64_t bm_f = bal[f];
+                    if ((bm_f >> lane) & 1ull)
+                        stage[pos + (uint32_t)__popcll(bm_f & ((1ull << lane) - 1ull))] = make_uint2(v4[f], j0 + f);
+                    pos += (uint32_t)__popcll(bm_f);
+                }
+                __syncthreads();
+                cnt += misc[s3];
+                s3 = s3n;
+            }
+            ring[r] = f2_load1(a.w0, sb + kRing * kF2Sub, a.lim);
         }
     }
+    if (cnt) f2_flush(a, cnt, stage, hist, wsum, misc);
 }
 
 // ---- candidate order ------------------------------------------------------------------
@@ -227,8 +317,24 @@ __device__ __forceinline__ void load_target(const uint32_t* __restrict__ tp, uin
 }
 
 // ---- F3: one workgroup per partition --------------------------------------------------
+// Setup: the partition's survivor runs are counting-sorted into LDS by the remaining
+// Lm - b1 prefix bits (two passes over the runs: histogram, then placement by running
+// offsets).  Queries, per chunk of kF3Threads targets:
+//   A  one LANE per target: a register-resident sorted top-K of its subtree's candidates
+//      keyed by (w0 distance, LDS position) -- exact unless two candidates' w0 words tie
+//      at or above the k-th place, which the lane detects (adjacent equal distances in its
+//      list, or an evicted/rejected distance equal to the k-th);
+//   B  targets with such ties or with large subtrees: one WAVE per target, exact order by
+//      the full 160-bit key (words 1..4 read from the id planes).
+// Targets whose subtree holds fewer than min(k, n) ids go to the F4 fallback list.
+constexpr uint32_t kLaneMax = 256;   // largest subtree a lane scans alone
+
+__host__ __device__ inline uint32_t f3_words(uint32_t nblk1, uint32_t nsub) {
+    return (nblk1 + 1 + 2 * nsub + 1 + 17 + kF3Threads + 1 + 1) & ~1u;
+}
+
 struct F3Args {
-    const uint2* ireg; const uint32_t* tab2; uint32_t nblk2;
+    const uint2* ireg; const uint32_t* tabr; const uint32_t* rbase; uint32_t max_runs;
     const uint2* treg; const uint32_t* tab1; uint32_t nblk1;
     uint32_t Lm, b1;
     uint32_t* bitmap; uint32_t nwords;
@@ -236,149 +342,199 @@ struct F3Args {
     const uint32_t* tp; uint64_t ts; uint32_t k;
     const uint32_t* gidx; uint32_t base;
     uint32_t* out_idx; uint32_t* out_cnt;
-    uint32_t* fb_count; uint32_t* fb_list;   // fb_count[0] = fallback targets, fb_count[1] = survivors
+    uint32_t* ctr; uint32_t* fb_list;   // ctr[0] = fallback targets, ctr[2] = runs written by F2
+    uint32_t dbg;
 };
 
+// exact wave-cooperative answer for one target (ties on w0, large subtrees)
+__device__ void f3_wave_answer(const F3Args& a, const uint2* S, uint32_t lo, uint32_t hi, uint32_t qi,
+                               uint32_t t0, uint32_t want, uint32_t lane) {
+    uint32_t t[DHT_W];
+    load_target(a.tp, a.ts, qi, t);
+    uint32_t* orow = a.out_idx + (uint64_t)qi * a.k;
+    const uint32_t mm = hi - lo;
+    if (mm <= 64) {
+        const bool act = lane < mm;
+        const uint2 me = act ? S[lo + lane] : make_uint2(0u, 0u);
+        const uint32_t md = me.x ^ t0;
+        uint32_t rank = 0;
+        for (uint32_t o = 0; o < mm; ++o) {
+            const uint2 x = S[lo + o];
+            if (act && o != lane) rank += id_less(x.x ^ t0, x.y, md, me.y, a.planes, a.stride, t);
+        }
+        if (act && rank < want) orow[rank] = map_out(me.y, a.gidx, a.base);
+    } else {
+        // running lane-distributed top-`want` list
+        uint32_t ed = DHT_NONE, ei = DHT_NONE, cnt = 0;
+        for (uint32_t c = lo; c < hi; c += 64) {
+            const bool v = c + lane < hi;
+            const uint2 x = v ? S[c + lane] : make_uint2(0u, DHT_NONE);
+            const uint32_t xd = x.x ^ t0, xi = x.y;
+            uint32_t wd = cnt == want ? __builtin_amdgcn_readlane((int)ed, want - 1) : DHT_NONE;
+            uint32_t wi = cnt == want ? __builtin_amdgcn_readlane((int)ei, want - 1) : DHT_NONE;
+            uint64_t cm = __ballot(v && (cnt < want || id_less(xd, xi, wd, wi, a.planes, a.stride, t)));
+            while (cm) {
+                const uint32_t l = (uint32_t)__ffsll((long long)cm) - 1;
+                cm &= cm - 1;
+                const uint32_t cd = __builtin_amdgcn_readlane((int)xd, l), ci = __builtin_amdgcn_readlane((int)xi, l);
+                if (cnt == want && !id_less(cd, ci, wd, wi, a.planes, a.stride, t)) continue;
+                const bool closer = lane < cnt && id_less(ed, ei, cd, ci, a.planes, a.stride, t);
+                const uint32_t pos = (uint32_t)__popcll(__ballot(closer));
+                const uint32_t ud = __shfl_up(ed, 1), ui = __shfl_up(ei, 1);
+                if (lane == pos) { ed = cd; ei = ci; }
+                else if (lane > pos) { ed = ud; ei = ui; }
+                cnt = cnt + 1 < want ? cnt + 1 : want;
+                wd = cnt == want ? __builtin_amdgcn_readlane((int)ed, want - 1) : DHT_NONE;
+                wi = cnt == want ? __builtin_amdgcn_readlane((int)ei, want - 1) : DHT_NONE;
+            }
+        }
+        if (lane < want) orow[lane] = map_out(ei, a.gidx, a.base);
+    }
+    if (lane >= want && lane < a.k) orow[lane] = DHT_NONE;
+    if (lane == 0) a.out_cnt[qi] = want;
+}
+
+template <int K>
 __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     extern __shared__ uint32_t sh[];
     const uint32_t p = blockIdx.x, np = gridDim.x;
     const uint32_t sb = a.Lm - a.b1, nsub = 1u << sb;
-    uint32_t* tpk = sh;                       // [nblk1] packed target runs
-    uint32_t* toff = tpk + a.nblk1;           // [nblk1 + 1]
-    uint32_t* ipk = toff + a.nblk1 + 1;       // [nblk2] packed survivor runs
-    uint32_t* ioff = ipk + a.nblk2;           // [nblk2 + 1]
-    uint32_t* sofs = ioff + a.nblk2 + 1;      // [nsub + 1]
-    uint32_t* wsum = sofs + nsub + 1;         // [17]
-    uint2* S = reinterpret_cast<uint2*>(sh + ((a.nblk1 * 2 + a.nblk2 * 2 + nsub + 2 + 2 + 17 + 1) & ~1u));
+    const uint32_t nruns = a.ctr[2];
+    uint32_t* toff = sh;                      // [nblk1 + 1]
+    uint32_t* sofs = toff + a.nblk1 + 1;      // [nsub + 1]
+    uint32_t* cur = sofs + nsub + 1;          // [nsub]
+    uint32_t* wsum = cur + nsub;              // [17]
+    uint32_t* slow = wsum + 17;               // [kF3Threads + 1] slow-path target slots, count last
+    uint2* S = reinterpret_cast<uint2*>(sh + f3_words(a.nblk1, nsub));
+    uint2* T = S + kF3Cap;
     // the bitmap is no longer read in this call: clear this block's share of it
     for (uint32_t i = p + np * threadIdx.x; i < a.nwords; i += np * kF3Threads) a.bitmap[i] = 0;
-    for (uint32_t b = threadIdx.x; b < a.nblk1; b += kF3Threads) {
-        const uint32_t x = a.tab1[(uint64_t)p * a.nblk1 + b];
-        tpk[b] = x;
-        toff[b] = x & 0xFFFFu;
-    }
-    for (uint32_t b = threadIdx.x; b < a.nblk2; b += kF3Threads) {
-        const uint32_t x = a.tab2[(uint64_t)p * a.nblk2 + b];
-        ipk[b] = x;
-        ioff[b] = x & 0xFFFFu;
-    }
+    for (uint32_t b = threadIdx.x; b < a.nblk1; b += kF3Threads) toff[b] = a.tab1[(uint64_t)p * a.nblk1 + b] & 0xFFFFu;
     for (uint32_t i = threadIdx.x; i <= nsub; i += kF3Threads) sofs[i] = 0;
     __syncthreads();
     const uint32_t mt = scan_lds<kF3Threads>(toff, a.nblk1, wsum);
     if (mt == 0) return;   // no targets in this partition (block-uniform)
-    const uint32_t m = scan_lds<kF3Threads>(ioff, a.nblk2, wsum);
-    if (threadIdx.x == 0) {
-        toff[a.nblk1] = mt;
-        ioff[a.nblk2] = m;
-        atomicAdd(a.fb_count + 1, m);
-    }
-    __syncthreads();
+    if (threadIdx.x == 0) toff[a.nblk1] = mt;
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     constexpr uint32_t NWV = kF3Threads / 64;
     auto target_at = [&](uint32_t j) -> uint2 {
         const uint32_t b = run_of(toff, a.nblk1, j);
-        return a.treg[(uint64_t)b * kF1Chunk + (tpk[b] >> 16) + (j - toff[b])];
+        return a.treg[(uint64_t)b * kF1Chunk + (a.tab1[(uint64_t)p * a.nblk1 + b] >> 16) + (j - toff[b])];
     };
+    // counting sort of the survivors by sub-prefix.  One thread per F2 run slice (about
+    // survivors / (partitions * runs) entries each): histogram, scan, then placement at
+    // running offsets.
+    const uint32_t smask = nsub - 1u;
+    const uint32_t* trow = a.tabr + (uint64_t)p * a.max_runs;
+    for (uint32_t r = threadIdx.x; r < nruns; r += kF3Threads) {
+        const uint32_t x = trow[r];
+        const uint32_t c = x & 0xFFFFu;
+        const uint2* src = a.ireg + a.rbase[r] + (x >> 16);
+        for (uint32_t i = 0; i < c; i += 4) {
+            uint32_t key[4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) key[u] = i + u < c ? src[i + u].x : 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u)
+                if (i + u < c) atomicAdd(sofs + (top_bits(key[u], a.Lm) & smask), 1u);
+        }
+    }
+    __syncthreads();
+    const uint32_t m = scan_lds<kF3Threads>(sofs, nsub, wsum);
+    if (a.dbg & 32) return;
     if (m > kF3Cap) {
         // strongly clustered ids: this partition's targets take the exact brute-force path
         for (uint32_t j = threadIdx.x; j < mt; j += kF3Threads) {
             const uint2 te = target_at(j);
-            a.fb_list[atomicAdd(a.fb_count, 1u)] = te.y;
+            a.fb_list[atomicAdd(a.ctr, 1u)] = te.y;
         }
         return;
     }
-    // gather the survivor runs (registers), histogram by sub-prefix, place sorted in LDS
-    uint2 e[kF3Per];
-    uint32_t rk[kF3Per];
-#pragma unroll
-    for (int r = 0; r < kF3Per; ++r) {
-        const uint32_t j = r * kF3Threads + threadIdx.x;
-        if (j < m) {
-            const uint32_t b = run_of(ioff, a.nblk2, j);
-            e[r] = a.ireg[(uint64_t)b * kF2Chunk + (ipk[b] >> 16) + (j - ioff[b])];
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < kF3Per; ++r) {
-        const uint32_t j = r * kF3Threads + threadIdx.x;
-        if (j < m) rk[r] = atomicAdd(sofs + (top_bits(e[r].x, a.Lm) & (nsub - 1u)), 1u);
-    }
-    __syncthreads();
-    scan_lds<kF3Threads>(sofs, nsub, wsum);
+    for (uint32_t i = threadIdx.x; i < nsub; i += kF3Threads) cur[i] = sofs[i];
     if (threadIdx.x == 0) sofs[nsub] = m;
     __syncthreads();
+    for (uint32_t r = threadIdx.x; r < nruns; r += kF3Threads) {
+        const uint32_t x = trow[r];
+        const uint32_t c = x & 0xFFFFu;
+        const uint2* src = a.ireg + a.rbase[r] + (x >> 16);
+        for (uint32_t i = 0; i < c; i += 4) {
+            uint2 e[4];
 #pragma unroll
-    for (int r = 0; r < kF3Per; ++r) {
-        const uint32_t j = r * kF3Threads + threadIdx.x;
-        if (j < m) S[sofs[top_bits(e[r].x, a.Lm) & (nsub - 1u)] + rk[r]] = e[r];
+            for (uint32_t u = 0; u < 4; ++u) e[u] = i + u < c ? src[i + u] : make_uint2(0u, 0u);
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u)
+                if (i + u < c) S[atomicAdd(cur + (top_bits(e[u].x, a.Lm) & smask), 1u)] = e[u];
+        }
     }
     __syncthreads();
-    // answer: one wave per target
+    if (a.dbg & 16) return;
     const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
-    for (uint32_t jt = wv; jt < mt; jt += NWV) {
-        const uint2 te = target_at(jt);
-        const uint32_t qi = __builtin_amdgcn_readfirstlane(te.y);
-        const uint32_t t0 = __builtin_amdgcn_readfirstlane(te.x);
-        const uint32_t s = top_bits(t0, a.Lm) & (nsub - 1u);
-        const uint32_t lo = sofs[s], hi = sofs[s + 1], mm = hi - lo;
-        if (mm < want) {
-            if (lane == 0) a.fb_list[atomicAdd(a.fb_count, 1u)] = qi;
-            continue;
-        }
-        uint32_t t[DHT_W];
-        t[0] = t0;
+    for (uint32_t t0i = 0; t0i < mt; t0i += kF3Threads) {
+        const uint32_t mtr = mt - t0i < kF3Threads ? mt - t0i : kF3Threads;
+        if (threadIdx.x < mtr) T[threadIdx.x] = target_at(t0i + threadIdx.x);
+        if (threadIdx.x == 0) slow[kF3Threads] = 0;
+        __syncthreads();
+        // A: one lane per target
+        if (threadIdx.x < mtr) {
+            const uint2 te = T[threadIdx.x];
+            const uint32_t t0 = te.x, qi = te.y;
+            const uint32_t s = top_bits(t0, a.Lm) & smask;
+            const uint32_t lo = sofs[s], hi = sofs[s + 1], mm = hi - lo;
+            if (mm < want) {
+                a.fb_list[atomicAdd(a.ctr, 1u)] = qi;
+            } else if (mm > kLaneMax || a.Lm == 0) {
+                slow[atomicAdd(slow + kF3Threads, 1u)] = threadIdx.x;
+            } else {
+                uint32_t dk[K], ok[K];
 #pragma unroll
-        for (int w = 1; w < DHT_W; ++w) t[w] = __builtin_amdgcn_readfirstlane(a.tp[(uint64_t)w * a.ts + qi]);
-        uint32_t* orow = a.out_idx + (uint64_t)qi * a.k;
-        if (mm <= 64) {
-            const bool act = lane < mm;
-            const uint2 me = act ? S[lo + lane] : make_uint2(0u, 0u);
-            const uint32_t md = me.x ^ t0;
-            const unsigned long long key = ((unsigned long long)md << 32) | me.y;
-            uint32_t rank = 0, eq = 0;
-            for (uint32_t o = 0; o < mm; ++o) {
-                const uint2 x = S[lo + o];
-                const unsigned long long ko = ((unsigned long long)(x.x ^ t0) << 32) | x.y;
-                rank += ko < key;
-                eq += x.x == me.x;
-            }
-            if (__ballot(act && eq > 1)) {   // equal w0 words: rank by the full 160-bit key
-                rank = 0;
-                for (uint32_t o = 0; o < mm; ++o) {
-                    const uint2 x = S[lo + o];
-                    if (act && o != lane) rank += id_less(x.x ^ t0, x.y, md, me.y, a.planes, a.stride, t);
+                for (int r = 0; r < K; ++r) { dk[r] = DHT_NONE; ok[r] = DHT_NONE; }
+                uint32_t rmin = DHT_NONE;   // smallest distance that left (or never entered) the list
+                for (uint32_t o = lo; o < hi; ++o) {
+                    const uint32_t d = S[o].x ^ t0;   // < 2^(32 - Lm) <= 2^31 < NONE
+                    const bool ins = d < dk[K - 1];
+                    rmin = min(rmin, ins ? dk[K - 1] : d);
+                    if (ins) {
+#pragma unroll
+                        for (int r = K - 1; r > 0; --r) {
+                            const bool up = d < dk[r - 1];
+                            const bool here = d < dk[r];
+                            ok[r] = up ? ok[r - 1] : (here ? o : ok[r]);
+                            dk[r] = up ? dk[r - 1] : (here ? d : dk[r]);
+                        }
+                        if (d < dk[0]) { dk[0] = d; ok[0] = o; }
+                    }
+                }
+                // ties on w0 at or above the want-th place need the full key
+                bool tie = rmin == dk[want - 1];
+#pragma unroll
+                for (int r = 0; r + 1 < K; ++r) tie = tie || ((uint32_t)r + 1 < want && dk[r] == dk[r + 1]);
+                // (r + 1 < want covers pairs inside the top-want; the pair (want-1, want)
+                // inside the list is caught by rmin unless the list is longer than want)
+                if (want < (uint32_t)K) {
+#pragma unroll
+                    for (int r = 0; r + 1 < K; ++r) tie = tie || ((uint32_t)r + 1 == want && dk[r] == dk[r + 1]);
+                }
+                if (tie) {
+                    slow[atomicAdd(slow + kF3Threads, 1u)] = threadIdx.x;
+                } else {
+                    uint32_t* orow = a.out_idx + (uint64_t)qi * a.k;
+#pragma unroll
+                    for (int r = 0; r < K; ++r)
+                        if ((uint32_t)r < a.k) orow[r] = (uint32_t)r < want ? map_out(S[ok[r]].y, a.gidx, a.base) : DHT_NONE;
+                    a.out_cnt[qi] = want;
                 }
             }
-            if (act && rank < want) orow[rank] = map_out(me.y, a.gidx, a.base);
-        } else {
-            // large subtree (clustered ids): running lane-distributed top-`want` list
-            uint32_t ed = DHT_NONE, ei = DHT_NONE, cnt = 0;
-            for (uint32_t c = lo; c < hi; c += 64) {
-                const bool v = c + lane < hi;
-                const uint2 x = v ? S[c + lane] : make_uint2(0u, DHT_NONE);
-                const uint32_t xd = x.x ^ t0, xi = x.y;
-                uint32_t wd = cnt == want ? __builtin_amdgcn_readlane((int)ed, want - 1) : DHT_NONE;
-                uint32_t wi = cnt == want ? __builtin_amdgcn_readlane((int)ei, want - 1) : DHT_NONE;
-                uint64_t cm = __ballot(v && (cnt < want || id_less(xd, xi, wd, wi, a.planes, a.stride, t)));
-                while (cm) {
-                    const uint32_t l = (uint32_t)__ffsll((long long)cm) - 1;
-                    cm &= cm - 1;
-                    const uint32_t cd = __builtin_amdgcn_readlane((int)xd, l), ci = __builtin_amdgcn_readlane((int)xi, l);
-                    if (cnt == want && !id_less(cd, ci, wd, wi, a.planes, a.stride, t)) continue;
-                    const bool closer = lane < cnt && id_less(ed, ei, cd, ci, a.planes, a.stride, t);
-                    const uint32_t pos = (uint32_t)__popcll(__ballot(closer));
-                    const uint32_t ud = __shfl_up(ed, 1), ui = __shfl_up(ei, 1);
-                    if (lane == pos) { ed = cd; ei = ci; }
-                    else if (lane > pos) { ed = ud; ei = ui; }
-                    cnt = cnt + 1 < want ? cnt + 1 : want;
-                    wd = cnt == want ? __builtin_amdgcn_readlane((int)ed, want - 1) : DHT_NONE;
-                    wi = cnt == want ? __builtin_amdgcn_readlane((int)ei, want - 1) : DHT_NONE;
-                }
-            }
-            if (lane < want) orow[lane] = map_out(ei, a.gidx, a.base);
         }
-        if (lane >= want && lane < a.k) orow[lane] = DHT_NONE;
-        if (lane == 0) a.out_cnt[qi] = want;
+        __syncthreads();
+        // B: one wave per target for ties and large subtrees
+        const uint32_t ns = slow[kF3Threads];
+        for (uint32_t i = wv; i < ns; i += NWV) {
+            const uint2 te = T[slow[i]];
+            const uint32_t t0 = __builtin_amdgcn_readfirstlane(te.x), qi = __builtin_amdgcn_readfirstlane(te.y);
+            const uint32_t s = top_bits(t0, a.Lm) & smask;
+            f3_wave_answer(a, S, sofs[s], sofs[s + 1], qi, t0, want, lane);
+        }
+        __syncthreads();
     }
 }
 
@@ -450,8 +606,11 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_fallback(const uint32_t* __re
 }
 
 struct BatchPlan {
-    uint32_t Lm, b1, nwords, nblk1, nblk2;
+    uint32_t Lm, b1, nwords, nblk1, nblk2, max_runs, stage;
+    uint64_t per_blk;
 };
+
+
 
 uint32_t floor_log2(uint64_t x) {
     uint32_t r = 0;
@@ -459,7 +618,7 @@ uint32_t floor_log2(uint64_t x) {
     return r;
 }
 
-BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k) {
+BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     BatchPlan P;
     // mark level: about 4k ids per level-Lm subtree
     const uint64_t per = 4ull * k;
@@ -475,33 +634,48 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k) {
     P.b1 = b1;
     P.nwords = P.Lm >= 5 ? (1u << (P.Lm - 5)) : 1u;
     P.nblk1 = (q + kF1Chunk - 1) / kF1Chunk;
-    P.nblk2 = (uint32_t)((n + kF2Chunk - 1) / kF2Chunk);
+    // F2: one persistent workgroup per CU, ranges in whole chunks
+    const uint64_t chunks = (n + kF2Step - 1) / kF2Step;
+    const uint64_t g = num_cus > 0 ? (uint64_t)num_cus : 256;
+    const uint64_t cpb = (chunks + g - 1) / g;
+    P.per_blk = (cpb ? cpb : 1) * kF2Step;
+    P.nblk2 = (uint32_t)((n + P.per_blk - 1) / P.per_blk);
+    // F2 LDS stage: what is left of the LDS next to the bitmap and histogram
+    const size_t fixed = (size_t)f2_fixed_words(P.nwords, 1u << P.b1) * 4;
+    const size_t room = fixed < kLdsMax ? (kLdsMax - fixed) / 8 : 0;
+    P.stage = (uint32_t)(room < kStage ? room : kStage);
+    // every run but a block's last holds > stage - kF2Sub entries
+    P.max_runs = P.stage > kF2Sub ? (uint32_t)(n / (P.stage - kF2Sub + 1)) + P.nblk2 + 1 : 0;
     return P;
+}
+
+size_t f2_lds(const BatchPlan& P) {
+    return (size_t)f2_fixed_words(P.nwords, 1u << P.b1) * 4 + (size_t)P.stage * 8;
 }
 
 size_t f3_lds(const BatchPlan& P) {
     const uint32_t nsub = 1u << (P.Lm - P.b1);
-    const size_t words = ((size_t)(P.nblk1 * 2 + P.nblk2 * 2 + nsub + 2 + 2 + 17 + 1) & ~size_t(1));
-    return words * 4 + (size_t)kF3Cap * 8;
+    return (size_t)f3_words(P.nblk1, nsub) * 4 + (size_t)(kF3Cap + kF3Threads) * 8;
 }
 
 }  // namespace
 
-bool batch_supported(uint64_t n, uint32_t q, uint32_t k) {
-    if (k == 0 || k > DHTGPU_MAX_K_DEV) return false;
-    const BatchPlan P = plan_batch(n, q, k);
-    if (P.nblk2 > kMaxBlk2 || P.nblk1 > kMaxBlk1) return false;
-    if (P.Lm - P.b1 > 13) return false;
-    return f3_lds(P) <= kLdsMax;
+bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
+    if (k == 0 || k > DHTGPU_MAX_K_DEV || n >= (1ull << 31)) return false;
+    const BatchPlan P = plan_batch(n, q, k, num_cus);
+    if (P.nblk1 > kMaxBlk1) return false;
+    if (P.Lm - P.b1 > 13 || P.stage < 2 * kF2Sub) return false;
+    return f3_lds(P) <= kLdsMax && f2_lds(P) <= kLdsMax;
 }
 
-// workspace: bitmap (64 KB, all-zero between calls) | fb_count | fb_list[q] | treg[q] |
-// tab1[np * nblk1] | tab2[np * nblk2] | ireg[nblk2 * kF2Chunk]
-size_t batch_bytes(uint64_t n, uint32_t q, uint32_t k) {
-    const BatchPlan P = plan_batch(n, q, k);
+// workspace: bitmap (64 KB, all-zero between calls) | ctr[4] | fb_list[q] | treg[q] |
+// tab1[np * nblk1] | tabr[np * max_runs] | rbase[max_runs] | ireg[n]
+size_t batch_bytes(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
+    const BatchPlan P = plan_batch(n, q, k, num_cus);
     const size_t np = 1ull << P.b1;
-    return 65536 + 256 + (size_t)q * 4 + 16 + (size_t)q * 8 + 16 + np * P.nblk1 * 4 + 16 + np * P.nblk2 * 4 + 16 +
-           (size_t)P.nblk2 * kF2Chunk * 8 + 256;
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    return al(65536) + al(16) + al((size_t)q * 4) + al((size_t)q * 8) + al(np * P.nblk1 * 4) +
+           al(np * P.max_runs * 4) + al((size_t)P.max_runs * 4) + al((size_t)(n ? n : 1) * 8);
 }
 
 const uint32_t* batch_stats(const void* ws) {
@@ -510,9 +684,9 @@ const uint32_t* batch_stats(const void* ws) {
 
 hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp,
                              uint64_t ts, uint32_t q, uint32_t k, const uint32_t* gidx, uint32_t base,
-                             uint32_t* out_idx, uint32_t* out_cnt, hipStream_t s, hipEvent_t* ev) {
+                             uint32_t* out_idx, uint32_t* out_cnt, int num_cus, hipStream_t s, hipEvent_t* ev) {
     if (!q) return hipSuccess;
-    const BatchPlan P = plan_batch(n, q, k);
+    const BatchPlan P = plan_batch(n, q, k, num_cus);
     const uint32_t np = 1u << P.b1;
     uint8_t* w = static_cast<uint8_t*>(ws);
     auto take = [&](size_t bytes) {
@@ -521,33 +695,45 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
         return r;
     };
     uint32_t* bitmap = reinterpret_cast<uint32_t*>(take(65536));
-    uint32_t* fb_count = reinterpret_cast<uint32_t*>(take(16));
+    uint32_t* ctr = reinterpret_cast<uint32_t*>(take(16));
     uint32_t* fb_list = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
     uint2* treg = reinterpret_cast<uint2*>(take((size_t)q * 8));
     uint32_t* tab1 = reinterpret_cast<uint32_t*>(take((size_t)np * P.nblk1 * 4));
-    uint32_t* tab2 = reinterpret_cast<uint32_t*>(take((size_t)np * (P.nblk2 ? P.nblk2 : 1) * 4));
-    uint2* ireg = reinterpret_cast<uint2*>(take((size_t)(P.nblk2 ? P.nblk2 : 1) * kF2Chunk * 8));
+    uint32_t* tabr = reinterpret_cast<uint32_t*>(take((size_t)np * P.max_runs * 4));
+    uint32_t* rbase = reinterpret_cast<uint32_t*>(take((size_t)P.max_runs * 4));
+    uint2* ireg = reinterpret_cast<uint2*>(take((size_t)(n ? n : 1) * 8));
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k_f2_filter, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
-        (void)hipFuncSetAttribute((const void*)k_f3_answer, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
+        (void)hipFuncSetAttribute((const void*)k_f3_answer<8>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
+        (void)hipFuncSetAttribute((const void*)k_f3_answer<16>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
+        (void)hipFuncSetAttribute((const void*)k_f3_answer<32>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
         attr_set = true;
     }
+    static const uint32_t dbg = getenv("DHTGPU_DBG") ? (uint32_t)atoi(getenv("DHTGPU_DBG")) : 0u;
     if (ev) (void)hipEventRecord(ev[0], s);
     k_f1_targets<<<P.nblk1, kF1Threads, (np + 1 + 17) * 4, s>>>(tp, q, P.Lm, P.b1, bitmap, tab1, P.nblk1, treg,
-                                                                fb_count);
+                                                                ctr);
     if (ev) (void)hipEventRecord(ev[1], s);
-    if (P.nblk2)
-        k_f2_filter<<<P.nblk2, kF2Threads, (P.nwords + np + 1 + 17) * 4, s>>>(planes, n, P.Lm, P.b1, bitmap,
-                                                                               P.nwords, tab2, P.nblk2, ireg);
+    if (n) {
+        F2Args a2{planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, tabr, P.max_runs, rbase, ireg, ctr, P.stage, dbg,
+                  (uint32_t)(5 * stride - 4 < 0xFFFFFFF0ull ? 5 * stride - 4 : 0xFFFFFFF0ull)};
+        k_f2_filter<<<P.nblk2, kF2Threads, f2_lds(P), s>>>(a2);
+    }
     if (ev) (void)hipEventRecord(ev[2], s);
-    F3Args a{ireg, tab2, P.nblk2, treg, tab1, P.nblk1, P.Lm, P.b1, bitmap, P.nwords, planes, stride, n,
-             tp, ts, k, gidx, base, out_idx, out_cnt, fb_count, fb_list};
-    k_f3_answer<<<np, kF3Threads, f3_lds(P), s>>>(a);
+    if (dbg & 15) {   // experiments: F1 + F2 only
+        for (int i = 3; ev && i < 5; ++i) (void)hipEventRecord(ev[i], s);
+        return hipGetLastError();
+    }
+    F3Args a{ireg, tabr, rbase, P.max_runs, treg, tab1, P.nblk1, P.Lm, P.b1, bitmap, P.nwords, planes, stride, n,
+             tp, ts, k, gidx, base, out_idx, out_cnt, ctr, fb_list, dbg};
+    if (k <= 8) k_f3_answer<8><<<np, kF3Threads, f3_lds(P), s>>>(a);
+    else if (k <= 16) k_f3_answer<16><<<np, kF3Threads, f3_lds(P), s>>>(a);
+    else k_f3_answer<32><<<np, kF3Threads, f3_lds(P), s>>>(a);
     if (ev) (void)hipEventRecord(ev[3], s);
     const uint32_t want = n < k ? (uint32_t)n : k;
-    k_f4_fallback<<<64, kF4Threads, ((size_t)want * kF4Threads + kF4Threads / 64) * 8, s>>>(fb_count, fb_list, planes, stride, n, tp, ts, k, gidx, base, out_idx,
-                                           out_cnt);
+    k_f4_fallback<<<64, kF4Threads, ((size_t)want * kF4Threads + kF4Threads / 64) * 8, s>>>(
+        ctr, fb_list, planes, stride, n, tp, ts, k, gidx, base, out_idx, out_cnt);
     if (ev) (void)hipEventRecord(ev[4], s);
     return hipGetLastError();
 }

@@ -84,12 +84,13 @@ hipError_t launch_index_query(const void* ws, uint64_t n, uint32_t B, const uint
 // batch.hip: K6 per-batch target-prefix filter + exact top-k (no persistent index).
 // out_idx/out_cnt indices are mapped through gidx (nullable) or offset by base.
 // ev (nullable): 5 events recorded around F1, F2, F3, F4.
-bool batch_supported(uint64_t n, uint32_t q, uint32_t k);
-size_t batch_bytes(uint64_t n, uint32_t q, uint32_t k);
+bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus);
+size_t batch_bytes(uint64_t n, uint32_t q, uint32_t k, int num_cus);
 // device address of {fallback targets, survivors} of the last call on workspace ws
 const uint32_t* batch_stats(const void* ws);
 hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp,
                              uint64_t ts, uint32_t q, uint32_t k, const uint32_t* gidx, uint32_t base,
-                             uint32_t* out_idx, uint32_t* out_cnt, hipStream_t s, hipEvent_t* ev = nullptr);
+                             uint32_t* out_idx, uint32_t* out_cnt, int num_cus, hipStream_t s,
+                             hipEvent_t* ev = nullptr);
 
 }  // namespace dhtgpu

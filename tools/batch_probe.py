@@ -1,0 +1,53 @@
+"""Quick K6 driver for profiling: cfg-2 shaped inputs generated in HBM, `reps` stream-ordered
+calls of dhtgpu_batch_topk_dev, then the per-kernel event times of one timed call."""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import opendht_amd  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=1 << 24)
+ap.add_argument("--q", type=int, default=65536)
+ap.add_argument("--k", type=int, default=8)
+ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--algo", default="batch")
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(0)
+st = torch.cuda.Stream(dev)
+torch.cuda.set_stream(st)
+s = st.cuda_stream
+L = opendht_amd.lib()
+ctx = opendht_amd.Context(0)
+ctx.gen_ids(2024, a.n)
+ts = (a.q + 63) // 64 * 64
+tp = torch.empty(5 * ts, dtype=torch.int32, device=dev)
+assert L.dhtgpu_gen_dev(2025, 0, a.q, tp.data_ptr(), ts, s) == 0
+oi = torch.empty((a.q, a.k), dtype=torch.int32, device=dev)
+oc = torch.empty(a.q, dtype=torch.int32, device=dev)
+
+
+def call():
+    if a.algo == "batch":
+        ctx.batch_topk_dev(tp.data_ptr(), ts, a.q, a.k, oi.data_ptr(), oc.data_ptr(), None, 0, s)
+    else:
+        ctx.index_build(s)
+        ctx.index_topk_dev(tp.data_ptr(), ts, a.q, a.k, oi.data_ptr(), oc.data_ptr(), None, 0, s)
+
+
+call()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(a.reps):
+    call()
+torch.cuda.synchronize()
+dt = (time.perf_counter() - t0) / a.reps
+print(f"{a.algo} n={a.n} q={a.q} k={a.k}: {dt * 1e3:.4f} ms/call  {a.q / dt / 1e6:.1f} M q/s")
+if a.algo == "batch":
+    ms, fb, surv = ctx.batch_topk_timed(tp.data_ptr(), ts, a.q, a.k, oi.data_ptr(), oc.data_ptr(), s)
+    print("phases ms (F1,F2,F3,F4):", [round(x, 4) for x in ms], "fallback", fb, "survivors", surv)
+ctx.close()

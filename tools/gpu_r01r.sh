@@ -1,0 +1,6 @@
+set -o pipefail
+OUT=gpurun_out/r01r; mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_SMEM -d $OUT/pmc1 -o run --output-format csv -- python3 tools/batch_probe.py --reps 2 > $OUT/pmc1.log 2>&1 && echo pmc1-ok &&
+timeout -s KILL 90 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR -d $OUT/pmc2 -o run --output-format csv -- python3 tools/batch_probe.py --reps 2 > $OUT/pmc2.log 2>&1 && echo pmc2-ok &&
+timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_MISC SQ_INSTS_SENDMSG -d $OUT/pmc3 -o run --output-format csv -- python3 tools/batch_probe.py --reps 2 > $OUT/pmc3.log 2>&1 && echo pmc3-ok
