@@ -445,7 +445,7 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     const size_t need = batch_bytes(c->n, q, k, c->num_cus);
     if (need > c->batch.cap) c->batch_clean = false;
     DHT_TRY(c->batch.ensure(need));
-    if (!c->batch_clean) DHT_TRY(hipMemsetAsync(c->batch.p, 0, 65536 + 256, s));
+    if (!c->batch_clean) DHT_TRY(hipMemsetAsync(c->batch.p, 0, batch_clean_bytes(), s));
     c->batch_clean = false;   // re-established below once every launch went through
     const uint32_t* gidx = c->has_gidx ? c->gidx.as<uint32_t>() : nullptr;
     uint32_t* li = out_idx;

@@ -44,6 +44,7 @@ constexpr int kF1Per = 4;
 constexpr uint32_t kF1Chunk = kF1Threads * kF1Per;   // targets per F1 block
 constexpr int kF3Threads = 256;
 constexpr uint32_t kF3Cap = 4096;                    // survivors per partition staged in LDS
+constexpr uint32_t kF3Per = kF3Cap / kF3Threads;
 constexpr int kF4Threads = 256;
 constexpr uint32_t kMaxLm = 19;                      // 2^19-bit bitmap = 64 KB of LDS in F2
 constexpr uint32_t kMaxSubBits = 11;                 // F3 sub-prefix histogram <= 2048 bins
@@ -144,12 +145,10 @@ __global__ __launch_bounds__(kF1Threads) void k_f1_targets(const uint32_t* __res
 }
 
 // ---- F2: stream w0, keep ids in marked subtrees, partition them ----------------------
-// Persistent: one workgroup per CU, each owning a contiguous id range streamed in chunks
-// of kF2Step ids (the next chunk's loads are in flight while the current one is
-// filtered).  Survivors are appended to an LDS stage; when the stage could overflow (and
-// at the end) it is flushed as one RUN: counting-sorted by partition (top b1 bits) and
-// written contiguously at a region offset taken from a global cursor, with the run's
-// per-partition {start, count} written to tabr[p * max_runs + run].
+// Persistent: one workgroup per CU, each owning a contiguous id range streamed through
+// a ring of kRing 16-B loads per lane (128 KB in flight per CU).  Survivors are appended
+// to an LDS stage; when the stage could overflow (and at the end) it is flushed into the
+// partition-major survivor buckets pbuf[p][...] (see f2_flush).
 constexpr int kF2Threads = 1024;
 constexpr uint32_t kF2Sub = 4 * kF2Threads;          // ids per sub-step (one uint4 per thread)
 constexpr uint32_t kF2Step = 4 * kF2Sub;             // ids per chunk
@@ -163,37 +162,36 @@ struct F2Args {
     const uint32_t* w0; uint64_t n; uint64_t per_blk;
     uint32_t Lm, b1;
     const uint32_t* bitmap; uint32_t nwords;
-    uint32_t* tabr; uint32_t max_runs; uint32_t* rbase;
-    uint2* ireg; uint32_t* ctr;   // ctr[1] = survivor cursor, ctr[2] = run count
+    uint32_t* pcount;             // [np] survivors per partition (all-zero between calls)
+    uint2* pbuf;                  // [np][pcap] survivors, partition-major
+    uint32_t pcap;
+    uint32_t* ctr;                // ctr[1] = survivor total
     uint32_t stage;               // LDS stage capacity (entries, <= kStage)
     uint32_t dbg;                 // experiment switches (0 in production)
     uint32_t lim;                 // last 16-B aligned word offset loadable inside the plane allocation
 };
 
-__device__ void f2_flush(const F2Args& a, uint32_t cnt, const uint2* stage, uint32_t* hist, uint32_t* wsum,
-                         uint32_t* misc) {
+// Flush the stage: per partition, one returning global atomic reserves the slots of the
+// partition's bucket (pbuf[p][...]); entries are then written at running offsets.  A
+// partition that outgrows pcap keeps counting (F3 sends its targets to the fallback).
+__device__ void f2_flush(const F2Args& a, uint32_t cnt, const uint2* stage, uint32_t* hist) {
     const uint32_t np = 1u << a.b1;
-    for (uint32_t i = threadIdx.x; i <= np; i += kF2Threads) hist[i] = 0;
+    for (uint32_t i = threadIdx.x; i < np; i += kF2Threads) hist[i] = 0;
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < cnt; j += kF2Threads) atomicAdd(hist + top_bits(stage[j].x, a.b1), 1u);
     __syncthreads();
-    scan_lds<kF2Threads>(hist, np, wsum);
-    if (threadIdx.x == 0) {
-        hist[np] = cnt;
-        misc[3] = atomicAdd(a.ctr + 2, 1u);
-        misc[4] = atomicAdd(a.ctr + 1, cnt);
+    for (uint32_t p = threadIdx.x; p < np; p += kF2Threads) {
+        const uint32_t c = hist[p];
+        hist[p] = c ? atomicAdd(a.pcount + p, c) : 0u;
     }
+    if (threadIdx.x == 0) atomicAdd(a.ctr + 1, cnt);
     __syncthreads();
-    const uint32_t run = misc[3], off = misc[4];
     if (a.dbg & 2) { __syncthreads(); return; }
-    for (uint32_t p = threadIdx.x; p < np; p += kF2Threads)
-        a.tabr[(uint64_t)p * a.max_runs + run] = (hist[p] << 16) | (hist[p + 1] - hist[p]);
-    if (threadIdx.x == 0) a.rbase[run] = off;
-    __syncthreads();
-    // order inside a partition is free: the running offsets hand out the slots
     for (uint32_t j = threadIdx.x; j < cnt; j += kF2Threads) {
         const uint2 e = stage[j];
-        a.ireg[(uint64_t)off + atomicAdd(hist + top_bits(e.x, a.b1), 1u)] = e;
+        const uint32_t p = top_bits(e.x, a.b1);
+        const uint32_t pos = atomicAdd(hist + p, 1u);
+        if (pos < a.pcap) a.pbuf[(uint64_t)p * a.pcap + pos] = e;
     }
     __syncthreads();
 }
@@ -256,9 +254,11 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
 #pragma unroll
         for (uint32_t r = 0; r < kRing; ++r) {
             const uint32_t sb = c0 + r * kF2Sub;
-            if (sb < hi) {   // block-uniform
+            if (a.dbg & 64) {
+                cnt += ring[r].x ^ ring[r].y ^ ring[r].z ^ ring[r].w;
+            } else if (sb < hi) {   // block-uniform
                 if (cnt > a.stage - kF2Sub) {
-                    f2_flush(a, cnt, stage, hist, wsum, misc);
+                    f2_flush(a, cnt, stage, hist);
                     cnt = 0;
                 }
                 const uint32_t j0 = sb + 4 * threadIdx.x;
@@ -292,7 +292,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
             ring[r] = f2_load1(a.w0, sb + kRing * kF2Sub, a.lim);
         }
     }
-    if (cnt) f2_flush(a, cnt, stage, hist, wsum, misc);
+    if (a.dbg & 64) { if (cnt == 0x12345678u) a.ctr[3] = cnt; return; }
+    if (cnt) f2_flush(a, cnt, stage, hist);
 }
 
 // ---- candidate order ------------------------------------------------------------------
@@ -334,7 +335,7 @@ __host__ __device__ inline uint32_t f3_words(uint32_t nblk1, uint32_t nsub) {
 }
 
 struct F3Args {
-    const uint2* ireg; const uint32_t* tabr; const uint32_t* rbase; uint32_t max_runs;
+    const uint2* pbuf; uint32_t* pcount; uint32_t pcap;
     const uint2* treg; const uint32_t* tab1; uint32_t nblk1;
     uint32_t Lm, b1;
     uint32_t* bitmap; uint32_t nwords;
@@ -342,7 +343,7 @@ struct F3Args {
     const uint32_t* tp; uint64_t ts; uint32_t k;
     const uint32_t* gidx; uint32_t base;
     uint32_t* out_idx; uint32_t* out_cnt;
-    uint32_t* ctr; uint32_t* fb_list;   // ctr[0] = fallback targets, ctr[2] = runs written by F2
+    uint32_t* ctr; uint32_t* fb_list;   // ctr[0] = fallback targets
     uint32_t dbg;
 };
 
@@ -399,7 +400,6 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     extern __shared__ uint32_t sh[];
     const uint32_t p = blockIdx.x, np = gridDim.x;
     const uint32_t sb = a.Lm - a.b1, nsub = 1u << sb;
-    const uint32_t nruns = a.ctr[2];
     uint32_t* toff = sh;                      // [nblk1 + 1]
     uint32_t* sofs = toff + a.nblk1 + 1;      // [nsub + 1]
     uint32_t* cur = sofs + nsub + 1;          // [nsub]
@@ -411,8 +411,10 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     for (uint32_t i = p + np * threadIdx.x; i < a.nwords; i += np * kF3Threads) a.bitmap[i] = 0;
     for (uint32_t b = threadIdx.x; b < a.nblk1; b += kF3Threads) toff[b] = a.tab1[(uint64_t)p * a.nblk1 + b] & 0xFFFFu;
     for (uint32_t i = threadIdx.x; i <= nsub; i += kF3Threads) sofs[i] = 0;
+    const uint32_t m = a.pcount[p];           // survivors of this partition (F2)
     __syncthreads();
-    const uint32_t mt = scan_lds<kF3Threads>(toff, a.nblk1, wsum);
+    const uint32_t mt = scan_lds<kF3Threads>(toff, a.nblk1, wsum);   // (barriers: every thread read m)
+    if (threadIdx.x == 0) a.pcount[p] = 0;    // all-zero again for the next call
     if (mt == 0) return;   // no targets in this partition (block-uniform)
     if (threadIdx.x == 0) toff[a.nblk1] = mt;
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
@@ -421,28 +423,11 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         const uint32_t b = run_of(toff, a.nblk1, j);
         return a.treg[(uint64_t)b * kF1Chunk + (a.tab1[(uint64_t)p * a.nblk1 + b] >> 16) + (j - toff[b])];
     };
-    // counting sort of the survivors by sub-prefix.  One thread per F2 run slice (about
-    // survivors / (partitions * runs) entries each): histogram, scan, then placement at
-    // running offsets.
+    // counting sort of the partition's survivors by sub-prefix: coalesced loads into
+    // registers, LDS histogram (ranks from the atomics), scan, placement
     const uint32_t smask = nsub - 1u;
-    const uint32_t* trow = a.tabr + (uint64_t)p * a.max_runs;
-    for (uint32_t r = threadIdx.x; r < nruns; r += kF3Threads) {
-        const uint32_t x = trow[r];
-        const uint32_t c = x & 0xFFFFu;
-        const uint2* src = a.ireg + a.rbase[r] + (x >> 16);
-        for (uint32_t i = 0; i < c; i += 4) {
-            uint32_t key[4];
-#pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) key[u] = i + u < c ? src[i + u].x : 0u;
-#pragma unroll
-            for (uint32_t u = 0; u < 4; ++u)
-                if (i + u < c) atomicAdd(sofs + (top_bits(key[u], a.Lm) & smask), 1u);
-        }
-    }
-    __syncthreads();
-    const uint32_t m = scan_lds<kF3Threads>(sofs, nsub, wsum);
     if (a.dbg & 32) return;
-    if (m > kF3Cap) {
+    if (m > kF3Cap || m > a.pcap) {
         // strongly clustered ids: this partition's targets take the exact brute-force path
         for (uint32_t j = threadIdx.x; j < mt; j += kF3Threads) {
             const uint2 te = target_at(j);
@@ -450,22 +435,24 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         }
         return;
     }
-    for (uint32_t i = threadIdx.x; i < nsub; i += kF3Threads) cur[i] = sofs[i];
+    const uint2* src = a.pbuf + (uint64_t)p * a.pcap;
+    uint2 e[kF3Per];
+    uint32_t rk[kF3Per];
+#pragma unroll
+    for (uint32_t u = 0; u < kF3Per; ++u) {
+        const uint32_t j = u * kF3Threads + threadIdx.x;
+        e[u] = src[j < m ? j : 0];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kF3Per; ++u)
+        if (u * kF3Threads + threadIdx.x < m) rk[u] = atomicAdd(sofs + (top_bits(e[u].x, a.Lm) & smask), 1u);
+    __syncthreads();
+    scan_lds<kF3Threads>(sofs, nsub, wsum);
     if (threadIdx.x == 0) sofs[nsub] = m;
     __syncthreads();
-    for (uint32_t r = threadIdx.x; r < nruns; r += kF3Threads) {
-        const uint32_t x = trow[r];
-        const uint32_t c = x & 0xFFFFu;
-        const uint2* src = a.ireg + a.rbase[r] + (x >> 16);
-        for (uint32_t i = 0; i < c; i += 4) {
-            uint2 e[4];
 #pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) e[u] = i + u < c ? src[i + u] : make_uint2(0u, 0u);
-#pragma unroll
-            for (uint32_t u = 0; u < 4; ++u)
-                if (i + u < c) S[atomicAdd(cur + (top_bits(e[u].x, a.Lm) & smask), 1u)] = e[u];
-        }
-    }
+    for (uint32_t u = 0; u < kF3Per; ++u)
+        if (u * kF3Threads + threadIdx.x < m) S[sofs[top_bits(e[u].x, a.Lm) & smask] + rk[u]] = e[u];
     __syncthreads();
     if (a.dbg & 16) return;
     const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
@@ -606,7 +593,7 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_fallback(const uint32_t* __re
 }
 
 struct BatchPlan {
-    uint32_t Lm, b1, nwords, nblk1, nblk2, max_runs, stage;
+    uint32_t Lm, b1, nwords, nblk1, nblk2, stage;
     uint64_t per_blk;
 };
 
@@ -630,7 +617,7 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     uint32_t b1 = 0;
     while (b1 < P.Lm && surv / (double)(1ull << b1) > kF3Cap / 2) ++b1;
     if (P.Lm > kMaxSubBits && b1 < P.Lm - kMaxSubBits) b1 = P.Lm - kMaxSubBits;
-    if (b1 > 13) b1 = 13;
+    if (b1 > 13) b1 = 13;   // kMaxParts
     P.b1 = b1;
     P.nwords = P.Lm >= 5 ? (1u << (P.Lm - 5)) : 1u;
     P.nblk1 = (q + kF1Chunk - 1) / kF1Chunk;
@@ -644,8 +631,6 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     const size_t fixed = (size_t)f2_fixed_words(P.nwords, 1u << P.b1) * 4;
     const size_t room = fixed < kLdsMax ? (kLdsMax - fixed) / 8 : 0;
     P.stage = (uint32_t)(room < kStage ? room : kStage);
-    // every run but a block's last holds > stage - kF2Sub entries
-    P.max_runs = P.stage > kF2Sub ? (uint32_t)(n / (P.stage - kF2Sub + 1)) + P.nblk2 + 1 : 0;
     return P;
 }
 
@@ -668,14 +653,17 @@ bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     return f3_lds(P) <= kLdsMax && f2_lds(P) <= kLdsMax;
 }
 
-// workspace: bitmap (64 KB, all-zero between calls) | ctr[4] | fb_list[q] | treg[q] |
-// tab1[np * nblk1] | tabr[np * max_runs] | rbase[max_runs] | ireg[n]
+// workspace: bitmap (64 KB) | ctr[4] | pcount[kMaxParts] -- these three all-zero between
+// calls -- | fb_list[q] | treg[q] | tab1[np * nblk1] | pbuf[np * kF3Cap]
+constexpr uint32_t kMaxParts = 1u << 13;
+size_t batch_clean_bytes() { return 65536 + 256 + kMaxParts * 4; }
+
 size_t batch_bytes(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     const BatchPlan P = plan_batch(n, q, k, num_cus);
     const size_t np = 1ull << P.b1;
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    return al(65536) + al(16) + al((size_t)q * 4) + al((size_t)q * 8) + al(np * P.nblk1 * 4) +
-           al(np * P.max_runs * 4) + al((size_t)P.max_runs * 4) + al((size_t)(n ? n : 1) * 8);
+    return batch_clean_bytes() + al((size_t)q * 4) + al((size_t)q * 8) + al(np * P.nblk1 * 4) +
+           al(np * kF3Cap * 8);
 }
 
 const uint32_t* batch_stats(const void* ws) {
@@ -695,13 +683,12 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
         return r;
     };
     uint32_t* bitmap = reinterpret_cast<uint32_t*>(take(65536));
-    uint32_t* ctr = reinterpret_cast<uint32_t*>(take(16));
+    uint32_t* ctr = reinterpret_cast<uint32_t*>(take(256));
+    uint32_t* pcount = reinterpret_cast<uint32_t*>(take(kMaxParts * 4));
     uint32_t* fb_list = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
     uint2* treg = reinterpret_cast<uint2*>(take((size_t)q * 8));
     uint32_t* tab1 = reinterpret_cast<uint32_t*>(take((size_t)np * P.nblk1 * 4));
-    uint32_t* tabr = reinterpret_cast<uint32_t*>(take((size_t)np * P.max_runs * 4));
-    uint32_t* rbase = reinterpret_cast<uint32_t*>(take((size_t)P.max_runs * 4));
-    uint2* ireg = reinterpret_cast<uint2*>(take((size_t)(n ? n : 1) * 8));
+    uint2* pbuf = reinterpret_cast<uint2*>(take((size_t)np * kF3Cap * 8));
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k_f2_filter, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
@@ -716,16 +703,16 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
                                                                 ctr);
     if (ev) (void)hipEventRecord(ev[1], s);
     if (n) {
-        F2Args a2{planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, tabr, P.max_runs, rbase, ireg, ctr, P.stage, dbg,
+        F2Args a2{planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, kF3Cap, ctr, P.stage, dbg,
                   (uint32_t)(5 * stride - 4 < 0xFFFFFFF0ull ? 5 * stride - 4 : 0xFFFFFFF0ull)};
         k_f2_filter<<<P.nblk2, kF2Threads, f2_lds(P), s>>>(a2);
     }
     if (ev) (void)hipEventRecord(ev[2], s);
-    if (dbg & 15) {   // experiments: F1 + F2 only
+    if (dbg & ~48u) {   // experiments: F1 + F2 only
         for (int i = 3; ev && i < 5; ++i) (void)hipEventRecord(ev[i], s);
         return hipGetLastError();
     }
-    F3Args a{ireg, tabr, rbase, P.max_runs, treg, tab1, P.nblk1, P.Lm, P.b1, bitmap, P.nwords, planes, stride, n,
+    F3Args a{pbuf, pcount, kF3Cap, treg, tab1, P.nblk1, P.Lm, P.b1, bitmap, P.nwords, planes, stride, n,
              tp, ts, k, gidx, base, out_idx, out_cnt, ctr, fb_list, dbg};
     if (k <= 8) k_f3_answer<8><<<np, kF3Threads, f3_lds(P), s>>>(a);
     else if (k <= 16) k_f3_answer<16><<<np, kF3Threads, f3_lds(P), s>>>(a);

@@ -86,6 +86,8 @@ hipError_t launch_index_query(const void* ws, uint64_t n, uint32_t B, const uint
 // ev (nullable): 5 events recorded around F1, F2, F3, F4.
 bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus);
 size_t batch_bytes(uint64_t n, uint32_t q, uint32_t k, int num_cus);
+// leading workspace bytes that must be zero before the first call (they are left zero)
+size_t batch_clean_bytes();
 // device address of {fallback targets, survivors} of the last call on workspace ws
 const uint32_t* batch_stats(const void* ws);
 hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp,
