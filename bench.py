@@ -220,7 +220,7 @@ def main():
         runs = [ctx.batch_topk_timed(tp.data_ptr(), ts, q_local, a.k, out_idx.data_ptr(), out_cnt.data_ptr(), stream)
                 for _ in range(reps)]
         ph = [sum(r[0][i] for r in runs) / reps for i in range(4)]
-        n_fb, surv = runs[-1][1], runs[-1][2]
+        n_fb, surv, n_slow = runs[-1][1], runs[-1][2], runs[-1][3]
         kern = {"k_f1_targets": (ph[0], 12 * q_local),
                 "k_f2_filter": (ph[1], 4 * n_local + 8 * surv),
                 "k_f3_answer": (ph[2], 8 * surv + q_local * (8 + 16 + 4 * a.k + 4)),
@@ -237,7 +237,8 @@ def main():
                 # SURVEY 8(d) contract bytes (every id read whole, 20 B) and their time at peak
                 "contract_bytes": n_local * 20 + q_local * 20 + q_local * a.k * 4,
                 "contract_floor_ms": (n_local * 20 + q_local * 20 + q_local * a.k * 4) / HBM_PEAK_GBS / 1e6}
-        extra = {"survivors": surv, "survivor_frac": surv / max(n_local, 1), "fallback_targets": n_fb}
+        extra = {"survivors": surv, "survivor_frac": surv / max(n_local, 1), "fallback_targets": n_fb,
+                 "wave_path_targets": n_slow}
     elif a.algo == "index":
         # per-kernel device times of the index build (HIP events between its kernels, on
         # the bench stream) and of the query kernel alone

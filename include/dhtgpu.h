@@ -146,10 +146,11 @@ int dhtgpu_batch_topk_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_
                           uint32_t idx_base, void* stream);
 /* Diagnostics: the same call with HIP events between its kernels; synchronises and returns
  * per-phase device milliseconds ms4 = {F1 mark targets, F2 filter ids, F3 answer,
- * F4 fallback} and (nullable) stats2 = {targets answered by the fallback, surviving ids}. */
+ * F4 fallback} and (nullable) stats4 = {targets answered by the F4 fallback, surviving ids,
+ * targets answered by F3's exact wave path (w0 ties, large subtrees), 0}. */
 int dhtgpu_batch_topk_timed(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
                             uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, void* stream, float* ms4,
-                            uint32_t* stats2);
+                            uint32_t* stats4);
 /* Host form (synchronous). */
 int dhtgpu_batch_topk(dhtgpu_ctx* ctx, const uint8_t* targets20_be, uint32_t q, uint32_t k,
                       uint32_t* out_idx, uint32_t* out_cnt);

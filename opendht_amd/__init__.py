@@ -248,12 +248,13 @@ class Context:
 
     def batch_topk_timed(self, t_planes_ptr, t_stride, q, k, out_idx_ptr, out_cnt_ptr, stream=None):
         """One K6 call with HIP events between its kernels; returns (device ms per phase
-        (F1 mark targets, F2 filter ids, F3 answer, F4 fallback), fallback targets, survivors)."""
+        (F1 mark targets, F2 filter ids, F3 answer, F4 fallback), fallback targets, survivors,
+        targets answered by F3's exact wave path)."""
         ms = (ctypes.c_float * 4)()
-        st = (ctypes.c_uint32 * 2)()
+        st = (ctypes.c_uint32 * 4)()
         _check(lib().dhtgpu_batch_topk_timed(self._h, t_planes_ptr, t_stride, q, k, out_idx_ptr, out_cnt_ptr,
                                              stream, ms, st), "batch_topk_timed")
-        return tuple(ms), int(st[0]), int(st[1])
+        return tuple(ms), int(st[0]), int(st[1]), int(st[2])
 
     def topk_dev(self, t_planes_ptr, t_stride, q, k, out_idx_ptr=None, out_cnt_ptr=None, out_rec_ptr=None,
                  idx_base=0, stream=None):

@@ -478,7 +478,7 @@ int dhtgpu_batch_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
 }
 
 int dhtgpu_batch_topk_timed(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k,
-                            uint32_t* out_idx, uint32_t* out_cnt, void* stream, float* ms4, uint32_t* stats2) {
+                            uint32_t* out_idx, uint32_t* out_cnt, void* stream, float* ms4, uint32_t* stats4) {
     if (!c || !ms4 || k == 0 || k > DHTGPU_MAX_K || !q || !tp || !out_idx || !out_cnt) return DHTGPU_EINVAL;
     if (!c->has_ids) return DHTGPU_ENOIDS;
     DHT_TRY(c->bind());
@@ -491,8 +491,8 @@ int dhtgpu_batch_topk_timed(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint
     for (int i = 0; i < 5; ++i) (void)hipEventDestroy(ev[i]);
     if (r) return r;
     DHT_TRY(e);
-    if (stats2) {
-        DHT_TRY(hipMemcpyAsync(stats2, batch_stats(c->batch.p), 8, hipMemcpyDeviceToHost, s));
+    if (stats4) {
+        DHT_TRY(hipMemcpyAsync(stats4, batch_stats(c->batch.p), 16, hipMemcpyDeviceToHost, s));
         DHT_TRY(hipStreamSynchronize(s));
     }
     return DHTGPU_OK;

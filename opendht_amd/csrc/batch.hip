@@ -35,6 +35,8 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
+#include <vector>
 
 namespace dhtgpu {
 namespace {
@@ -52,6 +54,14 @@ constexpr uint32_t kMaxBlk1 = 4096;                  // F1 blocks (q <= 2^22)
 constexpr uint32_t kLdsMax = 160 * 1024;
 
 __device__ __forceinline__ uint32_t top_bits(uint32_t w, uint32_t b) { return b ? w >> (32 - b) : 0u; }
+
+// Workgroup barrier that orders LDS only.  __syncthreads() also drains this wave's
+// outstanding global stores (vmcnt) -- a full memory round trip after every burst of
+// result/bucket stores -- while nothing in these kernels reads another wave's global
+// stores before the kernel ends.
+__device__ __forceinline__ void sync_lds() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 // Exclusive scan of a[0, len) in LDS by a block of NT threads; returns the total.  Every
 // thread must call it.  wsum: NT / 64 + 1 words of LDS scratch.
@@ -71,7 +81,7 @@ __device__ uint32_t scan_lds(uint32_t* a, uint32_t len, uint32_t* wsum) {
         if (lane >= (uint32_t)o) x += y;
     }
     if (lane == 63) wsum[w] = x;
-    __syncthreads();
+    sync_lds();
     if (threadIdx.x < 64) {
         const uint32_t v = lane < (uint32_t)NW ? wsum[lane] : 0u;
         uint32_t xv = v;
@@ -83,7 +93,7 @@ __device__ uint32_t scan_lds(uint32_t* a, uint32_t len, uint32_t* wsum) {
         if (lane < (uint32_t)NW) wsum[lane] = xv - v;
         if (lane == (uint32_t)NW - 1) wsum[NW] = xv;
     }
-    __syncthreads();
+    sync_lds();
     uint32_t run = wsum[w] + x - s;
     for (uint32_t i = b; i < e; ++i) {
         const uint32_t v = a[i];
@@ -91,7 +101,7 @@ __device__ uint32_t scan_lds(uint32_t* a, uint32_t len, uint32_t* wsum) {
         run += v;
     }
     const uint32_t total = wsum[NW];
-    __syncthreads();
+    sync_lds();
     return total;
 }
 
@@ -117,7 +127,7 @@ __global__ __launch_bounds__(kF1Threads) void k_f1_targets(const uint32_t* __res
     uint32_t* wsum = sh + np + 1;
     for (uint32_t i = threadIdx.x; i <= np; i += kF1Threads) hist[i] = 0;
     if (blockIdx.x == 0 && threadIdx.x < 4) fb_count[threadIdx.x] = 0;   // fallback, survivors, runs
-    __syncthreads();
+    sync_lds();
     const uint32_t base = blockIdx.x * kF1Chunk;
     const uint32_t m = q - base < kF1Chunk ? q - base : kF1Chunk;
     uint32_t v[kF1Per], rk[kF1Per];
@@ -131,12 +141,12 @@ __global__ __launch_bounds__(kF1Threads) void k_f1_targets(const uint32_t* __res
             rk[e] = atomicAdd(hist + top_bits(v[e], b1), 1u);
         }
     }
-    __syncthreads();
+    sync_lds();
     scan_lds<kF1Threads>(hist, np, wsum);
     hist[np] = m;   // written by every thread, same value
-    __syncthreads();
+    sync_lds();
     for (uint32_t p = threadIdx.x; p < np; p += kF1Threads)
-        tab1[(uint64_t)p * nblk1 + blockIdx.x] = (hist[p] << 16) | (hist[p + 1] - hist[p]);
+        tab1[(uint64_t)blockIdx.x * np + p] = (hist[p] << 16) | (hist[p + 1] - hist[p]);   // row per block
 #pragma unroll
     for (int e = 0; e < kF1Per; ++e) {
         const uint32_t j = e * kF1Threads + threadIdx.x;
@@ -171,29 +181,68 @@ struct F2Args {
     uint32_t lim;                 // last 16-B aligned word offset loadable inside the plane allocation
 };
 
-// Flush the stage: per partition, one returning global atomic reserves the slots of the
-// partition's bucket (pbuf[p][...]); entries are then written at running offsets.  A
-// partition that outgrows pcap keeps counting (F3 sends its targets to the fallback).
-__device__ void f2_flush(const F2Args& a, uint32_t cnt, const uint2* stage, uint32_t* hist) {
+// Flush the stage: the entries move to registers, are counting-sorted by partition back
+// into the stage, and every partition's run is then written with consecutive lanes on
+// consecutive addresses of its bucket pbuf[p][...], whose slots one returning global
+// atomic per partition reserved.  A partition that outgrows pcap keeps counting (F3 then
+// sends its targets to the fallback).
+constexpr uint32_t kStagePer = (kStage + 1023) / 1024;
+__device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* hist, uint32_t* wsum) {
     const uint32_t np = 1u << a.b1;
-    for (uint32_t i = threadIdx.x; i < np; i += kF2Threads) hist[i] = 0;
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < cnt; j += kF2Threads) atomicAdd(hist + top_bits(stage[j].x, a.b1), 1u);
-    __syncthreads();
-    for (uint32_t p = threadIdx.x; p < np; p += kF2Threads) {
-        const uint32_t c = hist[p];
-        hist[p] = c ? atomicAdd(a.pcount + p, c) : 0u;
+    if (a.dbg & 128) { sync_lds(); return; }
+    for (uint32_t i = threadIdx.x; i <= np; i += kF2Threads) hist[i] = 0;
+    sync_lds();
+    uint2 e[kStagePer];
+    uint32_t rk[kStagePer];
+#pragma unroll
+    for (uint32_t r = 0; r < kStagePer; ++r) {
+        const uint32_t j = r * kF2Threads + threadIdx.x;
+        if (j < cnt) {
+            e[r] = stage[j];
+            rk[r] = atomicAdd(hist + top_bits(e[r].x, a.b1), 1u);
+        }
+    }
+    sync_lds();
+    // reserve the partitions' slots (before the scan overwrites the counts)
+    uint32_t res[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+        const uint32_t p = i * kF2Threads + threadIdx.x;
+        const uint32_t c = p < np ? hist[p] : 0u;
+        res[i] = c && !(a.dbg & 8) ? atomicAdd(a.pcount + p, c) : 0u;
     }
     if (threadIdx.x == 0) atomicAdd(a.ctr + 1, cnt);
-    __syncthreads();
-    if (a.dbg & 2) { __syncthreads(); return; }
-    for (uint32_t j = threadIdx.x; j < cnt; j += kF2Threads) {
-        const uint2 e = stage[j];
-        const uint32_t p = top_bits(e.x, a.b1);
-        const uint32_t pos = atomicAdd(hist + p, 1u);
-        if (pos < a.pcap) a.pbuf[(uint64_t)p * a.pcap + pos] = e;
+    scan_lds<kF2Threads>(hist, np, wsum);   // hist = partition starts inside the stage
+    if (threadIdx.x == 0) hist[np] = cnt;
+#pragma unroll
+    for (uint32_t r = 0; r < kStagePer; ++r) {
+        const uint32_t j = r * kF2Threads + threadIdx.x;
+        if (j < cnt) stage[hist[top_bits(e[r].x, a.b1)] + rk[r]] = e[r];
     }
-    __syncthreads();
+    // wsum is free again: reuse the stage-local starts to turn reservations into deltas
+    // (bucket offset of stage position j = res[p] - start[p] + j)
+    sync_lds();
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+        const uint32_t p = i * kF2Threads + threadIdx.x;
+        if (p < np) res[i] -= hist[p];
+    }
+    sync_lds();
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+        const uint32_t p = i * kF2Threads + threadIdx.x;
+        if (p < np) hist[p] = res[i];
+    }
+    sync_lds();
+    if (!(a.dbg & 2)) {
+        for (uint32_t j = threadIdx.x; j < cnt; j += kF2Threads) {
+            const uint2 x = stage[j];
+            const uint32_t p = top_bits(x.x, a.b1);
+            const uint32_t pos = hist[p] + j;
+            if (pos < a.pcap) a.pbuf[(uint64_t)p * a.pcap + pos] = x;
+        }
+    }
+    sync_lds();
 }
 
 // Loads are unconditional 16-B loads (no data-dependent branches, so every load of the
@@ -244,7 +293,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
 #pragma unroll
     for (uint32_t r = 0; r < kRing; ++r) ring[r] = f2_load1(a.w0, lo + r * kF2Sub, a.lim);
     if (threadIdx.x < 3) misc[threadIdx.x] = 0;
-    __syncthreads();
+    sync_lds();
     // Stage fill `cnt` is block-uniform.  Sub-step s reserves slots with one LDS atomic per
     // wave on counter misc[s % 3]; after the sub-step's barrier every wave adds that
     // counter to cnt.  The counter of sub-step s + 1 is zeroed during sub-step s (before
@@ -258,7 +307,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                 cnt += ring[r].x ^ ring[r].y ^ ring[r].z ^ ring[r].w;
             } else if (sb < hi) {   // block-uniform
                 if (cnt > a.stage - kF2Sub) {
-                    f2_flush(a, cnt, stage, hist);
+                    f2_flush(a, cnt, stage, hist, wsum);
                     cnt = 0;
                 }
                 const uint32_t j0 = sb + 4 * threadIdx.x;
@@ -285,15 +334,15 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                         stage[pos + (uint32_t)__popcll(bm_f & ((1ull << lane) - 1ull))] = make_uint2(v4[f], j0 + f);
                     pos += (uint32_t)__popcll(bm_f);
                 }
-                __syncthreads();
+                sync_lds();
                 cnt += misc[s3];
                 s3 = s3n;
             }
             ring[r] = f2_load1(a.w0, sb + kRing * kF2Sub, a.lim);
         }
     }
-    if (a.dbg & 64) { if (cnt == 0x12345678u) a.ctr[3] = cnt; return; }
-    if (cnt) f2_flush(a, cnt, stage, hist);
+    if (a.dbg & 64) { if (cnt == 0x12345678u) a.ctr[4] = cnt; return; }
+    if (cnt) f2_flush(a, cnt, stage, hist, wsum);
 }
 
 // ---- candidate order ------------------------------------------------------------------
@@ -331,13 +380,13 @@ __device__ __forceinline__ void load_target(const uint32_t* __restrict__ tp, uin
 constexpr uint32_t kLaneMax = 256;   // largest subtree a lane scans alone
 
 __host__ __device__ inline uint32_t f3_words(uint32_t nblk1, uint32_t nsub) {
-    return (nblk1 + 1 + 2 * nsub + 1 + 17 + kF3Threads + 1 + 1) & ~1u;
+    return (2 * nblk1 + 1 + nsub + 1 + 17 + kF3Threads + 1 + 1) & ~1u;
 }
 
 struct F3Args {
     const uint2* pbuf; uint32_t* pcount; uint32_t pcap;
     const uint2* treg; const uint32_t* tab1; uint32_t nblk1;
-    uint32_t Lm, b1;
+    uint32_t Lm, b1, Lq;
     uint32_t* bitmap; uint32_t nwords;
     const uint32_t* planes; uint64_t stride; uint64_t n;
     const uint32_t* tp; uint64_t ts; uint32_t k;
@@ -345,6 +394,7 @@ struct F3Args {
     uint32_t* out_idx; uint32_t* out_cnt;
     uint32_t* ctr; uint32_t* fb_list;   // ctr[0] = fallback targets
     uint32_t dbg;
+    unsigned long long* stamps;          // dbg & 256: per-block phase timestamps [np][8]
 };
 
 // exact wave-cooperative answer for one target (ties on w0, large subtrees)
@@ -358,10 +408,14 @@ __device__ void f3_wave_answer(const F3Args& a, const uint2* S, uint32_t lo, uin
         const bool act = lane < mm;
         const uint2 me = act ? S[lo + lane] : make_uint2(0u, 0u);
         const uint32_t md = me.x ^ t0;
+        // rank = candidates strictly closer; the other lanes' keys come from registers and
+        // the full key (id planes) is read only where two w0 distances are equal
         uint32_t rank = 0;
         for (uint32_t o = 0; o < mm; ++o) {
-            const uint2 x = S[lo + o];
-            if (act && o != lane) rank += id_less(x.x ^ t0, x.y, md, me.y, a.planes, a.stride, t);
+            const uint32_t xd = __builtin_amdgcn_readlane((int)md, (int)o);
+            const uint32_t xi = __builtin_amdgcn_readlane((int)me.y, (int)o);
+            if (xd < md) ++rank;
+            else if (xd == md && act && o != lane && id_less(xd, xi, md, me.y, a.planes, a.stride, t)) ++rank;
         }
         if (act && rank < want) orow[rank] = map_out(me.y, a.gidx, a.base);
     } else {
@@ -395,37 +449,45 @@ __device__ void f3_wave_answer(const F3Args& a, const uint2* S, uint32_t lo, uin
     if (lane == 0) a.out_cnt[qi] = want;
 }
 
+#define F3_STAMP(i) \
+    do { if ((a.dbg & 256) && threadIdx.x == 0) a.stamps[(uint64_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); } while (0)
+
 template <int K>
 __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     extern __shared__ uint32_t sh[];
     const uint32_t p = blockIdx.x, np = gridDim.x;
-    const uint32_t sb = a.Lm - a.b1, nsub = 1u << sb;
+    F3_STAMP(0);
+    // survivors are sorted by their prefix bits [b1, Lq); a target answers from the deepest
+    // level L in [Lm, Lq] whose subtree sub(t, L) holds >= want ids (a contiguous range)
+    const uint32_t nsub = 1u << (a.Lq - a.b1);
     uint32_t* toff = sh;                      // [nblk1 + 1]
-    uint32_t* sofs = toff + a.nblk1 + 1;      // [nsub + 1]
-    uint32_t* cur = sofs + nsub + 1;          // [nsub]
-    uint32_t* wsum = cur + nsub;              // [17]
+    uint32_t* tpk = toff + a.nblk1 + 1;       // [nblk1] F1 run starts of this partition
+    uint32_t* sofs = tpk + a.nblk1;           // [nsub + 1]
+    uint32_t* wsum = sofs + nsub + 1;         // [17]
     uint32_t* slow = wsum + 17;               // [kF3Threads + 1] slow-path target slots, count last
     uint2* S = reinterpret_cast<uint2*>(sh + f3_words(a.nblk1, nsub));
     uint2* T = S + kF3Cap;
     // the bitmap is no longer read in this call: clear this block's share of it
     for (uint32_t i = p + np * threadIdx.x; i < a.nwords; i += np * kF3Threads) a.bitmap[i] = 0;
-    for (uint32_t b = threadIdx.x; b < a.nblk1; b += kF3Threads) toff[b] = a.tab1[(uint64_t)p * a.nblk1 + b] & 0xFFFFu;
+    for (uint32_t b = threadIdx.x; b < a.nblk1; b += kF3Threads) {
+        const uint32_t x = a.tab1[(uint64_t)b * np + p];
+        toff[b] = x & 0xFFFFu;
+        tpk[b] = x >> 16;
+    }
     for (uint32_t i = threadIdx.x; i <= nsub; i += kF3Threads) sofs[i] = 0;
     const uint32_t m = a.pcount[p];           // survivors of this partition (F2)
-    __syncthreads();
+    sync_lds();
     const uint32_t mt = scan_lds<kF3Threads>(toff, a.nblk1, wsum);   // (barriers: every thread read m)
     if (threadIdx.x == 0) a.pcount[p] = 0;    // all-zero again for the next call
     if (mt == 0) return;   // no targets in this partition (block-uniform)
+    F3_STAMP(1);
     if (threadIdx.x == 0) toff[a.nblk1] = mt;
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     constexpr uint32_t NWV = kF3Threads / 64;
     auto target_at = [&](uint32_t j) -> uint2 {
         const uint32_t b = run_of(toff, a.nblk1, j);
-        return a.treg[(uint64_t)b * kF1Chunk + (a.tab1[(uint64_t)p * a.nblk1 + b] >> 16) + (j - toff[b])];
+        return a.treg[(uint64_t)b * kF1Chunk + tpk[b] + (j - toff[b])];
     };
-    // counting sort of the partition's survivors by sub-prefix: coalesced loads into
-    // registers, LDS histogram (ranks from the atomics), scan, placement
-    const uint32_t smask = nsub - 1u;
     if (a.dbg & 32) return;
     if (m > kF3Cap || m > a.pcap) {
         // strongly clustered ids: this partition's targets take the exact brute-force path
@@ -435,6 +497,9 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         }
         return;
     }
+    // first chunk of targets and the partition's survivors: both loads in flight together
+    const uint2 tfirst = threadIdx.x < mt ? target_at(threadIdx.x) : make_uint2(0u, 0u);
+    const uint32_t smask = nsub - 1u;
     const uint2* src = a.pbuf + (uint64_t)p * a.pcap;
     uint2 e[kF3Per];
     uint32_t rk[kF3Per];
@@ -443,41 +508,57 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         const uint32_t j = u * kF3Threads + threadIdx.x;
         e[u] = src[j < m ? j : 0];
     }
+    // counting sort by sub-prefix: LDS histogram (ranks from the atomics), scan, placement
 #pragma unroll
     for (uint32_t u = 0; u < kF3Per; ++u)
-        if (u * kF3Threads + threadIdx.x < m) rk[u] = atomicAdd(sofs + (top_bits(e[u].x, a.Lm) & smask), 1u);
-    __syncthreads();
+        if (u * kF3Threads + threadIdx.x < m) rk[u] = atomicAdd(sofs + (top_bits(e[u].x, a.Lq) & smask), 1u);
+    sync_lds();
+    F3_STAMP(2);
     scan_lds<kF3Threads>(sofs, nsub, wsum);
     if (threadIdx.x == 0) sofs[nsub] = m;
-    __syncthreads();
+    sync_lds();
 #pragma unroll
     for (uint32_t u = 0; u < kF3Per; ++u)
-        if (u * kF3Threads + threadIdx.x < m) S[sofs[top_bits(e[u].x, a.Lm) & smask] + rk[u]] = e[u];
-    __syncthreads();
+        if (u * kF3Threads + threadIdx.x < m) S[sofs[top_bits(e[u].x, a.Lq) & smask] + rk[u]] = e[u];
+    F3_STAMP(3);
     if (a.dbg & 16) return;
     const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
     for (uint32_t t0i = 0; t0i < mt; t0i += kF3Threads) {
         const uint32_t mtr = mt - t0i < kF3Threads ? mt - t0i : kF3Threads;
-        if (threadIdx.x < mtr) T[threadIdx.x] = target_at(t0i + threadIdx.x);
+        if (threadIdx.x < mtr) T[threadIdx.x] = t0i ? target_at(t0i + threadIdx.x) : tfirst;
         if (threadIdx.x == 0) slow[kF3Threads] = 0;
-        __syncthreads();
-        // A: one lane per target
-        if (threadIdx.x < mtr) {
-            const uint2 te = T[threadIdx.x];
+        sync_lds();
+        if (t0i == 0) F3_STAMP(4);
+        // A: one lane per target; targets are dealt round-robin over the waves so that
+        // every SIMD runs a share of the (latency-bound) candidate loops
+        const uint32_t slot = lane * NWV + wv;
+        if (slot < mtr) {
+            const uint2 te = T[slot];
             const uint32_t t0 = te.x, qi = te.y;
-            const uint32_t s = top_bits(t0, a.Lm) & smask;
-            const uint32_t lo = sofs[s], hi = sofs[s + 1], mm = hi - lo;
+            // deepest level L in [Lm, Lq] with >= want ids in sub(t, L)
+            const uint32_t sq = top_bits(t0, a.Lq) & smask;
+            uint32_t lo = 0, hi = 0, L = a.Lq + 1;
+            do {
+                --L;
+                const uint32_t sh_l = a.Lq - L;
+                lo = sofs[(sq >> sh_l) << sh_l];
+                hi = sofs[((sq >> sh_l) + 1) << sh_l];
+            } while (hi - lo < want && L > a.Lm);
+            const uint32_t mm = hi - lo;
             if (mm < want) {
                 a.fb_list[atomicAdd(a.ctr, 1u)] = qi;
             } else if (mm > kLaneMax || a.Lm == 0) {
-                slow[atomicAdd(slow + kF3Threads, 1u)] = threadIdx.x;
+                slow[atomicAdd(slow + kF3Threads, 1u)] = slot;
             } else {
                 uint32_t dk[K], ok[K];
 #pragma unroll
                 for (int r = 0; r < K; ++r) { dk[r] = DHT_NONE; ok[r] = DHT_NONE; }
                 uint32_t rmin = DHT_NONE;   // smallest distance that left (or never entered) the list
-                for (uint32_t o = lo; o < hi; ++o) {
-                    const uint32_t d = S[o].x ^ t0;   // < 2^(32 - Lm) <= 2^31 < NONE
+                uint32_t nxt = S[lo].x;   // next candidate's word, read one iteration ahead
+                const uint32_t hi_l = (a.dbg & 512) ? lo + want : hi;
+                for (uint32_t o = lo; o < hi_l; ++o) {
+                    const uint32_t d = nxt ^ t0;   // < 2^(32 - Lm) <= 2^31 < NONE
+                    nxt = S[o + 1 < hi ? o + 1 : o].x;
                     const bool ins = d < dk[K - 1];
                     rmin = min(rmin, ins ? dk[K - 1] : d);
                     if (ins) {
@@ -491,38 +572,50 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                         if (d < dk[0]) { dk[0] = d; ok[0] = o; }
                     }
                 }
-                // ties on w0 at or above the want-th place need the full key
+                // ties on w0 at or above the want-th place need the full key: equal
+                // neighbours among places [0, want], or a distance that left the list
+                // equal to the want-th
                 bool tie = rmin == dk[want - 1];
 #pragma unroll
-                for (int r = 0; r + 1 < K; ++r) tie = tie || ((uint32_t)r + 1 < want && dk[r] == dk[r + 1]);
-                // (r + 1 < want covers pairs inside the top-want; the pair (want-1, want)
-                // inside the list is caught by rmin unless the list is longer than want)
-                if (want < (uint32_t)K) {
-#pragma unroll
-                    for (int r = 0; r + 1 < K; ++r) tie = tie || ((uint32_t)r + 1 == want && dk[r] == dk[r + 1]);
-                }
-                if (tie) {
-                    slow[atomicAdd(slow + kF3Threads, 1u)] = threadIdx.x;
+                for (int r = 0; r + 1 < K; ++r) tie = tie || ((uint32_t)r + 1 <= want && dk[r] == dk[r + 1]);
+                if (a.dbg & 1024) {
+                    if (dk[0] == 0x7FFFFFFF) a.out_cnt[qi] = ok[1];
+                } else if (tie) {
+                    slow[atomicAdd(slow + kF3Threads, 1u)] = slot;
+                    atomicAdd(a.ctr + 3, 1u);
                 } else {
                     uint32_t* orow = a.out_idx + (uint64_t)qi * a.k;
+                    uint32_t res[K];
 #pragma unroll
-                    for (int r = 0; r < K; ++r)
-                        if ((uint32_t)r < a.k) orow[r] = (uint32_t)r < want ? map_out(S[ok[r]].y, a.gidx, a.base) : DHT_NONE;
+                    for (int r = 0; r < K; ++r) res[r] = (uint32_t)r < want ? map_out(S[ok[r]].y, a.gidx, a.base) : DHT_NONE;
+                    if (a.k == (uint32_t)K && ((uintptr_t)a.out_idx & 15) == 0) {   // whole 16-B aligned row
+#pragma unroll
+                        for (int r = 0; r < K; r += 4)
+                            *reinterpret_cast<uint4*>(orow + r) = make_uint4(res[r], res[r + 1], res[r + 2], res[r + 3]);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < K; ++r)
+                            if ((uint32_t)r < a.k) orow[r] = res[r];
+                    }
                     a.out_cnt[qi] = want;
                 }
             }
         }
-        __syncthreads();
-        // B: one wave per target for ties and large subtrees
+        sync_lds();
+        if (t0i == 0) F3_STAMP(5);
+        // B: one wave per target for ties and large subtrees (the level-Lm subtree range)
         const uint32_t ns = slow[kF3Threads];
         for (uint32_t i = wv; i < ns; i += NWV) {
             const uint2 te = T[slow[i]];
             const uint32_t t0 = __builtin_amdgcn_readfirstlane(te.x), qi = __builtin_amdgcn_readfirstlane(te.y);
-            const uint32_t s = top_bits(t0, a.Lm) & smask;
-            f3_wave_answer(a, S, sofs[s], sofs[s + 1], qi, t0, want, lane);
+            const uint32_t sh_m = a.Lq - a.Lm;
+            const uint32_t sm = (top_bits(t0, a.Lq) & smask) >> sh_m;
+            f3_wave_answer(a, S, sofs[sm << sh_m], sofs[(sm + 1) << sh_m], qi, t0, want, lane);
         }
-        __syncthreads();
+        sync_lds();
+        if (t0i == 0) F3_STAMP(6);
     }
+    F3_STAMP(7);
 }
 
 // ---- F4: exact brute force for the fallback targets -------------------------------------
@@ -593,7 +686,7 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_fallback(const uint32_t* __re
 }
 
 struct BatchPlan {
-    uint32_t Lm, b1, nwords, nblk1, nblk2, stage;
+    uint32_t Lm, b1, Lq, nwords, nblk1, nblk2, stage;
     uint64_t per_blk;
 };
 
@@ -619,6 +712,9 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     if (P.Lm > kMaxSubBits && b1 < P.Lm - kMaxSubBits) b1 = P.Lm - kMaxSubBits;
     if (b1 > 13) b1 = 13;   // kMaxParts
     P.b1 = b1;
+    // F3 sorts by up to 1 bit below the mark level (finer candidate ranges), <= 4096 bins
+    P.Lq = P.Lm + 1 < 32 ? P.Lm + 1 : 32;
+    while (P.Lq > P.Lm && P.Lq - P.b1 > 12) --P.Lq;
     P.nwords = P.Lm >= 5 ? (1u << (P.Lm - 5)) : 1u;
     P.nblk1 = (q + kF1Chunk - 1) / kF1Chunk;
     // F2: one persistent workgroup per CU, ranges in whole chunks
@@ -639,7 +735,7 @@ size_t f2_lds(const BatchPlan& P) {
 }
 
 size_t f3_lds(const BatchPlan& P) {
-    const uint32_t nsub = 1u << (P.Lm - P.b1);
+    const uint32_t nsub = 1u << (P.Lq - P.b1);
     return (size_t)f3_words(P.nblk1, nsub) * 4 + (size_t)(kF3Cap + kF3Threads) * 8;
 }
 
@@ -654,7 +750,7 @@ bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
 }
 
 // workspace: bitmap (64 KB) | ctr[4] | pcount[kMaxParts] -- these three all-zero between
-// calls -- | fb_list[q] | treg[q] | tab1[np * nblk1] | pbuf[np * kF3Cap]
+// calls -- | fb_list[q] | treg[q] | tab1[nblk1][np] | pbuf[np * kF3Cap]
 constexpr uint32_t kMaxParts = 1u << 13;
 size_t batch_clean_bytes() { return 65536 + 256 + kMaxParts * 4; }
 
@@ -708,16 +804,34 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
         k_f2_filter<<<P.nblk2, kF2Threads, f2_lds(P), s>>>(a2);
     }
     if (ev) (void)hipEventRecord(ev[2], s);
-    if (dbg & ~48u) {   // experiments: F1 + F2 only
+    if (dbg & ~(48u | 256u | 512u | 1024u)) {   // experiments: F1 + F2 only
         for (int i = 3; ev && i < 5; ++i) (void)hipEventRecord(ev[i], s);
         return hipGetLastError();
     }
-    F3Args a{pbuf, pcount, kF3Cap, treg, tab1, P.nblk1, P.Lm, P.b1, bitmap, P.nwords, planes, stride, n,
-             tp, ts, k, gidx, base, out_idx, out_cnt, ctr, fb_list, dbg};
+    static unsigned long long* stamps = nullptr;
+    if ((dbg & 256) && !stamps) (void)hipMalloc(&stamps, (size_t)8192 * 8 * 8);
+    if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)np * 8 * 8, s);
+    F3Args a{pbuf, pcount, kF3Cap, treg, tab1, P.nblk1, P.Lm, P.b1, P.Lq, bitmap, P.nwords, planes, stride, n,
+             tp, ts, k, gidx, base, out_idx, out_cnt, ctr, fb_list, dbg, stamps};
     if (k <= 8) k_f3_answer<8><<<np, kF3Threads, f3_lds(P), s>>>(a);
     else if (k <= 16) k_f3_answer<16><<<np, kF3Threads, f3_lds(P), s>>>(a);
     else k_f3_answer<32><<<np, kF3Threads, f3_lds(P), s>>>(a);
     if (ev) (void)hipEventRecord(ev[3], s);
+    if (dbg & 256) {   // phase profile of F3 (cycles, averaged over blocks)
+        std::vector<unsigned long long> h((size_t)np * 8);
+        (void)hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        double acc[8] = {0};
+        unsigned long long t0min = ~0ull, t7max = 0;
+        for (uint32_t b = 0; b < np; ++b) {
+            for (int i = 1; i < 8; ++i) acc[i] += (double)(h[b * 8 + i] - h[b * 8 + i - 1]);
+            t0min = h[b * 8] < t0min ? h[b * 8] : t0min;
+            t7max = h[b * 8 + 7] > t7max ? h[b * 8 + 7] : t7max;
+        }
+        fprintf(stderr, "F3 phases (avg cycles/block):");
+        for (int i = 1; i < 8; ++i) fprintf(stderr, " %.0f", acc[i] / np);
+        fprintf(stderr, "  span %llu\n", t7max - t0min);
+    }
     const uint32_t want = n < k ? (uint32_t)n : k;
     k_f4_fallback<<<64, kF4Threads, ((size_t)want * kF4Threads + kF4Threads / 64) * 8, s>>>(
         ctr, fb_list, planes, stride, n, tp, ts, k, gidx, base, out_idx, out_cnt);

@@ -48,6 +48,6 @@ torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / a.reps
 print(f"{a.algo} n={a.n} q={a.q} k={a.k}: {dt * 1e3:.4f} ms/call  {a.q / dt / 1e6:.1f} M q/s")
 if a.algo == "batch":
-    ms, fb, surv = ctx.batch_topk_timed(tp.data_ptr(), ts, a.q, a.k, oi.data_ptr(), oc.data_ptr(), s)
-    print("phases ms (F1,F2,F3,F4):", [round(x, 4) for x in ms], "fallback", fb, "survivors", surv)
+    ms, fb, surv, slow = ctx.batch_topk_timed(tp.data_ptr(), ts, a.q, a.k, oi.data_ptr(), oc.data_ptr(), s)
+    print("phases ms (F1,F2,F3,F4):", [round(x, 4) for x in ms], "fallback", fb, "survivors", surv, "wave-path", slow)
 ctx.close()
