@@ -81,6 +81,22 @@ def parse():
     return ap.parse_args()
 
 
+PMC_FILE = "profiles/r01_batch/pmc_traffic.json"
+
+
+def pmc_traffic(kernel, n, q, k):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
+    (tools/pmc_traffic.py; gfx950 FETCH correction applied there), when they were taken on this
+    workload (cfg 2 shape); None otherwise."""
+    try:
+        d = json.load(open(os.path.join(ROOT, PMC_FILE)))
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != [n, q, k]:
+        return None
+    return d["kernels"].get(kernel, {}).get("traffic_bytes")
+
+
 def oracle():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O
@@ -228,8 +244,11 @@ def main():
         dom = max(kern, key=lambda k: kern[k][0])
         dom_ms, dom_bytes = kern[dom]
         step_bytes = sum(v[1] for v in kern.values())
+        tb = pmc_traffic(dom, n_local, q_local, a.k)
         roof = {"bound": "hbm", "achieved": dom_bytes / (dom_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                "frac": dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "traffic": tb / (dom_ms * 1e-3) / 1e9 if tb else None,
+                "traffic_bytes_per_launch": tb, "traffic_source": PMC_FILE if tb else None,
                 "kernel": dom, "kernel_ms": dom_ms, "alg_bytes_per_launch": dom_bytes,
                 "kernels_ms": {k: v[0] for k, v in kern.items()},
                 "step_alg_bytes": step_bytes,

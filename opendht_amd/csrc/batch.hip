@@ -288,10 +288,12 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     } else {
         for (uint32_t i = threadIdx.x; i < a.nwords; i += kF2Threads) bm[i] = a.bitmap[i];
     }
-    // ring of kRing sub-steps (one 16-B load per lane each) in flight: 128 KB per CU
+    // ring of kRing sub-steps (one 16-B load per lane each) in flight: 128 KB per CU.
+    // Loads past the block's range are clamped to its last 16 B (cache hits, masked).
+    const uint32_t lim = min(a.lim, ((hi + 3u) & ~3u) - 4u);
     uint4 ring[kRing];
 #pragma unroll
-    for (uint32_t r = 0; r < kRing; ++r) ring[r] = f2_load1(a.w0, lo + r * kF2Sub, a.lim);
+    for (uint32_t r = 0; r < kRing; ++r) ring[r] = f2_load1(a.w0, lo + r * kF2Sub, lim);
     if (threadIdx.x < 3) misc[threadIdx.x] = 0;
     sync_lds();
     // Stage fill `cnt` is block-uniform.  Sub-step s reserves slots with one LDS atomic per
@@ -338,7 +340,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                 cnt += misc[s3];
                 s3 = s3n;
             }
-            ring[r] = f2_load1(a.w0, sb + kRing * kF2Sub, a.lim);
+            ring[r] = f2_load1(a.w0, sb + kRing * kF2Sub, lim);
         }
     }
     if (a.dbg & 64) { if (cnt == 0x12345678u) a.ctr[4] = cnt; return; }
