@@ -18,6 +18,9 @@
  *                          (include/opendht/node_cache.h:31, src/node_cache.cpp:42-74)
  *   dhtgpu_classify        RoutingTable::findBucket (src/routing_table.cpp:153-166) +
  *                          InfoHash::commonBits (include/opendht/infohash.h:154-176)
+ *   dhtgpu_table_depth     RoutingTable::depth (src/routing_table.cpp:100-107)
+ *   dhtgpu_buffer_nodes    NetworkEngine::bufferNodes (src/network_engine.cpp:1003-1032)
+ *   dhtgpu_deserialize_nodes  NetworkEngine::deserializeNodes (src/network_engine.cpp:849-887)
  *
  * Threading (mirrors the reference, src/dhtrunner.cpp:115-150): one context per
  * thread, or external locking; every host-pointer call is synchronous.
@@ -181,6 +184,38 @@ int dhtgpu_classify_dev(const uint32_t* planes, uint64_t stride, uint64_t n, uin
  * the reference's walk order (not sorted), indices into the id set. */
 int dhtgpu_cached_nodes(dhtgpu_ctx* ctx, const uint8_t* accept, const uint8_t* targets20_be,
                         uint32_t q, uint32_t count, uint32_t* out_idx, uint32_t* out_cnt);
+
+/* ---- a6: RoutingTable::depth (src/routing_table.cpp:100-107) over a table snapshot ---- */
+/* *out_depth = max(lowbit(first[b]), lowbit(first[b+1])) + 1 (0 for an empty table);
+ * table_depth of Dht::getNodesStats (src/dht.cpp:1425-1444) is depth(findBucket(myid)). */
+int dhtgpu_table_depth(uint32_t nb, const uint8_t* firsts20, uint32_t b, uint32_t* out_depth);
+
+/* ---- a11 / f4: compact node wire format ---------------------------------------------- */
+/* NetworkEngine::bufferNodes(af, id, nodes) (src/network_engine.cpp:1003-1032), batched:
+ * for each target, its candidates cand[qi*c .. +c) (indices into the context's id set,
+ * DHTGPU_NONE = absent, c <= 64) are sorted by InfoHash::xorCmp to the target, the first
+ * SEND_NODES = 8 are kept and written as 26-byte (af 4) / 38-byte (af 6) records
+ * id || address || port to out[qi * 8 * rec ..]; out_len[qi] = bytes written.
+ * node_tail[i*(alen+2)] = node i's address || port bytes as its sockaddr holds them
+ * (network order), alen = 4 / 16.  Equal ids (never in OpenDHT) keep candidate order. */
+int dhtgpu_buffer_nodes_dev(dhtgpu_ctx* ctx, const uint8_t* node_tail, uint32_t af, const uint32_t* t_planes,
+                            uint64_t t_stride, uint32_t q, const uint32_t* cand, uint32_t c, uint8_t* out,
+                            uint32_t* out_len, void* stream);
+int dhtgpu_buffer_nodes(dhtgpu_ctx* ctx, const uint8_t* node_tail, uint32_t af, const uint8_t* targets20,
+                        uint32_t q, const uint32_t* cand, uint32_t c, uint8_t* out, uint32_t* out_len);
+/* NetworkEngine::deserializeNodes (src/network_engine.cpp:849-887), batched over m received
+ * n4 (af 4) / n6 (af 6) blobs: message i is blob[msg_off[i] .. msg_off[i+1]), received from
+ * from_addr[i*16 ..] (family from_af[i]: 4, 6 or 0).  msg_status[i] = 1 when its length is
+ * not a whole number of records (the reference's WRONG_NODE_INFO_BUF_LEN; none of its
+ * records is decoded), else 0.  Every record of the other messages is decoded, in order,
+ * into out_ids20 / out_tail (address || port after the loopback -> sender rewrite) and
+ * out_status: 0 accepted, 1 own id (myid20), 2 martian (NetworkEngine::isMartian).
+ * *out_nrec = records decoded (<= msg_off[m] / rec); isNodeBlacklisted stays with the
+ * caller. */
+int dhtgpu_deserialize_nodes(dhtgpu_ctx* ctx, uint32_t af, const uint8_t* myid20, const uint8_t* blob,
+                             const uint64_t* msg_off, uint32_t m, const uint8_t* from_af, const uint8_t* from_addr,
+                             uint8_t* out_ids20, uint8_t* out_tail, uint8_t* out_status, uint8_t* msg_status,
+                             uint32_t* out_nrec);
 
 #ifdef __cplusplus
 }

@@ -94,6 +94,13 @@ def lib():
         "dhtgpu_batch_topk_timed": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp,
                                      ctypes.POINTER(ctypes.c_float), _u32p], ctypes.c_int),
         "dhtgpu_batch_topk": ([_vp, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p], ctypes.c_int),
+        "dhtgpu_table_depth": ([ctypes.c_uint32, _u8p, ctypes.c_uint32, _u32p], ctypes.c_int),
+        "dhtgpu_buffer_nodes_dev": ([_vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp,
+                                     ctypes.c_uint32, _vp, _vp, _vp], ctypes.c_int),
+        "dhtgpu_buffer_nodes": ([_vp, _u8p, ctypes.c_uint32, _u8p, ctypes.c_uint32, _u32p, ctypes.c_uint32, _u8p,
+                                 _u32p], ctypes.c_int),
+        "dhtgpu_deserialize_nodes": ([_vp, ctypes.c_uint32, _u8p, _u8p, _u64p, ctypes.c_uint32, _u8p, _u8p, _u8p,
+                                      _u8p, _u8p, _u8p, _u32p], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -111,7 +118,8 @@ def exported_symbols():
             "dhtgpu_gen_dev", "dhtgpu_find_closest", "dhtgpu_classify", "dhtgpu_classify_dev",
             "dhtgpu_cached_nodes", "dhtgpu_index_build", "dhtgpu_index_topk_dev", "dhtgpu_index_topk",
             "dhtgpu_index_build_timed", "dhtgpu_gen_ids_prefix", "dhtgpu_select_prefix_dev",
-            "dhtgpu_batch_topk_dev", "dhtgpu_batch_topk_timed", "dhtgpu_batch_topk"]
+            "dhtgpu_batch_topk_dev", "dhtgpu_batch_topk_timed", "dhtgpu_batch_topk", "dhtgpu_table_depth",
+            "dhtgpu_buffer_nodes_dev", "dhtgpu_buffer_nodes", "dhtgpu_deserialize_nodes"]
 
 
 def _ids(a, name="ids"):
@@ -276,6 +284,45 @@ class Context:
                                          _p(out, _u32p), _p(cnt, _u32p)), "find_closest")
         return out, cnt
 
+    # ---- a11 / f4: compact node wire format ---------------------------------------
+    def buffer_nodes(self, node_tail, af, targets, cand):
+        """NetworkEngine::bufferNodes, batched: (q, 8*rec) uint8 blobs and (q,) byte lengths."""
+        t = _ids(targets, "targets")
+        q = t.shape[0]
+        cand = np.ascontiguousarray(cand, dtype=np.uint32).reshape(q, -1)
+        alen = 4 if af == 4 else 16
+        tail = np.ascontiguousarray(node_tail, dtype=np.uint8).reshape(-1, alen + 2)
+        rec = 20 + alen + 2
+        out = np.zeros((q, 8 * rec), dtype=np.uint8)
+        ln = np.zeros(q, dtype=np.uint32)
+        _check(lib().dhtgpu_buffer_nodes(self._h, _p(tail, _u8p), af, _p(t, _u8p), q, _p(cand, _u32p),
+                                         cand.shape[1], _p(out, _u8p), _p(ln, _u32p)), "buffer_nodes")
+        return out, ln
+
+    def deserialize_nodes(self, af, myid, blobs, from_af, from_addr):
+        """NetworkEngine::deserializeNodes over a list of received blobs: returns
+        (ids (r,20), tails (r, alen+2), status (r,), msg_status (m,))."""
+        alen = 4 if af == 4 else 16
+        m = len(blobs)
+        off = np.zeros(m + 1, dtype=np.uint64)
+        for i, b in enumerate(blobs):
+            off[i + 1] = off[i] + len(b)
+        blob = np.frombuffer(b"".join(bytes(b) for b in blobs) or b"\0", dtype=np.uint8).copy()
+        fa = np.ascontiguousarray(from_af, dtype=np.uint8).reshape(m) if m else np.zeros(1, np.uint8)
+        fad = np.ascontiguousarray(from_addr, dtype=np.uint8).reshape(m, 16) if m else np.zeros((1, 16), np.uint8)
+        cap = max(1, int(off[-1]) // (20 + alen + 2))
+        ids = np.zeros((cap, 20), np.uint8)
+        tail = np.zeros((cap, alen + 2), np.uint8)
+        st = np.zeros(cap, np.uint8)
+        ms = np.zeros(max(m, 1), np.uint8)
+        nrec = ctypes.c_uint32()
+        my = np.ascontiguousarray(myid, dtype=np.uint8).reshape(20)
+        _check(lib().dhtgpu_deserialize_nodes(self._h, af, _p(my, _u8p), _p(blob, _u8p), _p(off, _u64p), m,
+                                              _p(fa, _u8p), _p(fad, _u8p), _p(ids, _u8p), _p(tail, _u8p),
+                                              _p(st, _u8p), _p(ms, _u8p), ctypes.byref(nrec)), "deserialize_nodes")
+        r = nrec.value
+        return ids[:r], tail[:r], st[:r], ms[:m]
+
     # ---- K2: classification -------------------------------------------------------
     def classify(self, firsts, myid, buckets=True):
         firsts = _ids(firsts, "firsts")
@@ -300,6 +347,14 @@ class Context:
         _check(lib().dhtgpu_cached_nodes(self._h, _p(acc, _u8p) if acc is not None else None, _p(t, _u8p), q,
                                          count, _p(out, _u32p), _p(cnt, _u32p)), "cached_nodes")
         return out, cnt
+
+
+def table_depth(firsts, b):
+    """RoutingTable::depth of bucket b of a table snapshot (src/routing_table.cpp:100-107)."""
+    f = _ids(firsts, "firsts") if len(firsts) else np.zeros((0, 20), np.uint8)
+    d = ctypes.c_uint32()
+    _check(lib().dhtgpu_table_depth(f.shape[0], _p(f, _u8p), b, ctypes.byref(d)), "table_depth")
+    return d.value
 
 
 def device_count():

@@ -68,6 +68,7 @@ struct dhtgpu_ctx {
     DevBuf index;           // K4 workspace: entries | directory | partition scratch
     uint32_t index_B = 0;
     bool index_valid = false;
+    DevBuf wire;            // wire-format staging (tails, candidates, blobs)
     DevBuf batch;           // K6 workspace; its 64 KB bitmap head is all-zero between calls
     bool batch_clean = false;
 
@@ -136,7 +137,7 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
     (void)c->bind();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->planes, &c->staging, &c->targets, &c->out_idx, &c->out_cnt, &c->rec,
-                      &c->aux, &c->aux2, &c->aux3, &c->index, &c->gidx, &c->batch})
+                      &c->aux, &c->aux2, &c->aux3, &c->index, &c->gidx, &c->batch, &c->wire})
         b->release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -640,6 +641,121 @@ int dhtgpu_cached_nodes(dhtgpu_ctx* c, const uint8_t* accept, const uint8_t* t20
     DHT_TRY(hipMemcpyAsync(out_idx, c->aux2.p, (size_t)q * count * 4, hipMemcpyDeviceToHost, c->stream));
     DHT_TRY(hipMemcpyAsync(out_cnt, c->aux3.p, (size_t)q * 4, hipMemcpyDeviceToHost, c->stream));
     DHT_TRY(hipStreamSynchronize(c->stream));
+    return DHTGPU_OK;
+}
+
+// ---- a11 / f4: compact node wire format ------------------------------------------------
+static inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
+
+int dhtgpu_buffer_nodes_dev(dhtgpu_ctx* c, const uint8_t* node_tail, uint32_t af, const uint32_t* tp, uint64_t ts,
+                            uint32_t q, const uint32_t* cand, uint32_t nc, uint8_t* out, uint32_t* out_len,
+                            void* stream) {
+    if (!c || (af != 4 && af != 6) || nc > 64) return DHTGPU_EINVAL;
+    if (q && (!tp || !out || !out_len || (nc && (!cand || !node_tail)))) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    DHT_TRY(launch_wire_encode(c->planes.as<uint32_t>(), c->stride, node_tail, af == 4 ? 4u : 16u, tp, ts, q, cand,
+                               nc, out, out_len, stream ? (hipStream_t)stream : c->stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_buffer_nodes(dhtgpu_ctx* c, const uint8_t* node_tail, uint32_t af, const uint8_t* t20, uint32_t q,
+                        const uint32_t* cand, uint32_t nc, uint8_t* out, uint32_t* out_len) {
+    if (!c || (af != 4 && af != 6) || nc > 64) return DHTGPU_EINVAL;
+    if (q && (!t20 || !out || !out_len || (nc && (!cand || !node_tail)))) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    const uint32_t alen = af == 4 ? 4u : 16u, rec = 20 + alen + 2;
+    const size_t tl = (size_t)c->n * (alen + 2), cl = (size_t)q * nc * 4, ol = (size_t)q * 8 * rec, ll = (size_t)q * 4;
+    DHT_TRY(c->wire.ensure(al256(tl) + al256(cl) + al256(ol) + al256(ll) + 256));
+    uint8_t* base = c->wire.as<uint8_t>();
+    uint8_t* d_tail = base;
+    uint32_t* d_cand = reinterpret_cast<uint32_t*>(base + al256(tl));
+    uint8_t* d_out = base + al256(tl) + al256(cl);
+    uint32_t* d_len = reinterpret_cast<uint32_t*>(d_out + al256(ol));
+    if (tl) DHT_TRY(hipMemcpyAsync(d_tail, node_tail, tl, hipMemcpyHostToDevice, c->stream));
+    if (cl) DHT_TRY(hipMemcpyAsync(d_cand, cand, cl, hipMemcpyHostToDevice, c->stream));
+    uint64_t ts = 0;
+    DHT_TRY(c->upload_targets(t20, q, &ts));
+    DHT_TRY(launch_wire_encode(c->planes.as<uint32_t>(), c->stride, d_tail, alen, c->targets.as<uint32_t>(), ts, q,
+                               d_cand, nc, d_out, d_len, c->stream));
+    DHT_TRY(hipMemcpyAsync(out, d_out, ol, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(out_len, d_len, ll, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_deserialize_nodes(dhtgpu_ctx* c, uint32_t af, const uint8_t* myid20, const uint8_t* blob,
+                             const uint64_t* msg_off, uint32_t m, const uint8_t* from_af, const uint8_t* from_addr,
+                             uint8_t* out_ids20, uint8_t* out_tail, uint8_t* out_status, uint8_t* msg_status,
+                             uint32_t* out_nrec) {
+    if (!c || (af != 4 && af != 6) || !myid20 || !out_nrec) return DHTGPU_EINVAL;
+    if (m && (!msg_off || !from_af || !from_addr || !msg_status)) return DHTGPU_EINVAL;
+    *out_nrec = 0;
+    if (!m) return DHTGPU_OK;
+    const uint32_t alen = af == 4 ? 4u : 16u, rl = 20 + alen + 2;
+    // per-message record ranges; a length that is not a whole number of records is the
+    // reference's WRONG_NODE_INFO_BUF_LEN (the message's nodes are not used)
+    std::vector<uint32_t> rs((size_t)m + 1, 0);
+    for (uint32_t i = 0; i < m; ++i) {
+        if (msg_off[i + 1] < msg_off[i]) return DHTGPU_EINVAL;
+        const uint64_t len = msg_off[i + 1] - msg_off[i];
+        msg_status[i] = len % rl ? 1 : 0;
+        const uint64_t nr = len % rl ? 0 : len / rl;
+        if ((uint64_t)rs[i] + nr > 0xFFFFFFF0ull) return DHTGPU_ERANGE;
+        rs[i + 1] = rs[i] + (uint32_t)nr;
+    }
+    const uint32_t nrec = rs[m];
+    *out_nrec = nrec;
+    if (!nrec) return DHTGPU_OK;
+    if (!blob || !out_ids20 || !out_tail || !out_status) return DHTGPU_EINVAL;
+    DHT_TRY(c->bind());
+    const uint64_t blen = msg_off[m];
+    const size_t sz[] = {(size_t)blen, ((size_t)m + 1) * 8, ((size_t)m + 1) * 4, 32, m, (size_t)m * 16,
+                         (size_t)nrec * 20, (size_t)nrec * (alen + 2), nrec};
+    size_t tot = 0;
+    for (size_t x : sz) tot += al256(x);
+    DHT_TRY(c->wire.ensure(tot));
+    uint8_t* p[9];
+    uint8_t* w = c->wire.as<uint8_t>();
+    for (int i = 0; i < 9; ++i) {
+        p[i] = w;
+        w += al256(sz[i]);
+    }
+    DHT_TRY(hipMemcpyAsync(p[0], blob, sz[0], hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(hipMemcpyAsync(p[1], msg_off, sz[1], hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(hipMemcpyAsync(p[2], rs.data(), sz[2], hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(hipMemcpyAsync(p[3], myid20, 20, hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(hipMemcpyAsync(p[4], from_af, sz[4], hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(hipMemcpyAsync(p[5], from_addr, sz[5], hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(launch_wire_decode(p[0], reinterpret_cast<const uint64_t*>(p[1]), reinterpret_cast<const uint32_t*>(p[2]),
+                               m, nrec, af, p[3], p[4], p[5], p[6], p[7], p[8], c->stream));
+    DHT_TRY(hipMemcpyAsync(out_ids20, p[6], sz[6], hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(out_tail, p[7], sz[7], hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(out_status, p[8], sz[8], hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    return DHTGPU_OK;
+}
+
+// RoutingTable::depth (src/routing_table.cpp:100-107) over a table snapshot: one more than
+// the larger lowbit (infohash.h:132-143) of the bucket's first and of the next bucket's.
+int dhtgpu_table_depth(uint32_t nb, const uint8_t* firsts20, uint32_t b, uint32_t* out_depth) {
+    if (!out_depth || (nb && !firsts20) || (nb && b >= nb)) return DHTGPU_EINVAL;
+    *out_depth = 0;
+    if (!nb) return DHTGPU_OK;
+    auto lowbit = [](const uint8_t* h) -> int {
+        int i = 19;
+        while (i >= 0 && h[i] == 0) --i;
+        if (i < 0) return -1;
+        int j = 7;
+        while (((h[i] >> (7 - j)) & 1) == 0) --j;
+        return 8 * i + j;
+    };
+    const int bit1 = lowbit(firsts20 + 20 * (size_t)b);
+    const int bit2 = b + 1 < nb ? lowbit(firsts20 + 20 * (size_t)(b + 1)) : -1;
+    *out_depth = (uint32_t)(std::max(bit1, bit2) + 1);
     return DHTGPU_OK;
 }
 

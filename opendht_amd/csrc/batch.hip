@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     if (lo64 >= a.n) return;
     const uint32_t lo = (uint32_t)lo64;
     const uint32_t hi = (uint32_t)(lo64 + a.per_blk < a.n ? lo64 + a.per_blk : a.n);
-    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t lane = lane_id();
     const uint32_t sh_lm = 32 - a.Lm;   // Lm >= 1 here is not guaranteed: handled by lm_mask
     const uint32_t lm_mask = a.Lm ? 0xFFFFFFFFu : 0u;
     // the prefix bitmap first (its loads would otherwise wait behind the id ring); indices

@@ -95,4 +95,13 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
                              uint32_t* out_idx, uint32_t* out_cnt, int num_cus, hipStream_t s,
                              hipEvent_t* ev = nullptr);
 
+// wire.hip: NetworkEngine::bufferNodes / deserializeNodes (compact node records)
+hipError_t launch_wire_encode(const uint32_t* planes, uint64_t stride, const uint8_t* tail, uint32_t alen,
+                              const uint32_t* tp, uint64_t ts, uint32_t q, const uint32_t* cand, uint32_t c,
+                              uint8_t* out, uint32_t* out_len, hipStream_t s);
+hipError_t launch_wire_decode(const uint8_t* blob, const uint64_t* msg_off, const uint32_t* rec_start, uint32_t m,
+                              uint32_t nrec, uint32_t af, const uint8_t* myid, const uint8_t* from_af,
+                              const uint8_t* from_addr, uint8_t* out_ids, uint8_t* out_tail, uint8_t* out_status,
+                              hipStream_t s);
+
 }  // namespace dhtgpu

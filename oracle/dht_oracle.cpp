@@ -318,4 +318,62 @@ uint32_t orc_cached_nodes(const uint8_t* sorted_ids20, uint64_t n, const uint8_t
     return cnt;
 }
 
+/* ---- compact node wire format (src/network_engine.cpp) ------------------------------ */
+/* NetworkEngine::bufferNodes, src/network_engine.cpp:1003-1032: std::sort by xorCmp to the
+ * target, keep SEND_NODES = 8 (:62), emit id (20 B) || sin_addr (4 B) / sin6_addr (16 B) ||
+ * port (2 B) exactly as stored in the sockaddr (network byte order): 26 / 38-byte records
+ * (NODE4/6_INFO_BUF_LEN).  `tail[i]` holds node i's address || port bytes (alen + 2).
+ * cand[c] are node indices (UINT32_MAX = absent).  std::sort is unstable; node ids are
+ * unique in the reference, and equal ids here keep their candidate order (documented
+ * extension, identical in the kernel).  Returns the blob length. */
+uint32_t orc_buffer_nodes(const uint8_t* ids20, const uint8_t* tail, uint32_t alen, const uint8_t* target20,
+                          const uint32_t* cand, uint32_t c, uint8_t* out) {
+    std::vector<uint32_t> v;
+    for (uint32_t j = 0; j < c; j++)
+        if (cand[j] != 0xFFFFFFFFu) v.push_back(cand[j]);
+    std::stable_sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) {
+        return xor_cmp(target20, ids20 + 20 * (size_t)a, ids20 + 20 * (size_t)b) < 0;
+    });
+    const uint32_t nnode = (uint32_t)std::min<size_t>(8, v.size());
+    const uint32_t rec = 20 + alen + 2;
+    for (uint32_t i = 0; i < nnode; i++) {
+        std::memcpy(out + rec * i, ids20 + 20 * (size_t)v[i], 20);
+        std::memcpy(out + rec * i + 20, tail + (size_t)(alen + 2) * v[i], alen + 2);
+    }
+    return nnode * rec;
+}
+
+/* NetworkEngine::deserializeNodes, src/network_engine.cpp:849-887, for one record of a
+ * message received from `from_addr` (family from_af: 4 or 6, 0 = none):
+ * deserializeIPv4/6 (:831-846), self skip (:858-859), loopback -> sender address with the
+ * record's port (:861-865, SockAddr::isLoopback src/utils.cpp:115-128), then
+ * NetworkEngine::isMartian (:362-386).  Writes the (possibly rewritten) address || port to
+ * out_tail; returns 0 = accepted, 1 = own id, 2 = martian.  (isNodeBlacklisted is host
+ * policy state and stays with the caller.) */
+int orc_deserialize_node(const uint8_t* rec, uint32_t af, const uint8_t* myid20, uint32_t from_af,
+                         const uint8_t* from_addr, uint8_t* out_tail) {
+    const uint32_t alen = af == 4 ? 4 : 16;
+    if (std::memcmp(rec, myid20, 20) == 0) return 1;
+    uint8_t a[16], port[2];
+    std::memcpy(a, rec + 20, alen);
+    std::memcpy(port, rec + 20 + alen, 2);
+    bool loop;
+    if (af == 4) {
+        loop = a[0] == 127;
+    } else {
+        static const uint8_t lo6[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1};
+        loop = std::memcmp(a, lo6, 16) == 0;
+    }
+    if (loop && from_af == af) std::memcpy(a, from_addr, alen);   /* addr = from; setPort(port) */
+    std::memcpy(out_tail, a, alen);
+    std::memcpy(out_tail + alen, port, 2);
+    if (port[0] == 0 && port[1] == 0) return 2;
+    if (af == 4) return (a[0] == 0 || (a[0] & 0xE0) == 0xE0) ? 2 : 0;
+    static const uint8_t zeroes[16] = {0};
+    static const uint8_t v4prefix[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0xFF, 0xFF};
+    const bool m = a[0] == 0xFF || (a[0] == 0xFE && (a[1] & 0xC0) == 0x80) || std::memcmp(a, zeroes, 16) == 0 ||
+                   std::memcmp(a, v4prefix, 12) == 0;
+    return m ? 2 : 0;
+}
+
 } // extern "C"

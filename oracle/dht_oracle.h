@@ -74,6 +74,17 @@ void orc_classify(uint32_t nb, const uint8_t* firsts20, const uint8_t* myid20,
 uint32_t orc_cached_nodes(const uint8_t* sorted_ids20, uint64_t n, const uint8_t* accept,
                           const uint8_t* target20, uint32_t count, uint32_t* out_idx);
 
+/* NetworkEngine::bufferNodes (src/network_engine.cpp:1003-1032): sort candidates by xorCmp
+ * to the target, keep 8, pack 26 (IPv4, alen 4) / 38 (IPv6, alen 16) byte records.
+ * tail[i] = node i's address || port bytes.  Returns the blob length. */
+uint32_t orc_buffer_nodes(const uint8_t* ids20, const uint8_t* tail, uint32_t alen, const uint8_t* target20,
+                          const uint32_t* cand, uint32_t c, uint8_t* out);
+/* NetworkEngine::deserializeNodes (src/network_engine.cpp:849-887) for one record:
+ * 0 = accepted, 1 = own id, 2 = martian; out_tail = address || port after the loopback
+ * rewrite.  af / from_af: 4 or 6 (from_af 0 = unknown sender family). */
+int orc_deserialize_node(const uint8_t* rec, uint32_t af, const uint8_t* myid20, uint32_t from_af,
+                         const uint8_t* from_addr, uint8_t* out_tail);
+
 #ifdef __cplusplus
 }
 #endif

@@ -56,6 +56,10 @@ def lib():
         L.orc_classify.argtypes = [ctypes.c_uint32, u8p, u8p, u8p, ctypes.c_uint64, u8p, u64p]
         L.orc_cached_nodes.argtypes = [u8p, ctypes.c_uint64, u8p, u8p, ctypes.c_uint32, u32p]
         L.orc_cached_nodes.restype = ctypes.c_uint32
+        L.orc_buffer_nodes.argtypes = [u8p, u8p, ctypes.c_uint32, u8p, u32p, ctypes.c_uint32, u8p]
+        L.orc_buffer_nodes.restype = ctypes.c_uint32
+        L.orc_deserialize_node.argtypes = [u8p, ctypes.c_uint32, u8p, ctypes.c_uint32, u8p, u8p]
+        L.orc_deserialize_node.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -176,6 +180,29 @@ def cached_nodes(sorted_ids, accept, target, count):
     return out[:c].copy()
 
 
+def buffer_nodes(ids, tail, alen, target, cand):
+    """NetworkEngine::bufferNodes restatement: blob bytes."""
+    ids = np.ascontiguousarray(ids, dtype=np.uint8)
+    tail = np.ascontiguousarray(tail, dtype=np.uint8)
+    target = np.ascontiguousarray(target, dtype=np.uint8)
+    cand = np.ascontiguousarray(cand, dtype=np.uint32)
+    out = np.zeros(8 * (22 + alen), dtype=np.uint8)
+    n = lib().orc_buffer_nodes(_p(ids, u8p), _p(tail, u8p), alen, _p(target, u8p), _p(cand, u32p), cand.shape[0],
+                               _p(out, u8p))
+    return out[:n].copy()
+
+
+def deserialize_node(rec, af, myid, from_af, from_addr):
+    """NetworkEngine::deserializeNodes for one record: (status, address || port bytes)."""
+    alen = 4 if af == 4 else 16
+    rec = np.ascontiguousarray(rec, dtype=np.uint8)
+    myid = np.ascontiguousarray(myid, dtype=np.uint8)
+    fa = np.ascontiguousarray(from_addr, dtype=np.uint8).reshape(16)
+    out = np.zeros(alen + 2, dtype=np.uint8)
+    st = lib().orc_deserialize_node(_p(rec, u8p), af, _p(myid, u8p), from_af, _p(fa, u8p), _p(out, u8p))
+    return st, out
+
+
 # ---- independent pure-Python restatement (big integers) used to cross-check the C oracle ----
 def py_dist(t, a):
     return int.from_bytes(bytes(t), "big") ^ int.from_bytes(bytes(a), "big")
@@ -185,3 +212,66 @@ def py_topk(ids, target, k):
     d = [(py_dist(target, row), i) for i, row in enumerate(ids)]
     d.sort()
     return [i for _, i in d[:k]]
+
+
+def py_buffer_nodes(ids, tail, target, cand):
+    """bufferNodes restated with big integers (stable order for equal ids)."""
+    c = [int(x) for x in cand if x != 0xFFFFFFFF]
+    c.sort(key=lambda i: py_dist(target, ids[i]))
+    out = b""
+    for i in c[:8]:
+        out += bytes(ids[i]) + bytes(tail[i])
+    return np.frombuffer(out, dtype=np.uint8)
+
+
+def py_deserialize_node(rec, af, myid, from_af, from_addr):
+    """deserializeNodes + isMartian restated from src/network_engine.cpp:362-386, :831-887."""
+    alen = 4 if af == 4 else 16
+    rec = bytes(rec)
+    if rec[:20] == bytes(myid):
+        return 1, None
+    a = bytearray(rec[20:20 + alen])
+    port = rec[20 + alen:22 + alen]
+    loop = (a[0] == 127) if af == 4 else (bytes(a) == bytes(15) + b"\x01")
+    if loop and from_af == af:
+        a = bytearray(bytes(from_addr)[:alen])
+    tailb = np.frombuffer(bytes(a) + port, dtype=np.uint8)
+    if port == b"\0\0":
+        return 2, tailb
+    if af == 4:
+        return (2 if a[0] == 0 or (a[0] & 0xE0) == 0xE0 else 0), tailb
+    m = a[0] == 0xFF or (a[0] == 0xFE and (a[1] & 0xC0) == 0x80) or bytes(a) == bytes(16) or \
+        bytes(a[:12]) == bytes(10) + b"\xff\xff"
+    return (2 if m else 0), tailb
+
+
+def special_addrs(rng, n, af):
+    """Address || port tails mixing ordinary, loopback, martian and port-0 cases."""
+    alen = 4 if af == 4 else 16
+    t = rng.integers(0, 256, size=(n, alen + 2), dtype=np.uint8)
+    k = rng.integers(0, 8, size=n)
+    for i in range(n):
+        if k[i] == 0:
+            t[i, alen:] = 0                                   # port 0
+        elif k[i] == 1:
+            if af == 4:
+                t[i, 0] = 127                                 # loopback
+            else:
+                t[i, :16] = 0
+                t[i, 15] = 1
+        elif k[i] == 2:
+            if af == 4:
+                t[i, 0] = 0
+            else:
+                t[i, 0] = 0xFF                                # multicast
+        elif k[i] == 3:
+            if af == 4:
+                t[i, 0] = 0xE0 | (t[i, 0] & 0x1F)              # class D/E
+            else:
+                t[i, 0], t[i, 1] = 0xFE, 0x80 | (t[i, 1] & 0x3F)   # link-local
+        elif k[i] == 4 and af == 6:
+            t[i, :10] = 0
+            t[i, 10:12] = 0xFF                                # v4-mapped
+        elif k[i] == 5 and af == 6:
+            t[i, :16] = 0                                     # unspecified
+    return t

@@ -58,3 +58,15 @@ def build_adapter_check(exe):
                            src, "-o", exe, "-L", libdir, "-ldhtgpu", "-L", odir, "-loracle",
                            "-Wl,-rpath," + libdir, "-Wl,-rpath," + odir])
     return exe
+
+
+def test_table_depth_vs_oracle():
+    """Host-side helper of the C ABI (no device work): RoutingTable::depth."""
+    import numpy as np
+    import oracle as O
+    import opendht_amd
+    for seed in (1, 2, 3):
+        firsts, _, _ = O.Table(O.gen_ids(seed, 1)[0]).grow(O.gen_ids(seed + 10, 20000)).export()
+        for b in range(firsts.shape[0]):
+            assert opendht_amd.table_depth(firsts, b) == O.depth(firsts, b)
+    assert opendht_amd.table_depth(np.zeros((0, 20), np.uint8), 0) == 0

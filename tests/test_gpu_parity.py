@@ -341,3 +341,69 @@ def test_batch_records_merge(ctx):
     assert np.array_equal(cnt.cpu().numpy().view(np.uint32), wcnt)
     for c in shards:
         c.close()
+
+
+@pytest.mark.parametrize("af", [4, 6])
+def test_buffer_nodes_vs_oracle(ctx, af):
+    """bufferNodes on the device: per target, its k-NN result (and shuffled / padded / short
+    candidate lists) packed into 26 / 38-byte records, byte-identical to the oracle."""
+    rng = np.random.default_rng(20 + af)
+    alen = 4 if af == 4 else 16
+    ids = O.gen_ids(950 + af, 5000)
+    ids[:50, :4] = ids[0, :4]
+    tail = O.special_addrs(rng, 5000, af)
+    ctx.set_ids(ids)
+    tg = O.gen_ids(960 + af, 400)
+    tg[:30, :4] = ids[0, :4]
+    knn, _ = ctx.topk(tg, 14)
+    cand = knn.copy()
+    for i in range(0, 400, 3):
+        rng.shuffle(cand[i])
+    cand[::5, 9:] = 0xFFFFFFFF
+    cand[7, :] = 0xFFFFFFFF
+    out, ln = ctx.buffer_nodes(tail, af, tg, cand)
+    for i in range(400):
+        want = O.buffer_nodes(ids, tail, alen, tg[i], cand[i])
+        assert ln[i] == want.size, i
+        assert np.array_equal(out[i, : ln[i]], want), i
+
+
+@pytest.mark.parametrize("af", [4, 6])
+def test_deserialize_nodes_vs_oracle(ctx, af):
+    rng = np.random.default_rng(30 + af)
+    alen = 4 if af == 4 else 16
+    rec = 22 + alen
+    myid = O.gen_ids(970, 1)[0]
+    ids = O.gen_ids(971, 3000)
+    ids[::41] = myid
+    tail = O.special_addrs(rng, 3000, af)
+    recs = np.concatenate([ids, tail], axis=1)
+    blobs, from_af, from_addr, expect = [], [], [], []
+    pos = 0
+    for m in range(300):
+        k = int(rng.integers(0, 9))
+        b = recs[pos:pos + k].reshape(-1)
+        pos += k
+        if m % 17 == 0:
+            b = np.concatenate([b, np.zeros(3, np.uint8)])     # not a whole number of records
+        blobs.append(b.tobytes())
+        from_af.append([0, 4, 6][m % 3])
+        from_addr.append(rng.integers(0, 256, size=16, dtype=np.uint8))
+    gids, gtail, gst, gms = ctx.deserialize_nodes(af, myid, blobs, np.array(from_af, np.uint8),
+                                                  np.stack(from_addr))
+    r = 0
+    for m, b in enumerate(blobs):
+        bad = len(b) % rec != 0
+        assert gms[m] == (1 if bad else 0), m
+        if bad:
+            continue
+        for j in range(len(b) // rec):
+            one = np.frombuffer(b[j * rec:(j + 1) * rec], dtype=np.uint8)
+            st, out = O.deserialize_node(one, af, myid, from_af[m], from_addr[m])
+            assert gst[r] == st, (m, j)
+            assert np.array_equal(gids[r], one[:20])
+            if st != 1:                       # own id: the reference skips the record
+                assert np.array_equal(gtail[r], out), (m, j)
+            r += 1
+    assert r == gids.shape[0]
+

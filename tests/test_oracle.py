@@ -202,3 +202,61 @@ def test_cached_nodes_restatement(n):
     for t in np.concatenate([O.gen_ids(22, 60), s[:5]]):
         for count in (1, 8, 14):
             assert list(O.cached_nodes(s, accept, t, count)) == _py_cached(s, accept, t, count)
+
+
+@pytest.mark.parametrize("af", [4, 6])
+def test_buffer_nodes_oracle_vs_python(af):
+    """bufferNodes restatement (C) == big-integer restatement, incl. absent candidates and
+    fewer than 8 nodes."""
+    rng = np.random.default_rng(af)
+    ids = O.gen_ids(700 + af, 300)
+    ids[:20, :4] = ids[0, :4]                 # shared w0 words: full-key ordering
+    alen = 4 if af == 4 else 16
+    tail = O.special_addrs(rng, 300, af)
+    for trial in range(200):
+        t = O.gen_ids(800 + trial, 1)[0]
+        if trial % 3 == 0:
+            t[:4] = ids[0, :4]
+        c = int(rng.integers(0, 33))
+        cand = rng.choice(300, size=c, replace=False).astype(np.uint32)
+        if c > 2 and trial % 2:
+            cand[rng.integers(0, c)] = 0xFFFFFFFF
+        got = O.buffer_nodes(ids, tail, alen, t, cand)
+        want = O.py_buffer_nodes(ids, tail, t, cand)
+        assert np.array_equal(got, want), trial
+        assert got.size % (22 + alen) == 0 and got.size <= 8 * (22 + alen)
+
+
+@pytest.mark.parametrize("af", [4, 6])
+def test_deserialize_node_oracle_vs_python(af):
+    rng = np.random.default_rng(10 + af)
+    alen = 4 if af == 4 else 16
+    myid = O.gen_ids(901, 1)[0]
+    ids = O.gen_ids(902, 500)
+    ids[::37] = myid
+    tail = O.special_addrs(rng, 500, af)
+    for i in range(500):
+        rec = np.concatenate([ids[i], tail[i]])
+        from_af = [0, 4, 6][i % 3]
+        from_addr = rng.integers(0, 256, size=16, dtype=np.uint8)
+        st, out = O.deserialize_node(rec, af, myid, from_af, from_addr)
+        wst, wout = O.py_deserialize_node(rec, af, myid, from_af, from_addr)
+        assert st == wst, i
+        if st != 1:
+            assert np.array_equal(out, wout), i
+
+
+def test_ipv4_record_layout_known_answer():
+    """A hand-built 26-byte record (id || sin_addr || sin_port, network order) decodes to
+    itself; 127.0.0.1 from an IPv4 sender takes the sender's address and keeps its port."""
+    myid = O.h("00" * 20)
+    rid = O.h("0123456789abcdef0123456789abcdef01234567")
+    rec = np.concatenate([rid, O.h("c0a80001"), O.h("1f90")])          # 192.168.0.1:8080
+    st, out = O.deserialize_node(rec, 4, myid, 4, np.zeros(16, np.uint8))
+    assert st == 0 and bytes(out) == bytes.fromhex("c0a800011f90")
+    rec2 = np.concatenate([rid, O.h("7f000001"), O.h("1f90")])         # 127.0.0.1:8080
+    frm = np.concatenate([O.h("0a000002"), np.zeros(12, np.uint8)])     # from 10.0.0.2
+    st, out = O.deserialize_node(rec2, 4, myid, 4, frm)
+    assert st == 0 and bytes(out) == bytes.fromhex("0a0000021f90")
+    st, _ = O.deserialize_node(np.concatenate([rid, O.h("e0000001"), O.h("1f90")]), 4, myid, 4, frm)
+    assert st == 2                                                      # 224.0.0.1: martian
