@@ -21,6 +21,8 @@
  *   dhtgpu_table_depth     RoutingTable::depth (src/routing_table.cpp:100-107)
  *   dhtgpu_buffer_nodes    NetworkEngine::bufferNodes (src/network_engine.cpp:1003-1032)
  *   dhtgpu_deserialize_nodes  NetworkEngine::deserializeNodes (src/network_engine.cpp:849-887)
+ *   dhtgpu_search_batch    Dht::Search node refresh: Search::insertNode (src/search.h:636-722)
+ *                          driven by find_node rounds (crawl replay, tools/dhtscanner.cpp)
  *
  * Threading (mirrors the reference, src/dhtrunner.cpp:115-150): one context per
  * thread, or external locking; every host-pointer call is synchronous.
@@ -216,6 +218,24 @@ int dhtgpu_deserialize_nodes(dhtgpu_ctx* ctx, uint32_t af, const uint8_t* myid20
                              const uint64_t* msg_off, uint32_t m, const uint8_t* from_af, const uint8_t* from_addr,
                              uint8_t* out_ids20, uint8_t* out_tail, uint8_t* out_status, uint8_t* msg_status,
                              uint32_t* out_nrec);
+
+/* ---- f3: crawl replay (BASELINE configs[4]) -------------------------------------------- */
+/* The context's id set becomes a synthetic network (model: opendht_amd/csrc/crawl.hip and
+ * oracle/crawl_oracle.cpp): node order by (first word, index), implicit k-bucket routing
+ * tables sampled with table_seed, dead[n] (host, nullable) marks nodes that never answer.
+ * Synchronous. */
+int dhtgpu_net_prepare(dhtgpu_ctx* ctx, const uint8_t* dead, uint64_t table_seed);
+/* One iterative search per target (Dht::Search, src/search.h: Search::insertNode :636-722,
+ * SEARCH_NODES = 14, MAX_REQUESTED_SEARCH_NODES = 4 per round, isSynced :734-747), started
+ * by node searchers[qi] from its own routing table.  Per search: the final SearchNode list
+ * out_idx[qi*64 ..] (node indices, DHTGPU_NONE padded) with out_flags (bit0 asked, bit1
+ * replied, bit2 bad), out_len, rounds run and find_node requests sent. */
+int dhtgpu_search_batch(dhtgpu_ctx* ctx, const uint8_t* targets20, uint32_t q, const uint32_t* searchers,
+                        uint32_t max_rounds, uint32_t* out_idx, uint8_t* out_flags, uint32_t* out_len,
+                        uint32_t* out_rounds, uint32_t* out_queries);
+int dhtgpu_search_batch_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
+                            const uint32_t* searchers, uint32_t max_rounds, uint32_t* out_idx, uint8_t* out_flags,
+                            uint32_t* out_len, uint32_t* out_rounds, uint32_t* out_queries, void* stream);
 
 #ifdef __cplusplus
 }

@@ -101,6 +101,11 @@ def lib():
                                  _u32p], ctypes.c_int),
         "dhtgpu_deserialize_nodes": ([_vp, ctypes.c_uint32, _u8p, _u8p, _u64p, ctypes.c_uint32, _u8p, _u8p, _u8p,
                                       _u8p, _u8p, _u8p, _u32p], ctypes.c_int),
+        "dhtgpu_net_prepare": ([_vp, _u8p, ctypes.c_uint64], ctypes.c_int),
+        "dhtgpu_search_batch": ([_vp, _u8p, ctypes.c_uint32, _u32p, ctypes.c_uint32, _u32p, _u8p, _u32p, _u32p,
+                                 _u32p], ctypes.c_int),
+        "dhtgpu_search_batch_dev": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, _vp,
+                                     _vp, _vp, _vp, _vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -119,7 +124,8 @@ def exported_symbols():
             "dhtgpu_cached_nodes", "dhtgpu_index_build", "dhtgpu_index_topk_dev", "dhtgpu_index_topk",
             "dhtgpu_index_build_timed", "dhtgpu_gen_ids_prefix", "dhtgpu_select_prefix_dev",
             "dhtgpu_batch_topk_dev", "dhtgpu_batch_topk_timed", "dhtgpu_batch_topk", "dhtgpu_table_depth",
-            "dhtgpu_buffer_nodes_dev", "dhtgpu_buffer_nodes", "dhtgpu_deserialize_nodes"]
+            "dhtgpu_buffer_nodes_dev", "dhtgpu_buffer_nodes", "dhtgpu_deserialize_nodes", "dhtgpu_net_prepare",
+            "dhtgpu_search_batch", "dhtgpu_search_batch_dev"]
 
 
 def _ids(a, name="ids"):
@@ -322,6 +328,28 @@ class Context:
                                               _p(st, _u8p), _p(ms, _u8p), ctypes.byref(nrec)), "deserialize_nodes")
         r = nrec.value
         return ids[:r], tail[:r], st[:r], ms[:m]
+
+    # ---- f3: crawl replay ------------------------------------------------------------
+    def net_prepare(self, dead=None, table_seed=0x5EED):
+        """Turn the uploaded id set into the crawl-model network (dead: (n,) bool/uint8)."""
+        d = None
+        if dead is not None:
+            d = np.ascontiguousarray(dead, dtype=np.uint8)
+            if d.shape[0] != self.num_ids:
+                raise ValueError("dead mask must have one byte per id")
+        _check(lib().dhtgpu_net_prepare(self._h, _p(d, _u8p) if d is not None else None, table_seed), "net_prepare")
+
+    def search_batch(self, targets, searchers, max_rounds=64):
+        """Iterative searches: (idx (q,64), flags (q,64), len (q,), rounds (q,), queries (q,))."""
+        t = _ids(targets, "targets")
+        q = t.shape[0]
+        sr = np.ascontiguousarray(searchers, dtype=np.uint32).reshape(q)
+        idx = np.empty((q, 64), np.uint32)
+        fl = np.empty((q, 64), np.uint8)
+        ln, rd, qs = (np.empty(q, np.uint32) for _ in range(3))
+        _check(lib().dhtgpu_search_batch(self._h, _p(t, _u8p), q, _p(sr, _u32p), max_rounds, _p(idx, _u32p),
+                                         _p(fl, _u8p), _p(ln, _u32p), _p(rd, _u32p), _p(qs, _u32p)), "search_batch")
+        return idx, fl, ln, rd, qs
 
     # ---- K2: classification -------------------------------------------------------
     def classify(self, firsts, myid, buckets=True):

@@ -69,6 +69,11 @@ struct dhtgpu_ctx {
     uint32_t index_B = 0;
     bool index_valid = false;
     DevBuf wire;            // wire-format staging (tails, candidates, blobs)
+    DevBuf net_sorted;      // crawl model: {w0, index} in node order (index rebuilt by net_prepare)
+    DevBuf net_dead;        // crawl model: dead mask (n bytes) or empty
+    DevBuf net_io;          // crawl model: search-batch staging
+    uint64_t net_seed = 0;
+    bool net_valid = false, net_has_dead = false;
     DevBuf batch;           // K6 workspace; its 64 KB bitmap head is all-zero between calls
     bool batch_clean = false;
 
@@ -137,7 +142,8 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
     (void)c->bind();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->planes, &c->staging, &c->targets, &c->out_idx, &c->out_cnt, &c->rec,
-                      &c->aux, &c->aux2, &c->aux3, &c->index, &c->gidx, &c->batch, &c->wire})
+                      &c->aux, &c->aux2, &c->aux3, &c->index, &c->gidx, &c->batch, &c->wire,
+                      &c->net_sorted, &c->net_dead, &c->net_io})
         b->release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -168,6 +174,7 @@ static int alloc_ids(dhtgpu_ctx* c, uint64_t n) {
     if (n >= 0xFFFFFFFFull) return DHTGPU_ERANGE;
     c->has_ids = false;
     c->index_valid = false;
+    c->net_valid = false;
     c->has_gidx = false;
     c->stride = pad_ids(n ? n : 1);
     DHT_TRY(c->planes.ensure((size_t)c->stride * 5 * 4));
@@ -756,6 +763,77 @@ int dhtgpu_table_depth(uint32_t nb, const uint8_t* firsts20, uint32_t b, uint32_
     const int bit1 = lowbit(firsts20 + 20 * (size_t)b);
     const int bit2 = b + 1 < nb ? lowbit(firsts20 + 20 * (size_t)(b + 1)) : -1;
     *out_depth = (uint32_t)(std::max(bit1, bit2) + 1);
+    return DHTGPU_OK;
+}
+
+// ---- f3: crawl replay (iterative searches over a synthetic network) ----------------------
+int dhtgpu_net_prepare(dhtgpu_ctx* c, const uint8_t* dead, uint64_t table_seed) {
+    if (!c) return DHTGPU_EINVAL;
+    if (!c->has_ids || !c->n) return DHTGPU_ENOIDS;
+    if (c->has_gidx) return DHTGPU_EINVAL;   // the network is the whole uploaded id set
+    int r = dhtgpu_index_build(c, c->stream);
+    if (r) return r;
+    DHT_TRY(c->net_sorted.ensure((size_t)c->n * 8));
+    DHT_TRY(launch_net_sort(c->index.p, c->n, c->index_B, c->net_sorted.as<uint2>(), c->stream));
+    c->net_has_dead = dead != nullptr;
+    if (dead) {
+        DHT_TRY(c->net_dead.ensure((size_t)c->n));
+        DHT_TRY(hipMemcpyAsync(c->net_dead.p, dead, (size_t)c->n, hipMemcpyHostToDevice, c->stream));
+    }
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    c->net_seed = table_seed;
+    c->net_valid = true;
+    return DHTGPU_OK;
+}
+
+int dhtgpu_search_batch_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, const uint32_t* searchers,
+                            uint32_t max_rounds, uint32_t* out_idx, uint8_t* out_flags, uint32_t* out_len,
+                            uint32_t* out_rounds, uint32_t* out_queries, void* stream) {
+    if (!c || (q && (!tp || !searchers || !out_idx || !out_flags || !out_len || !out_rounds || !out_queries)))
+        return DHTGPU_EINVAL;
+    if (!c->net_valid || !c->index_valid) return DHTGPU_ENOIDS;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    DHT_TRY(launch_search(c->planes.as<uint32_t>(), c->stride, c->net_sorted.as<uint2>(), c->index.p, c->n,
+                          c->index_B, c->net_has_dead ? c->net_dead.as<uint8_t>() : nullptr, c->net_seed, tp, ts, q,
+                          searchers, max_rounds, out_idx, out_flags, out_len, out_rounds, out_queries,
+                          stream ? (hipStream_t)stream : c->stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_search_batch(dhtgpu_ctx* c, const uint8_t* t20, uint32_t q, const uint32_t* searchers, uint32_t max_rounds,
+                        uint32_t* out_idx, uint8_t* out_flags, uint32_t* out_len, uint32_t* out_rounds,
+                        uint32_t* out_queries) {
+    if (!c || (q && (!t20 || !searchers || !out_idx || !out_flags || !out_len || !out_rounds || !out_queries)))
+        return DHTGPU_EINVAL;
+    if (!c->net_valid) return DHTGPU_ENOIDS;
+    if (!q) return DHTGPU_OK;
+    for (uint32_t i = 0; i < q; ++i)
+        if (searchers[i] >= c->n) return DHTGPU_EINVAL;
+    DHT_TRY(c->bind());
+    const size_t L = search_list_cap();
+    const size_t sz[] = {(size_t)q * 4, (size_t)q * L * 4, (size_t)q * L, (size_t)q * 4, (size_t)q * 4, (size_t)q * 4};
+    size_t tot = 0;
+    for (size_t x : sz) tot += al256(x);
+    DHT_TRY(c->net_io.ensure(tot));
+    uint8_t* p[6];
+    uint8_t* w = c->net_io.as<uint8_t>();
+    for (int i = 0; i < 6; ++i) {
+        p[i] = w;
+        w += al256(sz[i]);
+    }
+    uint64_t ts = 0;
+    DHT_TRY(c->upload_targets(t20, q, &ts));
+    DHT_TRY(hipMemcpyAsync(p[0], searchers, sz[0], hipMemcpyHostToDevice, c->stream));
+    int r = dhtgpu_search_batch_dev(c, c->targets.as<uint32_t>(), ts, q, (const uint32_t*)p[0], max_rounds,
+                                    (uint32_t*)p[1], p[2], (uint32_t*)p[3], (uint32_t*)p[4], (uint32_t*)p[5], c->stream);
+    if (r) return r;
+    DHT_TRY(hipMemcpyAsync(out_idx, p[1], sz[1], hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(out_flags, p[2], sz[2], hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(out_len, p[3], sz[3], hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(out_rounds, p[4], sz[4], hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(out_queries, p[5], sz[5], hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
     return DHTGPU_OK;
 }
 

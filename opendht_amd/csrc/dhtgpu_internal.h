@@ -104,4 +104,14 @@ hipError_t launch_wire_decode(const uint8_t* blob, const uint64_t* msg_off, cons
                               const uint8_t* from_addr, uint8_t* out_ids, uint8_t* out_tail, uint8_t* out_status,
                               hipStream_t s);
 
+// crawl.hip: crawl-replay model (iterative searches over implicit routing tables)
+uint32_t search_list_cap();
+// sorts the K4 index buckets (index workspace, n ids, B bits) by (w0, index) into out[n]
+hipError_t launch_net_sort(const void* index_ws, uint64_t n, uint32_t B, uint2* out, hipStream_t s);
+hipError_t launch_search(const uint32_t* planes, uint64_t stride, const uint2* sorted, const void* index_ws,
+                         uint64_t n, uint32_t B, const uint8_t* dead, uint64_t seed, const uint32_t* tp, uint64_t ts,
+                         uint32_t q, const uint32_t* searchers, uint32_t max_rounds, uint32_t* out_idx,
+                         uint8_t* out_flags, uint32_t* out_len, uint32_t* out_rounds, uint32_t* out_queries,
+                         hipStream_t s);
+
 }  // namespace dhtgpu

@@ -85,6 +85,15 @@ uint32_t orc_buffer_nodes(const uint8_t* ids20, const uint8_t* tail, uint32_t al
 int orc_deserialize_node(const uint8_t* rec, uint32_t af, const uint8_t* myid20, uint32_t from_af,
                          const uint8_t* from_addr, uint8_t* out_tail);
 
+/* Crawl-replay model (crawl_oracle.cpp header comment): one iterative search per target
+ * over an n-node network with implicit k-bucket routing tables.  Outputs the final
+ * SearchNode list (64 slots: index, flags bit0 asked / bit1 replied / bit2 bad), its
+ * length, the rounds run and the find_node requests sent. */
+void orc_search_batch(const uint8_t* ids20, uint64_t n, const uint8_t* dead, uint64_t table_seed,
+                      const uint8_t* targets20, const uint32_t* searchers, uint32_t q, uint32_t max_rounds,
+                      uint32_t* out_idx, uint8_t* out_flags, uint32_t* out_len, uint32_t* out_rounds,
+                      uint32_t* out_queries, int threads);
+
 #ifdef __cplusplus
 }
 #endif

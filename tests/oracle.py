@@ -60,6 +60,8 @@ def lib():
         L.orc_buffer_nodes.restype = ctypes.c_uint32
         L.orc_deserialize_node.argtypes = [u8p, ctypes.c_uint32, u8p, ctypes.c_uint32, u8p, u8p]
         L.orc_deserialize_node.restype = ctypes.c_int
+        L.orc_search_batch.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint64, u8p, u32p, ctypes.c_uint32,
+                                       ctypes.c_uint32, u32p, u8p, u32p, u32p, u32p, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -201,6 +203,22 @@ def deserialize_node(rec, af, myid, from_af, from_addr):
     out = np.zeros(alen + 2, dtype=np.uint8)
     st = lib().orc_deserialize_node(_p(rec, u8p), af, _p(myid, u8p), from_af, _p(fa, u8p), _p(out, u8p))
     return st, out
+
+
+def search_batch(ids, dead, table_seed, targets, searchers, max_rounds=64, threads=os.cpu_count() or 1):
+    """Crawl-replay model (oracle/crawl_oracle.cpp): (idx, flags, len, rounds, queries)."""
+    ids = np.ascontiguousarray(ids, dtype=np.uint8)
+    targets = np.ascontiguousarray(targets, dtype=np.uint8)
+    q = targets.shape[0]
+    sr = np.ascontiguousarray(searchers, dtype=np.uint32)
+    d = np.ascontiguousarray(dead, dtype=np.uint8) if dead is not None else None
+    idx = np.empty((q, 64), np.uint32)
+    fl = np.empty((q, 64), np.uint8)
+    ln, rd, qs = (np.empty(q, np.uint32) for _ in range(3))
+    lib().orc_search_batch(_p(ids, u8p), ids.shape[0], _p(d, u8p) if d is not None else None, table_seed,
+                           _p(targets, u8p), _p(sr, u32p), q, max_rounds, _p(idx, u32p), _p(fl, u8p),
+                           _p(ln, u32p), _p(rd, u32p), _p(qs, u32p), min(threads, 16))
+    return idx, fl, ln, rd, qs
 
 
 # ---- independent pure-Python restatement (big integers) used to cross-check the C oracle ----

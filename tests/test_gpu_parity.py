@@ -407,3 +407,36 @@ def test_deserialize_nodes_vs_oracle(ctx, af):
             r += 1
     assert r == gids.shape[0]
 
+
+
+@pytest.mark.parametrize("n,dead_frac,seed", [(3000, 0.0, 1), (100000, 0.2, 2), (40000, 0.5, 3)])
+def test_search_batch_vs_oracle(ctx, n, dead_frac, seed):
+    """Crawl-replay search kernel == the oracle's model, list for list (indices, flags,
+    lengths, rounds, requests)."""
+    ids = O.gen_ids(1000 + seed, n)
+    dead = (np.random.default_rng(seed).random(n) < dead_frac).astype(np.uint8) if dead_frac else None
+    tg = O.gen_ids(2000 + seed, 700)
+    tg[:40] = ids[:40]                     # targets that are network nodes
+    sr = ((np.arange(700, dtype=np.uint64) * 7919) % n).astype(np.uint32)
+    ctx.set_ids(ids)
+    ctx.net_prepare(dead, table_seed=seed)
+    got = ctx.search_batch(tg, sr)
+    want = O.search_batch(ids, dead, seed, tg, sr)
+    names = ["idx", "flags", "len", "rounds", "queries"]
+    for g, w, nm in zip(got, want, names):
+        bad = np.nonzero((g != w).reshape(g.shape[0], -1).any(axis=1))[0]
+        assert bad.size == 0, f"{nm}: {bad.size} searches differ, first {bad[:5]}"
+
+
+def test_crawl_gpu_vs_oracle(ctx):
+    """The dhtscanner crawl over the GPU search kernel visits the same steps and finds the
+    same nodes as over the oracle model."""
+    from opendht_amd import crawl
+    ids = O.gen_ids(555, 200000)
+    dead = (np.random.default_rng(5).random(200000) < 0.15).astype(np.uint8)
+    ctx.set_ids(ids)
+    ctx.net_prepare(dead, table_seed=31)
+    g = crawl.crawl(lambda t, s, r: ctx.search_batch(t, s, r), lambda ix: ids[ix], 4321)
+    o = crawl.crawl(lambda t, s, r: O.search_batch(ids, dead, 31, t, s, r), lambda ix: ids[ix], 4321)
+    assert g["steps"] == o["steps"] and g["queries"] == o["queries"] and g["rounds"] == o["rounds"]
+    assert np.array_equal(g["found"], o["found"])

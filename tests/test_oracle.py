@@ -260,3 +260,32 @@ def test_ipv4_record_layout_known_answer():
     assert st == 0 and bytes(out) == bytes.fromhex("0a0000021f90")
     st, _ = O.deserialize_node(np.concatenate([rid, O.h("e0000001"), O.h("1f90")]), 4, myid, 4, frm)
     assert st == 2                                                      # 224.0.0.1: martian
+
+
+def test_crawl_driver_on_oracle_model():
+    """dhtscanner restatement (opendht_amd/crawl.py) over the oracle's search model: the
+    scan stays within the 2^8 prefix steps of tools/dhtscanner.cpp and finds nodes close
+    to every probed prefix."""
+    from opendht_amd import crawl
+    ids = O.gen_ids(4242, 20000)
+    dead = (np.random.default_rng(1).random(20000) < 0.1).astype(np.uint8)
+    res = crawl.crawl(lambda t, s, r: O.search_batch(ids, dead, 99, t, s, r), lambda ix: ids[ix], 17)
+    assert 1 <= res["steps"] <= 256
+    assert res["found"].size > 100
+    assert res["queries"] > 0
+    # bit numbering of setBit: bit 159 is the last byte's lowest bit
+    assert crawl.set_bit(np.zeros(20, np.uint8), 159)[19] == 1
+    assert crawl.set_bit(np.zeros(20, np.uint8), 0)[0] == 0x80
+
+
+def test_search_model_converges_to_exact_topk():
+    """Size-independent property of the crawl model: with no dead nodes, nearly every
+    search ends with the exact 8 XOR-closest nodes of the network at the head of its list."""
+    ids = O.gen_ids(77, 50000)
+    tg = O.gen_ids(78, 200)
+    sr = (np.arange(200, dtype=np.uint32) * 211) % 50000
+    idx, fl, ln, rd, qs = O.search_batch(ids, None, 5, tg, sr)
+    want, _ = O.topk(ids, tg, 8)
+    exact = sum(list(idx[i, :8]) == list(want[i]) for i in range(200))
+    assert exact >= 190, exact
+    assert np.all(ln >= 8) and np.all(rd <= 64)
