@@ -11,6 +11,8 @@
  *       (include/opendht/node_cache.h:31, src/node_cache.cpp:42-74)
  *   ClosestIndex                                           flat exact k-NN over a fixed id
  *       set: std::partial_sort(.., InfoHash::xorCmp) (include/opendht/infohash.h:179-194)
+ *   bufferNodesBatch(ctx, af6, targets, nodes)             <- NetworkEngine::bufferNodes
+ *       (src/network_engine.cpp:1003-1032), batched
  *
  * The templates are written against the reference's member names only -- a table is a
  * list of buckets with `.first` (InfoHash) and `.nodes` (list of Sp<Node>); a node has
@@ -188,13 +190,66 @@ public:
         std::vector<uint32_t> idx(q * k), cnt(q);
         std::vector<std::vector<uint32_t>> res(q);
         if (q == 0) return res;
-        check(dhtgpu_topk(ctx_.get(), t.data(), (uint32_t)q, (uint32_t)k, idx.data(), cnt.data()), "topk");
+        // K6 per-batch prefix filter; the K1 streaming scan where K6's limits are exceeded
+        int rc = dhtgpu_batch_topk(ctx_.get(), t.data(), (uint32_t)q, (uint32_t)k, idx.data(), cnt.data());
+        if (rc == DHTGPU_ERANGE) rc = dhtgpu_topk(ctx_.get(), t.data(), (uint32_t)q, (uint32_t)k, idx.data(), cnt.data());
+        check(rc, "topk");
         for (size_t i = 0; i < q; ++i) res[i].assign(idx.begin() + i * k, idx.begin() + i * k + cnt[i]);
         return res;
     }
 private:
     Context& ctx_;
 };
+
+/* Drop-in for NetworkEngine::bufferNodes(af, id, nodes) (src/network_engine.cpp:1003-1032)
+ * over a batch: nodes[i] (candidates for targets[i], e.g. findClosestNodes results) are
+ * sorted by xorCmp to targets[i], the first SEND_NODES = 8 are packed as 26 (AF_INET) /
+ * 38 (AF_INET6) byte records id || address || port.  Written against the reference's
+ * member names: node->id, node->getAddr().getIPv4().sin_addr/.sin_port,
+ * getIPv6().sin6_addr/.sin6_port. */
+template <class HashT, class NodePtr>
+std::vector<std::vector<uint8_t>> bufferNodesBatch(Context& ctx, int af_inet6, const HashT* targets,
+                                                   const std::vector<std::vector<NodePtr>>& nodes) {
+    const uint32_t alen = af_inet6 ? 16u : 4u, rec = 20 + alen + 2;
+    const size_t q = nodes.size();
+    std::vector<std::vector<uint8_t>> res(q);
+    if (q == 0) return res;
+    size_t c = 0;
+    for (const auto& v : nodes) c = v.size() > c ? v.size() : c;
+    if (c > 64) throw Error(DHTGPU_EINVAL, "bufferNodes: more than 64 candidates");
+    std::vector<uint8_t> ids, tail, t;
+    std::vector<uint32_t> cand(q * (c ? c : 1), DHTGPU_NONE);
+    uint32_t n = 0;
+    for (size_t i = 0; i < q; ++i) {
+        detail::put_id(t, targets[i]);
+        for (size_t j = 0; j < nodes[i].size(); ++j, ++n) {
+            const auto& nd = nodes[i][j];
+            detail::put_id(ids, nd->id);
+            const uint8_t* a;
+            const uint8_t* p;
+            if (af_inet6) {
+                const auto& sin6 = nd->getAddr().getIPv6();
+                a = reinterpret_cast<const uint8_t*>(&sin6.sin6_addr);
+                p = reinterpret_cast<const uint8_t*>(&sin6.sin6_port);
+            } else {
+                const auto& sin = nd->getAddr().getIPv4();
+                a = reinterpret_cast<const uint8_t*>(&sin.sin_addr);
+                p = reinterpret_cast<const uint8_t*>(&sin.sin_port);
+            }
+            tail.insert(tail.end(), a, a + alen);
+            tail.insert(tail.end(), p, p + 2);
+            cand[i * c + j] = n;
+        }
+    }
+    check(dhtgpu_set_ids(ctx.get(), ids.empty() ? nullptr : ids.data(), n), "set_ids");
+    std::vector<uint8_t> out(q * 8 * rec);
+    std::vector<uint32_t> len(q);
+    check(dhtgpu_buffer_nodes(ctx.get(), tail.empty() ? nullptr : tail.data(), af_inet6 ? 6u : 4u, t.data(),
+                              (uint32_t)q, cand.data(), (uint32_t)c, out.data(), len.data()),
+          "buffer_nodes");
+    for (size_t i = 0; i < q; ++i) res[i].assign(out.begin() + i * 8 * rec, out.begin() + i * 8 * rec + len[i]);
+    return res;
+}
 
 }  // namespace dhtgpu
 
