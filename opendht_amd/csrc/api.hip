@@ -65,6 +65,7 @@ struct dhtgpu_ctx {
     bool has_ids = false;
     DevBuf gidx;            // shard -> global index map (dhtgpu_gen_ids_prefix), else unused
     bool has_gidx = false;
+    uint32_t shard_pbits = 0, shard_pval = 0;   // every id's top pbits bits == pval (prefix shard)
     DevBuf index;           // K4 workspace: entries | directory | partition scratch
     uint32_t index_B = 0;
     bool index_valid = false;
@@ -175,6 +176,7 @@ static int alloc_ids(dhtgpu_ctx* c, uint64_t n) {
     c->has_ids = false;
     c->index_valid = false;
     c->net_valid = false;
+    c->shard_pbits = c->shard_pval = 0;
     c->has_gidx = false;
     c->stride = pad_ids(n ? n : 1);
     DHT_TRY(c->planes.ensure((size_t)c->stride * 5 * 4));
@@ -231,6 +233,8 @@ int dhtgpu_gen_ids_prefix(dhtgpu_ctx* c, uint64_t seed, uint64_t start, uint64_t
     r = finish_ids(c, m);
     if (r) return r;
     c->has_gidx = true;
+    c->shard_pbits = pbits;
+    c->shard_pval = pval;
     return DHTGPU_OK;
 }
 
@@ -465,7 +469,8 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
         lc = c->out_cnt.as<uint32_t>();
     }
     DHT_TRY(launch_batch_topk(c->batch.p, c->planes.as<uint32_t>(), c->stride, c->n, tp, ts, q, k,
-                              out_rec ? nullptr : gidx, out_rec ? 0u : idx_base, li, lc, c->num_cus, s, ev));
+                              out_rec ? nullptr : gidx, out_rec ? 0u : idx_base, li, lc, c->num_cus, c->shard_pbits,
+                              c->shard_pval, s, ev));
     if (out_rec)
         DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
                                     out_rec, s));

@@ -105,6 +105,13 @@ __device__ uint32_t scan_lds(uint32_t* a, uint32_t len, uint32_t* wsum) {
     return total;
 }
 
+// median of three: with a <= b it is max(a, min(b, c)), the sorted-insertion step
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // largest r in [0, len) with a[r] <= j (a ascending, a[0] = 0 <= j)
 __device__ __forceinline__ uint32_t run_of(const uint32_t* a, uint32_t len, uint32_t j) {
     uint32_t lo = 0, hi = len;   // invariant a[lo] <= j, answer < hi
@@ -117,8 +124,14 @@ __device__ __forceinline__ uint32_t run_of(const uint32_t* a, uint32_t len, uint
 }
 
 // ---- F1: mark target prefixes, partition targets -----------------------------------
+// Shard contexts (dhtgpu_gen_ids_prefix): every id carries the same top `skip` bits
+// `pval`; all kernels work on w0 << skip (order-preserving inside the shard).  A target
+// whose top bits differ is flagged (index | kForeign) and answered by the F4 brute force.
+constexpr uint32_t kForeign = 0x80000000u;
+
 __global__ __launch_bounds__(kF1Threads) void k_f1_targets(const uint32_t* __restrict__ tw0, uint32_t q, uint32_t Lm,
-                                                          uint32_t b1, uint32_t* __restrict__ bitmap,
+                                                          uint32_t b1, uint32_t skip, uint32_t pval,
+                                                          uint32_t* __restrict__ bitmap,
                                                           uint32_t* __restrict__ tab1, uint32_t nblk1,
                                                           uint2* __restrict__ treg, uint32_t* __restrict__ fb_count) {
     extern __shared__ uint32_t sh[];   // hist[np + 1] | wsum
@@ -135,10 +148,12 @@ __global__ __launch_bounds__(kF1Threads) void k_f1_targets(const uint32_t* __res
     for (int e = 0; e < kF1Per; ++e) {
         const uint32_t j = e * kF1Threads + threadIdx.x;
         if (j < m) {
-            v[e] = tw0[base + j];
+            const uint32_t w = tw0[base + j];
+            v[e] = w << skip;
+            const bool mine = skip == 0 || (w >> (32 - skip)) == pval;
             const uint32_t pre = top_bits(v[e], Lm);
-            atomicOr(bitmap + (pre >> 5), 1u << (pre & 31));
-            rk[e] = atomicAdd(hist + top_bits(v[e], b1), 1u);
+            if (mine) atomicOr(bitmap + (pre >> 5), 1u << (pre & 31));
+            rk[e] = atomicAdd(hist + top_bits(v[e], b1), 1u) | (mine ? 0u : kForeign);
         }
     }
     sync_lds();
@@ -150,7 +165,8 @@ __global__ __launch_bounds__(kF1Threads) void k_f1_targets(const uint32_t* __res
 #pragma unroll
     for (int e = 0; e < kF1Per; ++e) {
         const uint32_t j = e * kF1Threads + threadIdx.x;
-        if (j < m) treg[base + hist[top_bits(v[e], b1)] + rk[e]] = make_uint2(v[e], base + j);
+        if (j < m)
+            treg[base + hist[top_bits(v[e], b1)] + (rk[e] & ~kForeign)] = make_uint2(v[e], (base + j) | (rk[e] & kForeign));
     }
 }
 
@@ -179,6 +195,8 @@ struct F2Args {
     uint32_t stage;               // LDS stage capacity (entries, <= kStage)
     uint32_t dbg;                 // experiment switches (0 in production)
     uint32_t lim;                 // last 16-B aligned word offset loadable inside the plane allocation
+    uint32_t skip;                // shard prefix bits (see kForeign)
+    uint32_t sparse;              // 1: no per-sub-step barrier (plan: the stage holds a block's survivors)
 };
 
 // Flush the stage: the entries move to registers, are counting-sorted by partition back
@@ -308,12 +326,13 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
             if (a.dbg & 64) {
                 cnt += ring[r].x ^ ring[r].y ^ ring[r].z ^ ring[r].w;
             } else if (sb < hi) {   // block-uniform
-                if (cnt > a.stage - kF2Sub) {
+                if (!a.sparse && cnt > a.stage - kF2Sub) {
                     f2_flush(a, cnt, stage, hist, wsum);
                     cnt = 0;
                 }
                 const uint32_t j0 = sb + 4 * threadIdx.x;
-                const uint32_t v4[4] = {ring[r].x, ring[r].y, ring[r].z, ring[r].w};
+                const uint32_t v4[4] = {ring[r].x << a.skip, ring[r].y << a.skip, ring[r].z << a.skip,
+                                        ring[r].w << a.skip};
                 uint64_t bal[4];
                 uint32_t tot = 0;
 #pragma unroll
@@ -323,6 +342,33 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                     if (a.dbg & 1) sv = (v4[f] & 0xFFFFF) == 0x12345;
                     bal[f] = __ballot(sv);
                     tot += (uint32_t)__popcll(bal[f]);
+                }
+                if (a.sparse) {
+                    // sparse survivors: the stage never fills on the planned workload, so no
+                    // barrier per sub-step -- one LDS atomic per wave reserves its slots and
+                    // the rare overflow goes straight to its partition bucket
+                    uint32_t base = 0;
+                    if (lane == 0 && tot) base = atomicAdd(misc, tot);
+                    uint32_t pos = __builtin_amdgcn_readfirstlane(base);
+#pragma unroll
+                    for (uint32_t f = 0; f < 4; ++f) {
+                        const uint64_t bm_f = bal[f];
+                        if ((bm_f >> lane) & 1ull) {
+                            const uint32_t at = pos + (uint32_t)__popcll(bm_f & ((1ull << lane) - 1ull));
+                            const uint2 e = make_uint2(v4[f], j0 + f);
+                            if (at < a.stage) {
+                                stage[at] = e;
+                            } else {
+                                const uint32_t p = top_bits(e.x, a.b1);
+                                const uint32_t slot = atomicAdd(a.pcount + p, 1u);
+                                atomicAdd(a.ctr + 1, 1u);
+                                if (slot < a.pcap) a.pbuf[(uint64_t)p * a.pcap + slot] = e;
+                            }
+                        }
+                        pos += (uint32_t)__popcll(bm_f);
+                    }
+                    ring[r] = f2_load1(a.w0, sb + kRing * kF2Sub, lim);
+                    continue;
                 }
                 const uint32_t s3n = s3 == 2 ? 0u : s3 + 1;
                 uint32_t base = 0;
@@ -344,6 +390,10 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
         }
     }
     if (a.dbg & 64) { if (cnt == 0x12345678u) a.ctr[4] = cnt; return; }
+    if (a.sparse) {
+        sync_lds();
+        cnt = misc[0] < a.stage ? misc[0] : a.stage;
+    }
     if (cnt) f2_flush(a, cnt, stage, hist, wsum);
 }
 
@@ -495,7 +545,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         // strongly clustered ids: this partition's targets take the exact brute-force path
         for (uint32_t j = threadIdx.x; j < mt; j += kF3Threads) {
             const uint2 te = target_at(j);
-            a.fb_list[atomicAdd(a.ctr, 1u)] = te.y;
+            a.fb_list[atomicAdd(a.ctr, 1u)] = te.y & ~kForeign;
         }
         return;
     }
@@ -536,7 +586,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         const uint32_t slot = lane * NWV + wv;
         if (slot < mtr) {
             const uint2 te = T[slot];
-            const uint32_t t0 = te.x, qi = te.y;
+            const uint32_t t0 = te.x, qi = te.y & ~kForeign;
             // deepest level L in [Lm, Lq] with >= want ids in sub(t, L)
             const uint32_t sq = top_bits(t0, a.Lq) & smask;
             uint32_t lo = 0, hi = 0, L = a.Lq + 1;
@@ -547,31 +597,56 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                 hi = sofs[((sq >> sh_l) + 1) << sh_l];
             } while (hi - lo < want && L > a.Lm);
             const uint32_t mm = hi - lo;
-            if (mm < want) {
+            if (mm < want || (te.y & kForeign)) {
                 a.fb_list[atomicAdd(a.ctr, 1u)] = qi;
             } else if (mm > kLaneMax || a.Lm == 0) {
                 slow[atomicAdd(slow + kF3Threads, 1u)] = slot;
             } else {
                 uint32_t dk[K], ok[K];
-#pragma unroll
-                for (int r = 0; r < K; ++r) { dk[r] = DHT_NONE; ok[r] = DHT_NONE; }
                 uint32_t rmin = DHT_NONE;   // smallest distance that left (or never entered) the list
-                uint32_t nxt = S[lo].x;   // next candidate's word, read one iteration ahead
                 const uint32_t hi_l = (a.dbg & 512) ? lo + want : hi;
-                for (uint32_t o = lo; o < hi_l; ++o) {
-                    const uint32_t d = nxt ^ t0;   // < 2^(32 - Lm) <= 2^31 < NONE
-                    nxt = S[o + 1 < hi ? o + 1 : o].x;
-                    const bool ins = d < dk[K - 1];
-                    rmin = min(rmin, ins ? dk[K - 1] : d);
-                    if (ins) {
+                if (a.Lm >= 12) {
+                    // packed keys (w0 distance << 12 | LDS position): distances are below
+                    // 2^(32 - Lm) <= 2^20 and positions below kF3Cap = 2^12, so the key order
+                    // is the (distance, position) order; one v_med3 per slot inserts
+                    uint32_t key[K];
 #pragma unroll
-                        for (int r = K - 1; r > 0; --r) {
-                            const bool up = d < dk[r - 1];
-                            const bool here = d < dk[r];
-                            ok[r] = up ? ok[r - 1] : (here ? o : ok[r]);
-                            dk[r] = up ? dk[r - 1] : (here ? d : dk[r]);
+                    for (int r = 0; r < K; ++r) key[r] = DHT_NONE;
+                    uint32_t lmin = DHT_NONE;
+                    uint32_t nxt = S[lo].x;   // next candidate's word, read one iteration ahead
+                    for (uint32_t o = lo; o < hi_l; ++o) {
+                        const uint32_t c = ((nxt ^ t0) << 12) | o;
+                        nxt = S[o + 1 < hi ? o + 1 : o].x;
+                        lmin = min(lmin, max(c, key[K - 1]));   // the key that leaves the list
+#pragma unroll
+                        for (int r = K - 1; r > 0; --r) key[r] = med3_u32(key[r - 1], key[r], c);
+                        key[0] = min(key[0], c);
+                    }
+#pragma unroll
+                    for (int r = 0; r < K; ++r) {
+                        dk[r] = key[r] == DHT_NONE ? DHT_NONE : key[r] >> 12;
+                        ok[r] = key[r] & 0xFFFu;
+                    }
+                    rmin = lmin == DHT_NONE ? DHT_NONE : lmin >> 12;
+                } else {
+#pragma unroll
+                    for (int r = 0; r < K; ++r) { dk[r] = DHT_NONE; ok[r] = DHT_NONE; }
+                    uint32_t nxt = S[lo].x;
+                    for (uint32_t o = lo; o < hi_l; ++o) {
+                        const uint32_t d = nxt ^ t0;   // < 2^(32 - Lm) <= 2^31 < NONE
+                        nxt = S[o + 1 < hi ? o + 1 : o].x;
+                        const bool ins = d < dk[K - 1];
+                        rmin = min(rmin, ins ? dk[K - 1] : d);
+                        if (ins) {
+#pragma unroll
+                            for (int r = K - 1; r > 0; --r) {
+                                const bool up = d < dk[r - 1];
+                                const bool here = d < dk[r];
+                                ok[r] = up ? ok[r - 1] : (here ? o : ok[r]);
+                                dk[r] = up ? dk[r - 1] : (here ? d : dk[r]);
+                            }
+                            if (d < dk[0]) { dk[0] = d; ok[0] = o; }
                         }
-                        if (d < dk[0]) { dk[0] = d; ok[0] = o; }
                     }
                 }
                 // ties on w0 at or above the want-th place need the full key: equal
@@ -609,12 +684,13 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         const uint32_t ns = slow[kF3Threads];
         for (uint32_t i = wv; i < ns; i += NWV) {
             const uint2 te = T[slow[i]];
-            const uint32_t t0 = __builtin_amdgcn_readfirstlane(te.x), qi = __builtin_amdgcn_readfirstlane(te.y);
+            const uint32_t t0 = __builtin_amdgcn_readfirstlane(te.x);
+            const uint32_t qi = __builtin_amdgcn_readfirstlane(te.y) & ~kForeign;
             const uint32_t sh_m = a.Lq - a.Lm;
             const uint32_t sm = (top_bits(t0, a.Lq) & smask) >> sh_m;
             f3_wave_answer(a, S, sofs[sm << sh_m], sofs[(sm + 1) << sh_m], qi, t0, want, lane);
         }
-        sync_lds();
+        if (ns || t0i + kF3Threads < mt) sync_lds();   // T / slow are reused by the next chunk
         if (t0i == 0) F3_STAMP(6);
     }
     F3_STAMP(7);
@@ -688,7 +764,7 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_fallback(const uint32_t* __re
 }
 
 struct BatchPlan {
-    uint32_t Lm, b1, Lq, nwords, nblk1, nblk2, stage;
+    uint32_t Lm, b1, Lq, nwords, nblk1, nblk2, stage, sparse;
     uint64_t per_blk;
 };
 
@@ -729,6 +805,19 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     const size_t fixed = (size_t)f2_fixed_words(P.nwords, 1u << P.b1) * 4;
     const size_t room = fixed < kLdsMax ? (kLdsMax - fixed) / 8 : 0;
     P.stage = (uint32_t)(room < kStage ? room : kStage);
+    // sparse mode when a block's survivors (mean + 8 sigma on uniform ids) fit the stage,
+    // with ranges shrunk (more blocks) while that helps
+    P.sparse = 0;
+    for (uint64_t pb = P.per_blk; pb >= kF2Step; pb /= 2) {
+        const double mean = (double)pb * f, sd = std::sqrt(mean * (1.0 - f));
+        if (mean + 8.0 * sd + 256.0 <= (double)P.stage) {
+            P.sparse = 1;
+            P.per_blk = (pb / kF2Step) * kF2Step;
+            P.nblk2 = (uint32_t)((n + P.per_blk - 1) / P.per_blk);
+            break;
+        }
+        if (pb == kF2Step) break;
+    }
     return P;
 }
 
@@ -770,7 +859,8 @@ const uint32_t* batch_stats(const void* ws) {
 
 hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp,
                              uint64_t ts, uint32_t q, uint32_t k, const uint32_t* gidx, uint32_t base,
-                             uint32_t* out_idx, uint32_t* out_cnt, int num_cus, hipStream_t s, hipEvent_t* ev) {
+                             uint32_t* out_idx, uint32_t* out_cnt, int num_cus, uint32_t skip, uint32_t pval,
+                             hipStream_t s, hipEvent_t* ev) {
     if (!q) return hipSuccess;
     const BatchPlan P = plan_batch(n, q, k, num_cus);
     const uint32_t np = 1u << P.b1;
@@ -797,12 +887,12 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
     }
     static const uint32_t dbg = getenv("DHTGPU_DBG") ? (uint32_t)atoi(getenv("DHTGPU_DBG")) : 0u;
     if (ev) (void)hipEventRecord(ev[0], s);
-    k_f1_targets<<<P.nblk1, kF1Threads, (np + 1 + 17) * 4, s>>>(tp, q, P.Lm, P.b1, bitmap, tab1, P.nblk1, treg,
+    k_f1_targets<<<P.nblk1, kF1Threads, (np + 1 + 17) * 4, s>>>(tp, q, P.Lm, P.b1, skip, pval, bitmap, tab1, P.nblk1, treg,
                                                                 ctr);
     if (ev) (void)hipEventRecord(ev[1], s);
     if (n) {
         F2Args a2{planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, kF3Cap, ctr, P.stage, dbg,
-                  (uint32_t)(5 * stride - 4 < 0xFFFFFFF0ull ? 5 * stride - 4 : 0xFFFFFFF0ull)};
+                  (uint32_t)(5 * stride - 4 < 0xFFFFFFF0ull ? 5 * stride - 4 : 0xFFFFFFF0ull), skip, P.sparse};
         k_f2_filter<<<P.nblk2, kF2Threads, f2_lds(P), s>>>(a2);
     }
     if (ev) (void)hipEventRecord(ev[2], s);

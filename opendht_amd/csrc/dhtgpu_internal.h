@@ -92,8 +92,8 @@ size_t batch_clean_bytes();
 const uint32_t* batch_stats(const void* ws);
 hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp,
                              uint64_t ts, uint32_t q, uint32_t k, const uint32_t* gidx, uint32_t base,
-                             uint32_t* out_idx, uint32_t* out_cnt, int num_cus, hipStream_t s,
-                             hipEvent_t* ev = nullptr);
+                             uint32_t* out_idx, uint32_t* out_cnt, int num_cus, uint32_t skip, uint32_t pval,
+                             hipStream_t s, hipEvent_t* ev = nullptr);
 
 // wire.hip: NetworkEngine::bufferNodes / deserializeNodes (compact node records)
 hipError_t launch_wire_encode(const uint32_t* planes, uint64_t stride, const uint8_t* tail, uint32_t alen,

@@ -254,6 +254,15 @@ def test_prefix_shard_matches_global_topk(ctx, pbits, pval):
     for fn in (ctx.topk, ctx.index_topk, ctx.batch_topk):
         got, cnt = fn(mine, 8)
         assert np.array_equal(cnt, wcnt) and np.array_equal(got, want)
+    if pbits:
+        # targets of other prefixes: the shard's own top-k (K6 answers them by brute force)
+        other = tg[top(tg) != pval][:200]
+        gl = np.nonzero(top(ids) == pval)[0].astype(np.uint32)
+        w2, c2 = O.topk(shard, other, 8)
+        w2 = np.where(w2 == 0xFFFFFFFF, w2, gl[np.minimum(w2, gl.size - 1)])
+        for fn in (ctx.topk, ctx.batch_topk):
+            got, cnt = fn(other, 8)
+            assert np.array_equal(cnt, c2) and np.array_equal(got, w2)
 
 
 def test_select_prefix_dev(ctx):
