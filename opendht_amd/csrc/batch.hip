@@ -273,6 +273,13 @@ __device__ __forceinline__ uint4 f2_load1(const uint32_t* __restrict__ w0, uint3
     return *reinterpret_cast<const uint4*>(w0 + j);
 }
 
+// Modes: kF2Dense flushes the stage whenever a sub-step could overflow it (one barrier
+// per sub-step); kF2Sparse (the plan proved a block's survivors fit the stage) has no
+// barrier in the loop and flushes once at the end; kF2Stream is the streaming-only
+// ablation (DHTGPU_DBG & 64).
+constexpr uint32_t kF2Dense = 0, kF2Sparse = 1, kF2Stream = 2;
+
+template <uint32_t Mode, bool Wide>
 __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     extern __shared__ uint32_t sh[];   // (32 spare) | misc[8] | bm[nwords] | hist[np + 1] | wsum[17] | stage
     const uint32_t np = 1u << a.b1;
@@ -286,8 +293,11 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     const uint32_t lo = (uint32_t)lo64;
     const uint32_t hi = (uint32_t)(lo64 + a.per_blk < a.n ? lo64 + a.per_blk : a.n);
     const uint32_t lane = lane_id();
-    const uint32_t sh_lm = 32 - a.Lm;   // Lm >= 1 here is not guaranteed: handled by lm_mask
-    const uint32_t lm_mask = a.Lm ? 0xFFFFFFFFu : 0u;
+    // level-Lm prefix of (w0 << skip) = bits [32 - skip - Lm, 32 - skip) of w0: one v_bfe
+    // (Wide: skip + Lm > 32, the prefix runs into the zeros shifted in)
+    const uint32_t pre_off = 32 - a.skip - a.Lm;
+    const uint32_t lm5 = a.Lm > 5 ? a.Lm - 5 : 0u;   // word index width
+    const uint32_t tid4 = 4 * threadIdx.x;
     // the prefix bitmap first (its loads would otherwise wait behind the id ring); indices
     // past the end are clamped, so a clamped lane rewrites a word with its own value
     if ((a.nwords & 3) == 0) {
@@ -314,48 +324,71 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     for (uint32_t r = 0; r < kRing; ++r) ring[r] = f2_load1(a.w0, lo + r * kF2Sub, lim);
     if (threadIdx.x < 3) misc[threadIdx.x] = 0;
     sync_lds();
-    // Stage fill `cnt` is block-uniform.  Sub-step s reserves slots with one LDS atomic per
-    // wave on counter misc[s % 3]; after the sub-step's barrier every wave adds that
-    // counter to cnt.  The counter of sub-step s + 1 is zeroed during sub-step s (before
-    // its barrier), when every read of its previous use (sub-step s - 2) is complete.
+    // Dense mode: stage fill `cnt` is block-uniform.  Sub-step s reserves slots with one
+    // LDS atomic per wave on counter misc[s % 3]; after the sub-step's barrier every wave
+    // adds that counter to cnt.  The counter of sub-step s + 1 is zeroed during sub-step s
+    // (before its barrier), when every read of its previous use (sub-step s - 2) is complete.
+    // Sparse mode: one counter misc[0] for the whole block, read after the final barrier.
     uint32_t cnt = 0, s3 = 0;
     for (uint32_t c0 = lo; c0 < hi; c0 += kRing * kF2Sub) {
 #pragma unroll
         for (uint32_t r = 0; r < kRing; ++r) {
             const uint32_t sb = c0 + r * kF2Sub;
-            if (a.dbg & 64) {
+            if (Mode == kF2Stream) {
                 cnt += ring[r].x ^ ring[r].y ^ ring[r].z ^ ring[r].w;
             } else if (sb < hi) {   // block-uniform
-                if (!a.sparse && cnt > a.stage - kF2Sub) {
+                if (Mode == kF2Dense && cnt > a.stage - kF2Sub) {
                     f2_flush(a, cnt, stage, hist, wsum);
                     cnt = 0;
                 }
                 const uint32_t j0 = sb + 4 * threadIdx.x;
-                const uint32_t v4[4] = {ring[r].x << a.skip, ring[r].y << a.skip, ring[r].z << a.skip,
-                                        ring[r].w << a.skip};
+                const uint32_t v4[4] = {ring[r].x, ring[r].y, ring[r].z, ring[r].w};
+                // lanes past hi (the block's last sub-step only) are masked by one compare
+                // against the sub-step's remaining length (block-uniform)
+                const uint32_t rem = hi - sb;
+                bool sv[4];
                 uint64_t bal[4];
-                uint32_t tot = 0;
 #pragma unroll
                 for (uint32_t f = 0; f < 4; ++f) {
-                    const uint32_t pre = (v4[f] & lm_mask) >> (sh_lm & 31);
-                    bool sv = j0 + f < hi && ((bm[pre >> 5] >> (pre & 31)) & 1u);
-                    if (a.dbg & 1) sv = (v4[f] & 0xFFFFF) == 0x12345;
-                    bal[f] = __ballot(sv);
-                    tot += (uint32_t)__popcll(bal[f]);
+                    // prefix bit: word pre >> 5 of the bitmap, bit pre & 31 (v_bfe masks it)
+                    const uint32_t pre = Wide ? (v4[f] << a.skip) >> (32 - a.Lm)
+                                              : __builtin_amdgcn_ubfe(v4[f], pre_off, a.Lm);
+                    const uint32_t wi = Wide ? pre >> 5 : __builtin_amdgcn_ubfe(v4[f], pre_off + 5, lm5);
+                    const bool hit = __builtin_amdgcn_ubfe(bm[wi], pre, 1) != 0, in = tid4 + f < rem;
+                    sv[f] = hit && in;
+                    bal[f] = __builtin_amdgcn_ballot_w64(hit) & __builtin_amdgcn_ballot_w64(in);
                 }
-                if (a.sparse) {
-                    // sparse survivors: the stage never fills on the planned workload, so no
-                    // barrier per sub-step -- one LDS atomic per wave reserves its slots and
-                    // the rare overflow goes straight to its partition bucket
-                    uint32_t base = 0;
-                    if (lane == 0 && tot) base = atomicAdd(misc, tot);
-                    uint32_t pos = __builtin_amdgcn_readfirstlane(base);
+                const uint32_t tot = (uint32_t)(__popcll(bal[0]) + __popcll(bal[1]) + __popcll(bal[2]) +
+                                                __popcll(bal[3]));
+                uint32_t base = 0;
+                const uint32_t ctr_i = Mode == kF2Sparse ? 0u : s3;
+                if (lane == 0 && tot) base = atomicAdd(misc + ctr_i, tot);
+                uint32_t pos = __builtin_amdgcn_readfirstlane(base);
+                if (Mode == kF2Dense) {
+                    pos += cnt;
+                    const uint32_t s3n = s3 == 2 ? 0u : s3 + 1;
+                    if (threadIdx.x == 0) misc[s3n] = 0;
+                    s3 = s3n;
+                }
+                if (Mode == kF2Dense || pos + tot <= a.stage) {   // wave-uniform
 #pragma unroll
                     for (uint32_t f = 0; f < 4; ++f) {
-                        const uint64_t bm_f = bal[f];
-                        if ((bm_f >> lane) & 1ull) {
-                            const uint32_t at = pos + (uint32_t)__popcll(bm_f & ((1ull << lane) - 1ull));
-                            const uint2 e = make_uint2(v4[f], j0 + f);
+                        if (sv[f]) {
+                            const uint32_t at = __builtin_amdgcn_mbcnt_hi(
+                                (uint32_t)(bal[f] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[f], pos));
+                            stage[at] = make_uint2(v4[f] << a.skip, j0 + f);
+                        }
+                        pos += (uint32_t)__popcll(bal[f]);
+                    }
+                } else {
+                    // sparse-mode overflow (never on the planned workload): the entries past
+                    // the stage go straight to their partition buckets
+#pragma unroll
+                    for (uint32_t f = 0; f < 4; ++f) {
+                        if (sv[f]) {
+                            const uint32_t at = __builtin_amdgcn_mbcnt_hi(
+                                (uint32_t)(bal[f] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[f], pos));
+                            const uint2 e = make_uint2(v4[f] << a.skip, j0 + f);
                             if (at < a.stage) {
                                 stage[at] = e;
                             } else {
@@ -365,32 +398,19 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                                 if (slot < a.pcap) a.pbuf[(uint64_t)p * a.pcap + slot] = e;
                             }
                         }
-                        pos += (uint32_t)__popcll(bm_f);
+                        pos += (uint32_t)__popcll(bal[f]);
                     }
-                    ring[r] = f2_load1(a.w0, sb + kRing * kF2Sub, lim);
-                    continue;
                 }
-                const uint32_t s3n = s3 == 2 ? 0u : s3 + 1;
-                uint32_t base = 0;
-                if (lane == 0 && tot) base = atomicAdd(misc + s3, tot);
-                if (threadIdx.x == 0) misc[s3n] = 0;
-                uint32_t pos = cnt + __builtin_amdgcn_readfirstlane(base);
-#pragma unroll
-                for (uint32_t f = 0; f < 4; ++f) {
-                    const uint64_t bm_f = bal[f];
-                    if ((bm_f >> lane) & 1ull)
-                        stage[pos + (uint32_t)__popcll(bm_f & ((1ull << lane) - 1ull))] = make_uint2(v4[f], j0 + f);
-                    pos += (uint32_t)__popcll(bm_f);
+                if (Mode == kF2Dense) {
+                    sync_lds();
+                    cnt += misc[s3 == 0 ? 2u : s3 - 1];
                 }
-                sync_lds();
-                cnt += misc[s3];
-                s3 = s3n;
             }
             ring[r] = f2_load1(a.w0, sb + kRing * kF2Sub, lim);
         }
     }
-    if (a.dbg & 64) { if (cnt == 0x12345678u) a.ctr[4] = cnt; return; }
-    if (a.sparse) {
+    if (Mode == kF2Stream) { if (cnt == 0x12345678u) a.ctr[4] = cnt; return; }
+    if (Mode == kF2Sparse) {
         sync_lds();
         cnt = misc[0] < a.stage ? misc[0] : a.stage;
     }
@@ -879,7 +899,10 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
     uint2* pbuf = reinterpret_cast<uint2*>(take((size_t)np * kF3Cap * 8));
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_f2_filter, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
+        const void* f2s[] = {(const void*)k_f2_filter<kF2Dense, false>, (const void*)k_f2_filter<kF2Sparse, false>,
+                             (const void*)k_f2_filter<kF2Stream, false>, (const void*)k_f2_filter<kF2Dense, true>,
+                             (const void*)k_f2_filter<kF2Sparse, true>};
+        for (const void* f : f2s) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
         (void)hipFuncSetAttribute((const void*)k_f3_answer<8>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
         (void)hipFuncSetAttribute((const void*)k_f3_answer<16>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
         (void)hipFuncSetAttribute((const void*)k_f3_answer<32>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
@@ -893,7 +916,13 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
     if (n) {
         F2Args a2{planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, kF3Cap, ctr, P.stage, dbg,
                   (uint32_t)(5 * stride - 4 < 0xFFFFFFF0ull ? 5 * stride - 4 : 0xFFFFFFF0ull), skip, P.sparse};
-        k_f2_filter<<<P.nblk2, kF2Threads, f2_lds(P), s>>>(a2);
+        const dim3 g2(P.nblk2), b2(kF2Threads);
+        const size_t l2 = f2_lds(P);
+        if (dbg & 64) k_f2_filter<kF2Stream, false><<<g2, b2, l2, s>>>(a2);
+        else if (skip + P.Lm > 32 && P.sparse) k_f2_filter<kF2Sparse, true><<<g2, b2, l2, s>>>(a2);
+        else if (skip + P.Lm > 32) k_f2_filter<kF2Dense, true><<<g2, b2, l2, s>>>(a2);
+        else if (P.sparse) k_f2_filter<kF2Sparse, false><<<g2, b2, l2, s>>>(a2);
+        else k_f2_filter<kF2Dense, false><<<g2, b2, l2, s>>>(a2);
     }
     if (ev) (void)hipEventRecord(ev[2], s);
     if (dbg & ~(48u | 256u | 512u | 1024u)) {   // experiments: F1 + F2 only
