@@ -33,24 +33,30 @@
 #include "dhtgpu_dev.h"
 #include "dhtgpu_internal.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
+#include <string>
 #include <vector>
 
 namespace dhtgpu {
 namespace {
 
-constexpr int kF1Threads = 256;
-constexpr int kF1Per = 4;
-constexpr uint32_t kF1Chunk = kF1Threads * kF1Per;   // targets per F1 block
+constexpr int kF1Threads = 256;                      // one thread per target
 constexpr int kF3Threads = 256;
 constexpr uint32_t kF3Cap = 4096;                    // survivors per partition staged in LDS
 constexpr uint32_t kF3Per = kF3Cap / kF3Threads;
 constexpr int kF4Threads = 256;
 constexpr uint32_t kMaxLm = 19;                      // 2^19-bit bitmap = 64 KB of LDS in F2
 constexpr uint32_t kMaxSubBits = 11;                 // F3 sub-prefix histogram <= 2048 bins
-constexpr uint32_t kMaxBlk1 = 4096;                  // F1 blocks (q <= 2^22)
+constexpr uint32_t kMaxQ = 1u << 22;                 // targets per call
+constexpr uint32_t kTieSlots = 4;                    // deferred-tie slots per F3 partition (F4 waves)
+// F1's per-target bucket counters tcount[p] sit 256 B apart: their returning atomics execute
+// at the memory side, one request per lane (random partitions), and counters packed into one
+// 4 KB run would all queue on the same channel.  F2's pcount stays packed: its flush reserves
+// consecutive partitions from consecutive lanes, which coalesce into one request per line.
+constexpr uint32_t kCtrStride = 64;
 constexpr uint32_t kLdsMax = 160 * 1024;
 
 __device__ __forceinline__ uint32_t top_bits(uint32_t w, uint32_t b) { return b ? w >> (32 - b) : 0u; }
@@ -112,62 +118,43 @@ __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
     return r;
 }
 
-// largest r in [0, len) with a[r] <= j (a ascending, a[0] = 0 <= j)
-__device__ __forceinline__ uint32_t run_of(const uint32_t* a, uint32_t len, uint32_t j) {
-    uint32_t lo = 0, hi = len;   // invariant a[lo] <= j, answer < hi
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a[mid] <= j) lo = mid;
-        else hi = mid;
-    }
-    return lo;
-}
-
-// ---- F1: mark target prefixes, partition targets -----------------------------------
-// Shard contexts (dhtgpu_gen_ids_prefix): every id carries the same top `skip` bits
-// `pval`; all kernels work on w0 << skip (order-preserving inside the shard).  A target
-// whose top bits differ is flagged (index | kForeign) and answered by the F4 brute force.
-constexpr uint32_t kForeign = 0x80000000u;
+// ---- F1: mark target prefixes, bucket the targets by partition ----------------------------
+// One thread per target: it sets the target's level-Lm prefix bit in the bitmap and appends
+// {w0 << skip, index} to its partition's bucket tbuf[p][...] (slot from a returning atomic on
+// tcount[p]; F3 reads the bucket as one coalesced run).  Shard contexts
+// (dhtgpu_gen_ids_prefix): every id carries the same top `skip` bits `pval`; all kernels work
+// on w0 << skip (order-preserving inside the shard).  A target whose top bits differ
+// (foreign), or whose bucket is full, goes to the spill list (count ctr[kSpill]); F3 moves
+// the spill list to the F4 fallback list.
+constexpr uint32_t kSpill = 8;   // ctr word: spilled targets (all-zero between calls)
 
 __global__ __launch_bounds__(kF1Threads) void k_f1_targets(const uint32_t* __restrict__ tw0, uint32_t q, uint32_t Lm,
                                                           uint32_t b1, uint32_t skip, uint32_t pval,
-                                                          uint32_t* __restrict__ bitmap,
-                                                          uint32_t* __restrict__ tab1, uint32_t nblk1,
-                                                          uint2* __restrict__ treg, uint32_t* __restrict__ fb_count) {
-    extern __shared__ uint32_t sh[];   // hist[np + 1] | wsum
-    const uint32_t np = 1u << b1;
-    uint32_t* hist = sh;
-    uint32_t* wsum = sh + np + 1;
-    for (uint32_t i = threadIdx.x; i <= np; i += kF1Threads) hist[i] = 0;
-    if (blockIdx.x == 0 && threadIdx.x < 4) fb_count[threadIdx.x] = 0;   // fallback, survivors, runs
-    sync_lds();
-    const uint32_t base = blockIdx.x * kF1Chunk;
-    const uint32_t m = q - base < kF1Chunk ? q - base : kF1Chunk;
-    uint32_t v[kF1Per], rk[kF1Per];
-#pragma unroll
-    for (int e = 0; e < kF1Per; ++e) {
-        const uint32_t j = e * kF1Threads + threadIdx.x;
-        if (j < m) {
-            const uint32_t w = tw0[base + j];
-            v[e] = w << skip;
-            const bool mine = skip == 0 || (w >> (32 - skip)) == pval;
-            const uint32_t pre = top_bits(v[e], Lm);
-            if (mine) atomicOr(bitmap + (pre >> 5), 1u << (pre & 31));
-            rk[e] = atomicAdd(hist + top_bits(v[e], b1), 1u) | (mine ? 0u : kForeign);
+                                                          uint32_t* __restrict__ bitmap, uint32_t* __restrict__ tcount,
+                                                          uint2* __restrict__ tbuf, uint32_t tcap,
+                                                          uint32_t* __restrict__ ctr, uint32_t* __restrict__ tspill) {
+    if (blockIdx.x == 0 && threadIdx.x < 4) ctr[threadIdx.x] = 0;   // fallback, survivors, wave path, -
+    const uint32_t i = blockIdx.x * kF1Threads + threadIdx.x;
+    if (i >= q) return;
+    const uint32_t w = tw0[i];
+    const uint32_t v = w << skip;
+    if (skip == 0 || (w >> (32 - skip)) == pval) {
+        const uint32_t pre = top_bits(v, Lm);
+        atomicOr(bitmap + (pre >> 5), 1u << (pre & 31));
+        const uint32_t p = top_bits(v, b1);
+        const uint32_t slot = atomicAdd(tcount + p * kCtrStride, 1u);
+        if (slot < tcap) {
+            tbuf[(uint64_t)p * tcap + slot] = make_uint2(v, i);
+            return;
         }
     }
-    sync_lds();
-    scan_lds<kF1Threads>(hist, np, wsum);
-    hist[np] = m;   // written by every thread, same value
-    sync_lds();
-    for (uint32_t p = threadIdx.x; p < np; p += kF1Threads)
-        tab1[(uint64_t)blockIdx.x * np + p] = (hist[p] << 16) | (hist[p + 1] - hist[p]);   // row per block
-#pragma unroll
-    for (int e = 0; e < kF1Per; ++e) {
-        const uint32_t j = e * kF1Threads + threadIdx.x;
-        if (j < m)
-            treg[base + hist[top_bits(v[e], b1)] + (rk[e] & ~kForeign)] = make_uint2(v[e], (base + j) | (rk[e] & kForeign));
-    }
+    // spill: one atomic per wave (a single counter would serialise every lane's add)
+    const uint64_t sp = __ballot(1);   // the lanes still here (the others returned)
+    const uint32_t lane = lane_id();
+    uint32_t base = 0;
+    if (lane == (uint32_t)__ffsll((long long)sp) - 1) base = atomicAdd(ctr + kSpill, (uint32_t)__popcll(sp));
+    base = __shfl((int)base, __ffsll((long long)sp) - 1);
+    tspill[base + (uint32_t)__popcll(sp & ((1ull << lane) - 1ull))] = i;
 }
 
 // ---- F2: stream w0, keep ids in marked subtrees, partition them ----------------------
@@ -195,7 +182,7 @@ struct F2Args {
     uint32_t stage;               // LDS stage capacity (entries, <= kStage)
     uint32_t dbg;                 // experiment switches (0 in production)
     uint32_t lim;                 // last 16-B aligned word offset loadable inside the plane allocation
-    uint32_t skip;                // shard prefix bits (see kForeign)
+    uint32_t skip;                // shard prefix bits (see F1)
     uint32_t sparse;              // 1: no per-sub-step barrier (plan: the stage holds a block's survivors)
 };
 
@@ -439,25 +426,29 @@ __device__ __forceinline__ void load_target(const uint32_t* __restrict__ tp, uin
 }
 
 // ---- F3: one workgroup per partition --------------------------------------------------
-// Setup: the partition's survivor runs are counting-sorted into LDS by the remaining
-// Lm - b1 prefix bits (two passes over the runs: histogram, then placement by running
-// offsets).  Queries, per chunk of kF3Threads targets:
-//   A  one LANE per target: a register-resident sorted top-K of its subtree's candidates
-//      keyed by (w0 distance, LDS position) -- exact unless two candidates' w0 words tie
-//      at or above the k-th place, which the lane detects (adjacent equal distances in its
-//      list, or an evicted/rejected distance equal to the k-th);
-//   B  targets with such ties or with large subtrees: one WAVE per target, exact order by
+// Setup: the partition's survivors (F2 bucket) and targets (F1 bucket) are loaded together;
+// the survivors are counting-sorted into LDS by their prefix bits [b1, Lq).  Queries, per
+// chunk of kF3Threads targets:
+//   A  G lanes per target (G = 4, 2 or 1 as the chunk fills the block): each lane keeps a
+//      register-resident sorted top-K of its share of the subtree's candidates keyed by
+//      (w0 distance, LDS position), the group merges them (DPP butterflies) -- exact
+//      unless two candidates' w0 words tie at or above the k-th place, which the group
+//      detects (adjacent equal distances, or an evicted distance equal to the k-th);
+//      such a target's candidates are handed to F4 (a wave per target, off this block's
+//      critical path) while one of the partition's kTieSlots slots is free;
+//   B  the remaining ties and large subtrees: one WAVE per target here, exact order by
 //      the full 160-bit key (words 1..4 read from the id planes).
 // Targets whose subtree holds fewer than min(k, n) ids go to the F4 fallback list.
 constexpr uint32_t kLaneMax = 256;   // largest subtree a lane scans alone
 
-__host__ __device__ inline uint32_t f3_words(uint32_t nblk1, uint32_t nsub) {
-    return (2 * nblk1 + 1 + nsub + 1 + 17 + kF3Threads + 1 + 1) & ~1u;
+__host__ __device__ inline uint32_t f3_words(uint32_t nsub) {
+    return (nsub + 1 + 17 + kF3Threads + 1 + 1 + 1) & ~1u;
 }
 
 struct F3Args {
     const uint2* pbuf; uint32_t* pcount; uint32_t pcap;
-    const uint2* treg; const uint32_t* tab1; uint32_t nblk1;
+    const uint2* tbuf; uint32_t* tcount; uint32_t tcap;   // F1 target buckets (tcount all-zero between calls)
+    const uint32_t* tspill;
     uint32_t Lm, b1, Lq;
     uint32_t* bitmap; uint32_t nwords;
     const uint32_t* planes; uint64_t stride; uint64_t n;
@@ -465,11 +456,23 @@ struct F3Args {
     const uint32_t* gidx; uint32_t base;
     uint32_t* out_idx; uint32_t* out_cnt;
     uint32_t* ctr; uint32_t* fb_list;   // ctr[0] = fallback targets
+    uint4* tie_hdr;                      // [np][kTieSlots] deferred ties {qi, t0, count, 0} (count 0 = free)
+    uint2* tie_cand;                     // [np][kTieSlots][64] their candidates {w0, idx}
     uint32_t dbg;
-    unsigned long long* stamps;          // dbg & 256: per-block phase timestamps [np][8]
+    unsigned long long* stamps;          // dbg & 256: per-block phase timestamps [np][16]
 };
 
-// exact wave-cooperative answer for one target (ties on w0, large subtrees)
+// (w0 distance, w1 distance, index) order; words 2..4 are read only when both distances tie
+__device__ __forceinline__ bool key2_less(uint32_t da, uint32_t a1, uint32_t ia, uint32_t db, uint32_t b1, uint32_t ib,
+                                          const uint32_t* __restrict__ planes, uint64_t stride, const uint32_t* t) {
+    if (da != db) return da < db;
+    if (a1 != b1) return a1 < b1;
+    return id_less(da, ia, db, ib, planes, stride, t);
+}
+
+// exact wave-cooperative answer for one target (ties on w0, large subtrees).  Every lane
+// gathers word 1 of its candidate up front (one round trip for the whole wave), so the
+// ordering loops below compare (w0, w1) distances in registers.
 __device__ void f3_wave_answer(const F3Args& a, const uint2* S, uint32_t lo, uint32_t hi, uint32_t qi,
                                uint32_t t0, uint32_t want, uint32_t lane) {
     uint32_t t[DHT_W];
@@ -480,38 +483,43 @@ __device__ void f3_wave_answer(const F3Args& a, const uint2* S, uint32_t lo, uin
         const bool act = lane < mm;
         const uint2 me = act ? S[lo + lane] : make_uint2(0u, 0u);
         const uint32_t md = me.x ^ t0;
-        // rank = candidates strictly closer; the other lanes' keys come from registers and
-        // the full key (id planes) is read only where two w0 distances are equal
+        const uint32_t m1 = act ? a.planes[a.stride + me.y] ^ t[1] : DHT_NONE;
+        // rank = candidates strictly closer
         uint32_t rank = 0;
         for (uint32_t o = 0; o < mm; ++o) {
             const uint32_t xd = __builtin_amdgcn_readlane((int)md, (int)o);
+            const uint32_t x1 = __builtin_amdgcn_readlane((int)m1, (int)o);
             const uint32_t xi = __builtin_amdgcn_readlane((int)me.y, (int)o);
-            if (xd < md) ++rank;
-            else if (xd == md && act && o != lane && id_less(xd, xi, md, me.y, a.planes, a.stride, t)) ++rank;
+            if (xd < md || (xd == md && x1 < m1)) ++rank;
+            else if (xd == md && x1 == m1 && act && o != lane && id_less(xd, xi, md, me.y, a.planes, a.stride, t)) ++rank;
         }
         if (act && rank < want) orow[rank] = map_out(me.y, a.gidx, a.base);
     } else {
-        // running lane-distributed top-`want` list
-        uint32_t ed = DHT_NONE, ei = DHT_NONE, cnt = 0;
+        // running lane-distributed top-`want` list of (w0 distance, w1 distance, index)
+        uint32_t ed = DHT_NONE, e1 = DHT_NONE, ei = DHT_NONE, cnt = 0;
         for (uint32_t c = lo; c < hi; c += 64) {
             const bool v = c + lane < hi;
             const uint2 x = v ? S[c + lane] : make_uint2(0u, DHT_NONE);
             const uint32_t xd = x.x ^ t0, xi = x.y;
+            const uint32_t x1 = v ? a.planes[a.stride + xi] ^ t[1] : DHT_NONE;
             uint32_t wd = cnt == want ? __builtin_amdgcn_readlane((int)ed, want - 1) : DHT_NONE;
+            uint32_t w1 = cnt == want ? __builtin_amdgcn_readlane((int)e1, want - 1) : DHT_NONE;
             uint32_t wi = cnt == want ? __builtin_amdgcn_readlane((int)ei, want - 1) : DHT_NONE;
-            uint64_t cm = __ballot(v && (cnt < want || id_less(xd, xi, wd, wi, a.planes, a.stride, t)));
+            uint64_t cm = __ballot(v && (cnt < want || key2_less(xd, x1, xi, wd, w1, wi, a.planes, a.stride, t)));
             while (cm) {
                 const uint32_t l = (uint32_t)__ffsll((long long)cm) - 1;
                 cm &= cm - 1;
-                const uint32_t cd = __builtin_amdgcn_readlane((int)xd, l), ci = __builtin_amdgcn_readlane((int)xi, l);
-                if (cnt == want && !id_less(cd, ci, wd, wi, a.planes, a.stride, t)) continue;
-                const bool closer = lane < cnt && id_less(ed, ei, cd, ci, a.planes, a.stride, t);
+                const uint32_t cd = __builtin_amdgcn_readlane((int)xd, l), c1 = __builtin_amdgcn_readlane((int)x1, l);
+                const uint32_t ci = __builtin_amdgcn_readlane((int)xi, l);
+                if (cnt == want && !key2_less(cd, c1, ci, wd, w1, wi, a.planes, a.stride, t)) continue;
+                const bool closer = lane < cnt && key2_less(ed, e1, ei, cd, c1, ci, a.planes, a.stride, t);
                 const uint32_t pos = (uint32_t)__popcll(__ballot(closer));
-                const uint32_t ud = __shfl_up(ed, 1), ui = __shfl_up(ei, 1);
-                if (lane == pos) { ed = cd; ei = ci; }
-                else if (lane > pos) { ed = ud; ei = ui; }
+                const uint32_t ud = __shfl_up(ed, 1), u1 = __shfl_up(e1, 1), ui = __shfl_up(ei, 1);
+                if (lane == pos) { ed = cd; e1 = c1; ei = ci; }
+                else if (lane > pos) { ed = ud; e1 = u1; ei = ui; }
                 cnt = cnt + 1 < want ? cnt + 1 : want;
                 wd = cnt == want ? __builtin_amdgcn_readlane((int)ed, want - 1) : DHT_NONE;
+                w1 = cnt == want ? __builtin_amdgcn_readlane((int)e1, want - 1) : DHT_NONE;
                 wi = cnt == want ? __builtin_amdgcn_readlane((int)ei, want - 1) : DHT_NONE;
             }
         }
@@ -521,8 +529,35 @@ __device__ void f3_wave_answer(const F3Args& a, const uint2* S, uint32_t lo, uin
     if (lane == 0) a.out_cnt[qi] = want;
 }
 
+// Merge the top-K list of this lane with its DPP partner's (CTRL: quad_perm lane ^ 1 or ^ 2):
+// both lists ascending, so min(mine[r], partner[K-1-r]) holds the K smallest of the union as a
+// bitonic sequence (the max side -- the K that leave -- lowers lmin); a half-cleaner network
+// then sorts it.  Both partners end with the same list.
+template <int K, int CTRL>
+__device__ __forceinline__ void f3_merge(uint32_t (&key)[K], uint32_t& lmin) {
+    uint32_t b[K];
+#pragma unroll
+    for (int r = 0; r < K; ++r) b[r] = (uint32_t)__builtin_amdgcn_mov_dpp((int)key[K - 1 - r], CTRL, 0xF, 0xF, true);
+    lmin = min(lmin, (uint32_t)__builtin_amdgcn_mov_dpp((int)lmin, CTRL, 0xF, 0xF, true));
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+        lmin = min(lmin, max(key[r], b[r]));
+        key[r] = min(key[r], b[r]);
+    }
+#pragma unroll
+    for (int d = K / 2; d >= 1; d >>= 1) {
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+            if (r & d) continue;
+            const uint32_t x = min(key[r], key[r + d]), y = max(key[r], key[r + d]);
+            key[r] = x;
+            key[r + d] = y;
+        }
+    }
+}
+
 #define F3_STAMP(i) \
-    do { if ((a.dbg & 256) && threadIdx.x == 0) a.stamps[(uint64_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); } while (0)
+    do { if ((a.dbg & 256) && threadIdx.x == 0) a.stamps[(uint64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
 template <int K>
 __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
@@ -532,49 +567,50 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     // survivors are sorted by their prefix bits [b1, Lq); a target answers from the deepest
     // level L in [Lm, Lq] whose subtree sub(t, L) holds >= want ids (a contiguous range)
     const uint32_t nsub = 1u << (a.Lq - a.b1);
-    uint32_t* toff = sh;                      // [nblk1 + 1]
-    uint32_t* tpk = toff + a.nblk1 + 1;       // [nblk1] F1 run starts of this partition
-    uint32_t* sofs = tpk + a.nblk1;           // [nsub + 1]
+    uint32_t* sofs = sh;                      // [nsub + 1]
     uint32_t* wsum = sofs + nsub + 1;         // [17]
     uint32_t* slow = wsum + 17;               // [kF3Threads + 1] slow-path target slots, count last
-    uint2* S = reinterpret_cast<uint2*>(sh + f3_words(a.nblk1, nsub));
+    uint32_t* ntie = slow + kF3Threads + 1;   // [1] deferred-tie slots taken
+    uint2* S = reinterpret_cast<uint2*>(sh + f3_words(nsub));
     uint2* T = S + kF3Cap;
     // the bitmap is no longer read in this call: clear this block's share of it
     for (uint32_t i = p + np * threadIdx.x; i < a.nwords; i += np * kF3Threads) a.bitmap[i] = 0;
-    for (uint32_t b = threadIdx.x; b < a.nblk1; b += kF3Threads) {
-        const uint32_t x = a.tab1[(uint64_t)b * np + p];
-        toff[b] = x & 0xFFFFu;
-        tpk[b] = x >> 16;
-    }
     for (uint32_t i = threadIdx.x; i <= nsub; i += kF3Threads) sofs[i] = 0;
+    if (threadIdx.x == 0) ntie[0] = 0;
     const uint32_t m = a.pcount[p];           // survivors of this partition (F2)
-    sync_lds();
-    const uint32_t mt = scan_lds<kF3Threads>(toff, a.nblk1, wsum);   // (barriers: every thread read m)
-    if (threadIdx.x == 0) a.pcount[p] = 0;    // all-zero again for the next call
+    const uint32_t mt0 = a.tcount[p * kCtrStride];   // targets of this partition (F1)
+    const uint32_t mt = mt0 < a.tcap ? mt0 : a.tcap;
+    const uint2* tsrc = a.tbuf + (uint64_t)p * a.tcap;
+    if (p == 0) {   // spilled targets (foreign, or a full bucket) join the fallback list
+        const uint32_t nsp = a.ctr[kSpill];
+        for (uint32_t j = threadIdx.x; j < nsp; j += kF3Threads) a.fb_list[atomicAdd(a.ctr, 1u)] = a.tspill[j];
+    }
+    sync_lds();   // every thread has read the counts
+    if (threadIdx.x == 0) {   // all-zero again for the next call
+        a.pcount[p] = 0;
+        a.tcount[p * kCtrStride] = 0;
+        if (p == 0) a.ctr[kSpill] = 0;
+    }
     if (mt == 0) return;   // no targets in this partition (block-uniform)
     F3_STAMP(1);
-    if (threadIdx.x == 0) toff[a.nblk1] = mt;
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     constexpr uint32_t NWV = kF3Threads / 64;
-    auto target_at = [&](uint32_t j) -> uint2 {
-        const uint32_t b = run_of(toff, a.nblk1, j);
-        return a.treg[(uint64_t)b * kF1Chunk + tpk[b] + (j - toff[b])];
-    };
     if (a.dbg & 32) return;
     if (m > kF3Cap || m > a.pcap) {
         // strongly clustered ids: this partition's targets take the exact brute-force path
-        for (uint32_t j = threadIdx.x; j < mt; j += kF3Threads) {
-            const uint2 te = target_at(j);
-            a.fb_list[atomicAdd(a.ctr, 1u)] = te.y & ~kForeign;
-        }
+        for (uint32_t j = threadIdx.x; j < mt; j += kF3Threads) a.fb_list[atomicAdd(a.ctr, 1u)] = tsrc[j].y;
         return;
     }
     // first chunk of targets and the partition's survivors: both loads in flight together
-    const uint2 tfirst = threadIdx.x < mt ? target_at(threadIdx.x) : make_uint2(0u, 0u);
+    const uint2 tfirst = tsrc[threadIdx.x < mt ? threadIdx.x : 0];
     const uint32_t smask = nsub - 1u;
     const uint2* src = a.pbuf + (uint64_t)p * a.pcap;
     uint2 e[kF3Per];
     uint32_t rk[kF3Per];
+    const uint32_t nper = (m + kF3Threads - 1) / kF3Threads;   // rounds actually needed (uniform)
+    const uint32_t sq_sh = 32 - a.Lq;                            // sub-prefix = bfe(w, 32 - Lq, Lq - b1)
+    // unconditional loads (a load under a branch gets its own wait): rounds past nper
+    // re-read entry 0 from the cache
 #pragma unroll
     for (uint32_t u = 0; u < kF3Per; ++u) {
         const uint32_t j = u * kF3Threads + threadIdx.x;
@@ -583,7 +619,8 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     // counting sort by sub-prefix: LDS histogram (ranks from the atomics), scan, placement
 #pragma unroll
     for (uint32_t u = 0; u < kF3Per; ++u)
-        if (u * kF3Threads + threadIdx.x < m) rk[u] = atomicAdd(sofs + (top_bits(e[u].x, a.Lq) & smask), 1u);
+        if (u < nper && u * kF3Threads + threadIdx.x < m)
+            rk[u] = atomicAdd(sofs + __builtin_amdgcn_ubfe(e[u].x, sq_sh, a.Lq - a.b1), 1u);
     sync_lds();
     F3_STAMP(2);
     scan_lds<kF3Threads>(sofs, nsub, wsum);
@@ -591,22 +628,28 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     sync_lds();
 #pragma unroll
     for (uint32_t u = 0; u < kF3Per; ++u)
-        if (u * kF3Threads + threadIdx.x < m) S[sofs[top_bits(e[u].x, a.Lq) & smask] + rk[u]] = e[u];
+        if (u < nper && u * kF3Threads + threadIdx.x < m)
+            S[sofs[__builtin_amdgcn_ubfe(e[u].x, sq_sh, a.Lq - a.b1)] + rk[u]] = e[u];
     F3_STAMP(3);
     if (a.dbg & 16) return;
     const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
+    const bool full_row = a.k == (uint32_t)K && want == (uint32_t)K && ((uintptr_t)a.out_idx & 15) == 0;
     for (uint32_t t0i = 0; t0i < mt; t0i += kF3Threads) {
         const uint32_t mtr = mt - t0i < kF3Threads ? mt - t0i : kF3Threads;
-        if (threadIdx.x < mtr) T[threadIdx.x] = t0i ? target_at(t0i + threadIdx.x) : tfirst;
+        if (threadIdx.x < mtr) T[threadIdx.x] = t0i ? tsrc[t0i + threadIdx.x] : tfirst;
         if (threadIdx.x == 0) slow[kF3Threads] = 0;
         sync_lds();
         if (t0i == 0) F3_STAMP(4);
-        // A: one lane per target; targets are dealt round-robin over the waves so that
-        // every SIMD runs a share of the (latency-bound) candidate loops
-        const uint32_t slot = lane * NWV + wv;
-        if (slot < mtr) {
+        // A: G lanes per target (G = 4 / 2 / 1 as the chunk's targets fill the block).  Lane
+        // j of a group scans candidates lo + j, lo + j + G, ... into its own top-K and the
+        // group merges its lists with DPP butterflies (f3_merge).  G = 1 deals the targets
+        // round-robin over the waves so that every SIMD runs a share of the candidate loops.
+        const uint32_t G = a.Lm >= 12 ? (mtr <= kF3Threads / 4 ? 4u : mtr <= kF3Threads / 2 ? 2u : 1u) : 1u;
+        const uint32_t slot = G == 4 ? threadIdx.x >> 2 : G == 2 ? threadIdx.x >> 1 : lane * NWV + wv;
+        const uint32_t gj = threadIdx.x & (G - 1);
+        if (slot < mtr) {   // group-uniform from here on
             const uint2 te = T[slot];
-            const uint32_t t0 = te.x, qi = te.y & ~kForeign;
+            const uint32_t t0 = te.x, qi = te.y;
             // deepest level L in [Lm, Lq] with >= want ids in sub(t, L)
             const uint32_t sq = top_bits(t0, a.Lq) & smask;
             uint32_t lo = 0, hi = 0, L = a.Lq + 1;
@@ -617,14 +660,16 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                 hi = sofs[((sq >> sh_l) + 1) << sh_l];
             } while (hi - lo < want && L > a.Lm);
             const uint32_t mm = hi - lo;
-            if (mm < want || (te.y & kForeign)) {
-                a.fb_list[atomicAdd(a.ctr, 1u)] = qi;
+            if (mm < want) {
+                if (gj == 0) a.fb_list[atomicAdd(a.ctr, 1u)] = qi;
             } else if (mm > kLaneMax || a.Lm == 0) {
-                slow[atomicAdd(slow + kF3Threads, 1u)] = slot;
+                if (gj == 0) {
+                    slow[atomicAdd(slow + kF3Threads, 1u)] = slot;
+                    atomicAdd(a.ctr + 2, 1u);
+                }
             } else {
                 uint32_t dk[K], ok[K];
                 uint32_t rmin = DHT_NONE;   // smallest distance that left (or never entered) the list
-                const uint32_t hi_l = (a.dbg & 512) ? lo + want : hi;
                 if (a.Lm >= 12) {
                     // packed keys (w0 distance << 12 | LDS position): distances are below
                     // 2^(32 - Lm) <= 2^20 and positions below kF3Cap = 2^12, so the key order
@@ -632,16 +677,19 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                     uint32_t key[K];
 #pragma unroll
                     for (int r = 0; r < K; ++r) key[r] = DHT_NONE;
-                    uint32_t lmin = DHT_NONE;
-                    uint32_t nxt = S[lo].x;   // next candidate's word, read one iteration ahead
-                    for (uint32_t o = lo; o < hi_l; ++o) {
+                    uint32_t lmin = DHT_NONE;   // smallest key that left the list
+                    uint32_t o = lo + gj;
+                    uint32_t nxt = S[o < hi ? o : lo].x;   // next candidate's word, read ahead
+                    for (; o < hi; o += G) {
                         const uint32_t c = ((nxt ^ t0) << 12) | o;
-                        nxt = S[o + 1 < hi ? o + 1 : o].x;
-                        lmin = min(lmin, max(c, key[K - 1]));   // the key that leaves the list
+                        nxt = S[o + G < hi ? o + G : o].x;
+                        lmin = min(lmin, max(c, key[K - 1]));
 #pragma unroll
                         for (int r = K - 1; r > 0; --r) key[r] = med3_u32(key[r - 1], key[r], c);
                         key[0] = min(key[0], c);
                     }
+                    if (G >= 2) f3_merge<K, 0xB1>(key, lmin);   // quad_perm [1,0,3,2]: lane ^ 1
+                    if (G == 4) f3_merge<K, 0x4E>(key, lmin);   // quad_perm [2,3,0,1]: lane ^ 2
 #pragma unroll
                     for (int r = 0; r < K; ++r) {
                         dk[r] = key[r] == DHT_NONE ? DHT_NONE : key[r] >> 12;
@@ -652,7 +700,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
 #pragma unroll
                     for (int r = 0; r < K; ++r) { dk[r] = DHT_NONE; ok[r] = DHT_NONE; }
                     uint32_t nxt = S[lo].x;
-                    for (uint32_t o = lo; o < hi_l; ++o) {
+                    for (uint32_t o = lo; o < hi; ++o) {
                         const uint32_t d = nxt ^ t0;   // < 2^(32 - Lm) <= 2^31 < NONE
                         nxt = S[o + 1 < hi ? o + 1 : o].x;
                         const bool ins = d < dk[K - 1];
@@ -675,26 +723,57 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                 bool tie = rmin == dk[want - 1];
 #pragma unroll
                 for (int r = 0; r + 1 < K; ++r) tie = tie || ((uint32_t)r + 1 <= want && dk[r] == dk[r + 1]);
-                if (a.dbg & 1024) {
-                    if (dk[0] == 0x7FFFFFFF) a.out_cnt[qi] = ok[1];
-                } else if (tie) {
-                    slow[atomicAdd(slow + kF3Threads, 1u)] = slot;
-                    atomicAdd(a.ctr + 3, 1u);
-                } else {
+                if (tie) {
+                    // hand the candidates to F4 (one wave per tie, off this block's critical
+                    // path) while a slot is free and they fit a wave; else phase B here
+                    uint32_t tsl = kTieSlots;
+                    if (gj == 0) {
+                        atomicAdd(a.ctr + 2, 1u);
+                        if (mm <= 64) tsl = atomicAdd(ntie, 1u);
+                    }
+                    if (G > 1) tsl = (uint32_t)__shfl((int)tsl, (int)(lane & ~(G - 1)));
+                    if (tsl < kTieSlots) {
+                        const uint32_t g = p * kTieSlots + tsl;
+                        uint2* dst = a.tie_cand + (uint64_t)g * 64;
+                        for (uint32_t o = gj; o < mm; o += G) dst[o] = S[lo + o];
+                        if (gj == 0) a.tie_hdr[g] = make_uint4(qi, t0, mm, 0u);
+                    } else if (gj == 0) {
+                        slow[atomicAdd(slow + kF3Threads, 1u)] = slot;
+                    }
+                } else if (gj == 0) {
                     uint32_t* orow = a.out_idx + (uint64_t)qi * a.k;
+                    // LDS reads first, then (shards) all gidx loads together: one wait before
+                    // the stores instead of one per place
                     uint32_t res[K];
+                    if (full_row) {   // k == K == want, 16-B aligned rows (block-uniform)
 #pragma unroll
-                    for (int r = 0; r < K; ++r) res[r] = (uint32_t)r < want ? map_out(S[ok[r]].y, a.gidx, a.base) : DHT_NONE;
-                    if (a.k == (uint32_t)K && ((uintptr_t)a.out_idx & 15) == 0) {   // whole 16-B aligned row
+                        for (int r = 0; r < K; ++r) res[r] = S[ok[r]].y;
+                        if (a.gidx) {
+#pragma unroll
+                            for (int r = 0; r < K; ++r) res[r] = a.gidx[res[r]];
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < K; ++r) res[r] += a.base;
+                        }
 #pragma unroll
                         for (int r = 0; r < K; r += 4)
                             *reinterpret_cast<uint4*>(orow + r) = make_uint4(res[r], res[r + 1], res[r + 2], res[r + 3]);
+                        a.out_cnt[qi] = want;
                     } else {
 #pragma unroll
+                        for (int r = 0; r < K; ++r) res[r] = (uint32_t)r < want ? S[ok[r] & (kF3Cap - 1)].y : 0u;
+                        if (a.gidx) {
+#pragma unroll
+                            for (int r = 0; r < K; ++r) res[r] = a.gidx[res[r]];
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < K; ++r) res[r] += a.base;
+                        }
+#pragma unroll
                         for (int r = 0; r < K; ++r)
-                            if ((uint32_t)r < a.k) orow[r] = res[r];
+                            if ((uint32_t)r < a.k) orow[r] = (uint32_t)r < want ? res[r] : DHT_NONE;
+                        a.out_cnt[qi] = want;
                     }
-                    a.out_cnt[qi] = want;
                 }
             }
         }
@@ -705,7 +784,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         for (uint32_t i = wv; i < ns; i += NWV) {
             const uint2 te = T[slow[i]];
             const uint32_t t0 = __builtin_amdgcn_readfirstlane(te.x);
-            const uint32_t qi = __builtin_amdgcn_readfirstlane(te.y) & ~kForeign;
+            const uint32_t qi = __builtin_amdgcn_readfirstlane(te.y);
             const uint32_t sh_m = a.Lq - a.Lm;
             const uint32_t sm = (top_bits(t0, a.Lq) & smask) >> sh_m;
             f3_wave_answer(a, S, sofs[sm << sh_m], sofs[(sm + 1) << sh_m], qi, t0, want, lane);
@@ -716,25 +795,34 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     F3_STAMP(7);
 }
 
-// ---- F4: exact brute force for the fallback targets -------------------------------------
-// One workgroup per target: every thread keeps a sorted top-`want` list of its strided
-// share of the ids in LDS (slot-major), then `want` rounds of a block arg-min merge.
-__global__ __launch_bounds__(kF4Threads) void k_f4_fallback(const uint32_t* __restrict__ fb_count,
-                                                           const uint32_t* __restrict__ fb_list,
-                                                           const uint32_t* __restrict__ planes, uint64_t stride,
-                                                           uint64_t n, const uint32_t* __restrict__ tp, uint64_t ts,
-                                                           uint32_t k, const uint32_t* __restrict__ gidx,
-                                                           uint32_t base, uint32_t* __restrict__ out_idx,
-                                                           uint32_t* __restrict__ out_cnt) {
+// ---- F4: deferred ties and the exact brute force for the fallback targets ---------------
+// Blocks [0, nfb): one workgroup per fallback target: every thread keeps a sorted
+// top-`want` list of its strided share of the ids in LDS (slot-major), then `want` rounds
+// of a block arg-min merge.  Blocks [nfb, nfb + np): the ties F3 partition blockIdx - nfb
+// deferred, one wave per slot (f3_wave_answer on the copied candidates); a slot is freed
+// (count 0) once answered, so the headers are all-zero between calls.
+static_assert(kF4Threads / 64 == (int)kTieSlots, "one F4 wave per deferred-tie slot");
+__global__ __launch_bounds__(kF4Threads) void k_f4_fallback(F3Args a, uint32_t nfb) {
     extern __shared__ uint2 lst[];            // [want][kF4Threads], then red[kF4Threads / 64]
-    const uint32_t cntq = *fb_count;
-    const uint32_t want = n < k ? (uint32_t)n : k;
+    const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    if (blockIdx.x >= nfb) {
+        const uint32_t g = (blockIdx.x - nfb) * kTieSlots + wv;
+        const uint4 h = a.tie_hdr[g];
+        if (h.z == 0) return;
+        f3_wave_answer(a, a.tie_cand + (uint64_t)g * 64, 0, h.z, h.x, h.y, want, lane);
+        if (lane == 0) a.tie_hdr[g].z = 0;
+        return;
+    }
+    const uint32_t cntq = a.ctr[0];
+    const uint32_t* __restrict__ planes = a.planes;
+    const uint64_t stride = a.stride, n = a.n;
+    const uint32_t k = a.k;
     uint2* red = lst + (size_t)want * kF4Threads;
-    for (uint32_t f = blockIdx.x; f < cntq; f += gridDim.x) {
-        const uint32_t qi = fb_list[f];
+    for (uint32_t f = blockIdx.x; f < cntq; f += nfb) {
+        const uint32_t qi = a.fb_list[f];
         uint32_t t[DHT_W];
-        load_target(tp, ts, qi, t);
+        load_target(a.tp, a.ts, qi, t);
         uint32_t c = 0, wd = DHT_NONE, wi = DHT_NONE;   // own list length and its worst entry
         for (uint64_t i = threadIdx.x; i < n; i += kF4Threads) {
             const uint32_t d = planes[i] ^ t[0];
@@ -775,16 +863,16 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_fallback(const uint32_t* __re
             }
             __syncthreads();
             if (ptr < c && lst[ptr * kF4Threads + threadIdx.x].y == best.y) ++ptr;   // indices are unique
-            if (threadIdx.x == 0) out_idx[(uint64_t)qi * k + r] = map_out(best.y, gidx, base);
+            if (threadIdx.x == 0) a.out_idx[(uint64_t)qi * k + r] = map_out(best.y, a.gidx, a.base);
         }
-        for (uint32_t r = want + threadIdx.x; r < k; r += kF4Threads) out_idx[(uint64_t)qi * k + r] = DHT_NONE;
-        if (threadIdx.x == 0) out_cnt[qi] = want;
+        for (uint32_t r = want + threadIdx.x; r < k; r += kF4Threads) a.out_idx[(uint64_t)qi * k + r] = DHT_NONE;
+        if (threadIdx.x == 0) a.out_cnt[qi] = want;
         __syncthreads();
     }
 }
 
 struct BatchPlan {
-    uint32_t Lm, b1, Lq, nwords, nblk1, nblk2, stage, sparse;
+    uint32_t Lm, b1, Lq, nwords, nblk1, nblk2, stage, sparse, tcap;
     uint64_t per_blk;
 };
 
@@ -814,7 +902,10 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     P.Lq = P.Lm + 1 < 32 ? P.Lm + 1 : 32;
     while (P.Lq > P.Lm && P.Lq - P.b1 > 12) --P.Lq;
     P.nwords = P.Lm >= 5 ? (1u << (P.Lm - 5)) : 1u;
-    P.nblk1 = (q + kF1Chunk - 1) / kF1Chunk;
+    P.nblk1 = (q + kF1Threads - 1) / kF1Threads;
+    // target buckets: mean + 6 sigma + 64 (uniform targets); overflow spills to F4
+    const double mu = (double)q / (double)(1u << P.b1);
+    P.tcap = ((uint32_t)(mu + 6.0 * std::sqrt(mu) + 64.0) + 63u) & ~63u;
     // F2: one persistent workgroup per CU, ranges in whole chunks
     const uint64_t chunks = (n + kF2Step - 1) / kF2Step;
     const uint64_t g = num_cus > 0 ? (uint64_t)num_cus : 256;
@@ -847,7 +938,7 @@ size_t f2_lds(const BatchPlan& P) {
 
 size_t f3_lds(const BatchPlan& P) {
     const uint32_t nsub = 1u << (P.Lq - P.b1);
-    return (size_t)f3_words(P.nblk1, nsub) * 4 + (size_t)(kF3Cap + kF3Threads) * 8;
+    return (size_t)f3_words(nsub) * 4 + (size_t)(kF3Cap + kF3Threads) * 8;
 }
 
 }  // namespace
@@ -855,21 +946,24 @@ size_t f3_lds(const BatchPlan& P) {
 bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     if (k == 0 || k > DHTGPU_MAX_K_DEV || n >= (1ull << 31)) return false;
     const BatchPlan P = plan_batch(n, q, k, num_cus);
-    if (P.nblk1 > kMaxBlk1) return false;
+    if (q > kMaxQ) return false;
     if (P.Lm - P.b1 > 13 || P.stage < 2 * kF2Sub) return false;
     return f3_lds(P) <= kLdsMax && f2_lds(P) <= kLdsMax;
 }
 
-// workspace: bitmap (64 KB) | ctr[4] | pcount[kMaxParts] -- these three all-zero between
-// calls -- | fb_list[q] | treg[q] | tab1[nblk1][np] | pbuf[np * kF3Cap]
+// workspace: bitmap (64 KB) | ctr[64] | pcount[kMaxParts] | tcount[kMaxParts * kCtrStride] |
+// tie_hdr[kMaxParts * kTieSlots] -- all-zero between calls -- | fb_list[q] | tspill[q] |
+// tbuf[np * tcap] | tie_cand[np * kTieSlots * 64] | pbuf[np * kF3Cap]
 constexpr uint32_t kMaxParts = 1u << 13;
-size_t batch_clean_bytes() { return 65536 + 256 + kMaxParts * 4; }
+size_t batch_clean_bytes() {
+    return 65536 + 256 + (size_t)kMaxParts * 4 + (size_t)kMaxParts * kCtrStride * 4 + (size_t)kMaxParts * kTieSlots * 16;
+}
 
 size_t batch_bytes(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     const BatchPlan P = plan_batch(n, q, k, num_cus);
     const size_t np = 1ull << P.b1;
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    return batch_clean_bytes() + al((size_t)q * 4) + al((size_t)q * 8) + al(np * P.nblk1 * 4) +
+    return batch_clean_bytes() + 2 * al((size_t)q * 4) + al(np * P.tcap * 8) + al(np * kTieSlots * 64 * 8) +
            al(np * kF3Cap * 8);
 }
 
@@ -892,10 +986,13 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
     };
     uint32_t* bitmap = reinterpret_cast<uint32_t*>(take(65536));
     uint32_t* ctr = reinterpret_cast<uint32_t*>(take(256));
-    uint32_t* pcount = reinterpret_cast<uint32_t*>(take(kMaxParts * 4));
+    uint32_t* pcount = reinterpret_cast<uint32_t*>(take((size_t)kMaxParts * 4));
+    uint32_t* tcount = reinterpret_cast<uint32_t*>(take((size_t)kMaxParts * kCtrStride * 4));
+    uint4* tie_hdr = reinterpret_cast<uint4*>(take((size_t)kMaxParts * kTieSlots * 16));
     uint32_t* fb_list = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
-    uint2* treg = reinterpret_cast<uint2*>(take((size_t)q * 8));
-    uint32_t* tab1 = reinterpret_cast<uint32_t*>(take((size_t)np * P.nblk1 * 4));
+    uint32_t* tspill = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
+    uint2* tbuf = reinterpret_cast<uint2*>(take((size_t)np * P.tcap * 8));
+    uint2* tie_cand = reinterpret_cast<uint2*>(take((size_t)np * kTieSlots * 64 * 8));
     uint2* pbuf = reinterpret_cast<uint2*>(take((size_t)np * kF3Cap * 8));
     static bool attr_set = false;
     if (!attr_set) {
@@ -910,8 +1007,8 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
     }
     static const uint32_t dbg = getenv("DHTGPU_DBG") ? (uint32_t)atoi(getenv("DHTGPU_DBG")) : 0u;
     if (ev) (void)hipEventRecord(ev[0], s);
-    k_f1_targets<<<P.nblk1, kF1Threads, (np + 1 + 17) * 4, s>>>(tp, q, P.Lm, P.b1, skip, pval, bitmap, tab1, P.nblk1, treg,
-                                                                ctr);
+    k_f1_targets<<<P.nblk1, kF1Threads, 0, s>>>(tp, q, P.Lm, P.b1, skip, pval, bitmap, tcount, tbuf, P.tcap, ctr,
+                                                tspill);
     if (ev) (void)hipEventRecord(ev[1], s);
     if (n) {
         F2Args a2{planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, kF3Cap, ctr, P.stage, dbg,
@@ -925,37 +1022,53 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
         else k_f2_filter<kF2Dense, false><<<g2, b2, l2, s>>>(a2);
     }
     if (ev) (void)hipEventRecord(ev[2], s);
-    if (dbg & ~(48u | 256u | 512u | 1024u)) {   // experiments: F1 + F2 only
+    if (dbg & ~(48u | 256u)) {   // experiments: F1 + F2 only
         for (int i = 3; ev && i < 5; ++i) (void)hipEventRecord(ev[i], s);
         return hipGetLastError();
     }
     static unsigned long long* stamps = nullptr;
-    if ((dbg & 256) && !stamps) (void)hipMalloc(&stamps, (size_t)8192 * 8 * 8);
-    if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)np * 8 * 8, s);
-    F3Args a{pbuf, pcount, kF3Cap, treg, tab1, P.nblk1, P.Lm, P.b1, P.Lq, bitmap, P.nwords, planes, stride, n,
-             tp, ts, k, gidx, base, out_idx, out_cnt, ctr, fb_list, dbg, stamps};
+    if ((dbg & 256) && !stamps) (void)hipMalloc(&stamps, (size_t)8192 * 16 * 8);
+    if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)np * 16 * 8, s);
+    F3Args a{pbuf, pcount, kF3Cap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, planes, stride, n,
+             tp, ts, k, gidx, base, out_idx, out_cnt, ctr, fb_list, tie_hdr, tie_cand, dbg, stamps};
     if (k <= 8) k_f3_answer<8><<<np, kF3Threads, f3_lds(P), s>>>(a);
     else if (k <= 16) k_f3_answer<16><<<np, kF3Threads, f3_lds(P), s>>>(a);
     else k_f3_answer<32><<<np, kF3Threads, f3_lds(P), s>>>(a);
     if (ev) (void)hipEventRecord(ev[3], s);
-    if (dbg & 256) {   // phase profile of F3 (cycles, averaged over blocks)
-        std::vector<unsigned long long> h((size_t)np * 8);
+    if (dbg & 256) {   // phase profile of F3 (100 MHz real-time stamps: 10 ns ticks)
+        std::vector<unsigned long long> h((size_t)np * 16);
         (void)hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);
-        double acc[8] = {0};
-        unsigned long long t0min = ~0ull, t7max = 0;
-        for (uint32_t b = 0; b < np; ++b) {
-            for (int i = 1; i < 8; ++i) acc[i] += (double)(h[b * 8 + i] - h[b * 8 + i - 1]);
-            t0min = h[b * 8] < t0min ? h[b * 8] : t0min;
-            t7max = h[b * 8 + 7] > t7max ? h[b * 8 + 7] : t7max;
+        unsigned long long t0min = ~0ull;
+        for (uint32_t b = 0; b < np; ++b) t0min = h[b * 16] && h[b * 16] < t0min ? h[b * 16] : t0min;
+        std::vector<uint32_t> live;
+        for (uint32_t b = 0; b < np; ++b)
+            if (h[b * 16 + 7]) live.push_back(b);
+        const size_t nb = live.size();
+        auto pct = [](std::vector<double> d) {
+            std::sort(d.begin(), d.end());
+            const size_t m = d.size();
+            char buf[96];
+            snprintf(buf, sizeof buf, "p10 %.2f p50 %.2f p90 %.2f max %.2f", d[m / 10], d[m / 2], d[m * 9 / 10], d[m - 1]);
+            return std::string(buf);
+        };
+        if (nb) {
+            for (int i = 1; i < 8; ++i) {
+                std::vector<double> d;
+                for (uint32_t b : live) d.push_back((double)(h[b * 16 + i] - h[b * 16 + i - 1]) / 100.0);
+                fprintf(stderr, "  phase %d %s\n", i, pct(d).c_str());
+            }
+            std::vector<double> en, st;
+            for (uint32_t b : live) {
+                en.push_back((double)(h[b * 16 + 7] - t0min) / 100.0);
+                st.push_back((double)(h[b * 16] - t0min) / 100.0);
+            }
+            fprintf(stderr, "  start %s\n  end   %s\n", pct(st).c_str(), pct(en).c_str());
         }
-        fprintf(stderr, "F3 phases (avg cycles/block):");
-        for (int i = 1; i < 8; ++i) fprintf(stderr, " %.0f", acc[i] / np);
-        fprintf(stderr, "  span %llu\n", t7max - t0min);
     }
     const uint32_t want = n < k ? (uint32_t)n : k;
-    k_f4_fallback<<<64, kF4Threads, ((size_t)want * kF4Threads + kF4Threads / 64) * 8, s>>>(
-        ctr, fb_list, planes, stride, n, tp, ts, k, gidx, base, out_idx, out_cnt);
+    constexpr uint32_t kFbBlocks = 64;
+    k_f4_fallback<<<kFbBlocks + np, kF4Threads, ((size_t)want * kF4Threads + kF4Threads / 64) * 8, s>>>(a, kFbBlocks);
     if (ev) (void)hipEventRecord(ev[4], s);
     return hipGetLastError();
 }
