@@ -184,7 +184,10 @@ struct F2Args {
     uint32_t lim;                 // last 16-B aligned word offset loadable inside the plane allocation
     uint32_t skip;                // shard prefix bits (see F1)
     uint32_t sparse;              // 1: no per-sub-step barrier (plan: the stage holds a block's survivors)
+    unsigned long long* stamps;   // dbg & 256: per-block phase timestamps [nblk2][16]
 };
+#define F2_STAMP(i) \
+    do { if ((a.dbg & 256) && threadIdx.x == 0) a.stamps[(uint64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
 // Flush the stage: the entries move to registers, are counting-sorted by partition back
 // into the stage, and every partition's run is then written with consecutive lanes on
@@ -217,6 +220,7 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
         res[i] = c && !(a.dbg & 8) ? atomicAdd(a.pcount + p, c) : 0u;
     }
     if (threadIdx.x == 0) atomicAdd(a.ctr + 1, cnt);
+    F2_STAMP(3);
     scan_lds<kF2Threads>(hist, np, wsum);   // hist = partition starts inside the stage
     if (threadIdx.x == 0) hist[np] = cnt;
 #pragma unroll
@@ -239,6 +243,7 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
         if (p < np) hist[p] = res[i];
     }
     sync_lds();
+    F2_STAMP(4);
     if (!(a.dbg & 2)) {
         for (uint32_t j = threadIdx.x; j < cnt; j += kF2Threads) {
             const uint2 x = stage[j];
@@ -277,6 +282,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     uint2* stage = reinterpret_cast<uint2*>(sh + f2_fixed_words(a.nwords, np));
     const uint64_t lo64 = (uint64_t)blockIdx.x * a.per_blk;
     if (lo64 >= a.n) return;
+    F2_STAMP(0);
     const uint32_t lo = (uint32_t)lo64;
     const uint32_t hi = (uint32_t)(lo64 + a.per_blk < a.n ? lo64 + a.per_blk : a.n);
     const uint32_t lane = lane_id();
@@ -285,8 +291,9 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     const uint32_t pre_off = 32 - a.skip - a.Lm;
     const uint32_t lm5 = a.Lm > 5 ? a.Lm - 5 : 0u;   // word index width
     const uint32_t tid4 = 4 * threadIdx.x;
-    // the prefix bitmap first (its loads would otherwise wait behind the id ring); indices
-    // past the end are clamped, so a clamped lane rewrites a word with its own value
+    // the prefix bitmap first (ahead of the ring, its loads land first: measured 1 µs better
+    // per block than ring-first); indices past the end are clamped, so a clamped lane
+    // rewrites a word with its own value
     if ((a.nwords & 3) == 0) {
         for (uint32_t i0 = 0; i0 < a.nwords; i0 += kF2Threads * 16) {
             uint4 t[4];
@@ -311,6 +318,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     for (uint32_t r = 0; r < kRing; ++r) ring[r] = f2_load1(a.w0, lo + r * kF2Sub, lim);
     if (threadIdx.x < 3) misc[threadIdx.x] = 0;
     sync_lds();
+    F2_STAMP(1);
     // Dense mode: stage fill `cnt` is block-uniform.  Sub-step s reserves slots with one
     // LDS atomic per wave on counter misc[s % 3]; after the sub-step's barrier every wave
     // adds that counter to cnt.  The counter of sub-step s + 1 is zeroed during sub-step s
@@ -401,7 +409,9 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
         sync_lds();
         cnt = misc[0] < a.stage ? misc[0] : a.stage;
     }
+    F2_STAMP(2);
     if (cnt) f2_flush(a, cnt, stage, hist, wsum);
+    F2_STAMP(5);
 }
 
 // ---- candidate order ------------------------------------------------------------------
@@ -1006,13 +1016,17 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
         attr_set = true;
     }
     static const uint32_t dbg = getenv("DHTGPU_DBG") ? (uint32_t)atoi(getenv("DHTGPU_DBG")) : 0u;
+    static unsigned long long* stamps = nullptr;   // dbg & 256: F3 [8192][16] then F2 [8192][16]
+    if ((dbg & 256) && !stamps) (void)hipMalloc(&stamps, (size_t)2 * 8192 * 16 * 8);
+    if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)2 * 8192 * 16 * 8, s);
     if (ev) (void)hipEventRecord(ev[0], s);
     k_f1_targets<<<P.nblk1, kF1Threads, 0, s>>>(tp, q, P.Lm, P.b1, skip, pval, bitmap, tcount, tbuf, P.tcap, ctr,
                                                 tspill);
     if (ev) (void)hipEventRecord(ev[1], s);
     if (n) {
         F2Args a2{planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, kF3Cap, ctr, P.stage, dbg,
-                  (uint32_t)(5 * stride - 4 < 0xFFFFFFF0ull ? 5 * stride - 4 : 0xFFFFFFF0ull), skip, P.sparse};
+                  (uint32_t)(5 * stride - 4 < 0xFFFFFFF0ull ? 5 * stride - 4 : 0xFFFFFFF0ull), skip, P.sparse,
+                  stamps ? stamps + 8192 * 16 : nullptr};
         const dim3 g2(P.nblk2), b2(kF2Threads);
         const size_t l2 = f2_lds(P);
         if (dbg & 64) k_f2_filter<kF2Stream, false><<<g2, b2, l2, s>>>(a2);
@@ -1026,15 +1040,37 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
         for (int i = 3; ev && i < 5; ++i) (void)hipEventRecord(ev[i], s);
         return hipGetLastError();
     }
-    static unsigned long long* stamps = nullptr;
-    if ((dbg & 256) && !stamps) (void)hipMalloc(&stamps, (size_t)8192 * 16 * 8);
-    if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)np * 16 * 8, s);
     F3Args a{pbuf, pcount, kF3Cap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, planes, stride, n,
              tp, ts, k, gidx, base, out_idx, out_cnt, ctr, fb_list, tie_hdr, tie_cand, dbg, stamps};
     if (k <= 8) k_f3_answer<8><<<np, kF3Threads, f3_lds(P), s>>>(a);
     else if (k <= 16) k_f3_answer<16><<<np, kF3Threads, f3_lds(P), s>>>(a);
     else k_f3_answer<32><<<np, kF3Threads, f3_lds(P), s>>>(a);
     if (ev) (void)hipEventRecord(ev[3], s);
+    if (dbg & 256) {   // phase profile of F2 (100 MHz real-time stamps: 10 ns ticks)
+        std::vector<unsigned long long> h((size_t)P.nblk2 * 16);
+        (void)hipMemcpyAsync(h.data(), stamps + 8192 * 16, h.size() * 8, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        unsigned long long t0 = ~0ull;
+        for (uint32_t b = 0; b < P.nblk2; ++b) t0 = h[b * 16] && h[b * 16] < t0 ? h[b * 16] : t0;
+        auto pct2 = [](std::vector<double> d) {
+            std::sort(d.begin(), d.end());
+            const size_t m = d.size();
+            char buf[96];
+            snprintf(buf, sizeof buf, "p10 %.2f p50 %.2f p90 %.2f max %.2f", d[m / 10], d[m / 2], d[m * 9 / 10], d[m - 1]);
+            return std::string(buf);
+        };
+        const char* nm[] = {"", "bitmap+ring", "stream+filter", "flush hist", "flush reserve+scan", "flush writes"};
+        for (int i = 1; i <= 5; ++i) {
+            std::vector<double> d;
+            for (uint32_t b = 0; b < P.nblk2; ++b)
+                if (h[b * 16 + 5]) d.push_back((double)(h[b * 16 + i] - h[b * 16 + i - 1]) / 100.0);
+            if (!d.empty()) fprintf(stderr, "  F2 %-20s %s\n", nm[i], pct2(d).c_str());
+        }
+        std::vector<double> st, en;
+        for (uint32_t b = 0; b < P.nblk2; ++b)
+            if (h[b * 16 + 5]) { st.push_back((double)(h[b * 16] - t0) / 100.0); en.push_back((double)(h[b * 16 + 5] - t0) / 100.0); }
+        if (!st.empty()) fprintf(stderr, "  F2 start %s\n  F2 end   %s\n", pct2(st).c_str(), pct2(en).c_str());
+    }
     if (dbg & 256) {   // phase profile of F3 (100 MHz real-time stamps: 10 ns ticks)
         std::vector<unsigned long long> h((size_t)np * 16);
         (void)hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, s);
