@@ -51,7 +51,7 @@ constexpr int kF4Threads = 256;
 constexpr uint32_t kMaxLm = 19;                      // 2^19-bit bitmap = 64 KB of LDS in F2
 constexpr uint32_t kMaxSubBits = 11;                 // F3 sub-prefix histogram <= 2048 bins
 constexpr uint32_t kMaxQ = 1u << 22;                 // targets per call
-constexpr uint32_t kTieSlots = 4;                    // deferred-tie slots per F3 partition (F4 waves)
+constexpr uint32_t kTieSlots = 8;                    // deferred-tie slots per F3 partition
 // F1's per-target bucket counters tcount[p] sit 256 B apart: their returning atomics execute
 // at the memory side, one request per lane (random partitions), and counters packed into one
 // 4 KB run would all queue on the same channel.  F2's pcount stays packed: its flush reserves
@@ -480,31 +480,45 @@ __device__ __forceinline__ bool key2_less(uint32_t da, uint32_t a1, uint32_t ia,
     return id_less(da, ia, db, ib, planes, stride, t);
 }
 
+// exact answer for one target from <= 64 candidates, one per lane (lane < mm): its rank is
+// the number of candidates strictly closer by (w0, w1) distance (full key on a double tie).
+// Word 1 and the target are loaded unconditionally (clamped), in one round trip.
+__device__ void wave_rank_answer(const F3Args& a, uint2 me, uint32_t mm, uint32_t qi, uint32_t t0, uint32_t want,
+                                 uint32_t lane) {
+    const bool act = lane < mm;
+    const uint32_t w1 = a.planes[a.stride + (act ? me.y : 0u)];
+    uint32_t t[DHT_W];
+    load_target(a.tp, a.ts, qi, t);
+    const uint32_t md = me.x ^ t0;
+    const uint32_t m1 = act ? w1 ^ t[1] : DHT_NONE;
+    uint32_t rank = 0;
+    for (uint32_t o = 0; o < mm; ++o) {
+        const uint32_t xd = __builtin_amdgcn_readlane((int)md, (int)o);
+        const uint32_t x1 = __builtin_amdgcn_readlane((int)m1, (int)o);
+        const uint32_t xi = __builtin_amdgcn_readlane((int)me.y, (int)o);
+        if (xd < md || (xd == md && x1 < m1)) ++rank;
+        else if (xd == md && x1 == m1 && act && o != lane && id_less(xd, xi, md, me.y, a.planes, a.stride, t)) ++rank;
+    }
+    uint32_t* orow = a.out_idx + (uint64_t)qi * a.k;
+    if (act && rank < want) orow[rank] = map_out(me.y, a.gidx, a.base);
+    if (lane >= want && lane < a.k) orow[lane] = DHT_NONE;
+    if (lane == 0) a.out_cnt[qi] = want;
+}
+
 // exact wave-cooperative answer for one target (ties on w0, large subtrees).  Every lane
 // gathers word 1 of its candidate up front (one round trip for the whole wave), so the
 // ordering loops below compare (w0, w1) distances in registers.
 __device__ void f3_wave_answer(const F3Args& a, const uint2* S, uint32_t lo, uint32_t hi, uint32_t qi,
                                uint32_t t0, uint32_t want, uint32_t lane) {
+    const uint32_t mm = hi - lo;
+    if (mm <= 64) {
+        wave_rank_answer(a, S[lo + (lane < mm ? lane : 0u)], mm, qi, t0, want, lane);
+        return;
+    }
     uint32_t t[DHT_W];
     load_target(a.tp, a.ts, qi, t);
     uint32_t* orow = a.out_idx + (uint64_t)qi * a.k;
-    const uint32_t mm = hi - lo;
-    if (mm <= 64) {
-        const bool act = lane < mm;
-        const uint2 me = act ? S[lo + lane] : make_uint2(0u, 0u);
-        const uint32_t md = me.x ^ t0;
-        const uint32_t m1 = act ? a.planes[a.stride + me.y] ^ t[1] : DHT_NONE;
-        // rank = candidates strictly closer
-        uint32_t rank = 0;
-        for (uint32_t o = 0; o < mm; ++o) {
-            const uint32_t xd = __builtin_amdgcn_readlane((int)md, (int)o);
-            const uint32_t x1 = __builtin_amdgcn_readlane((int)m1, (int)o);
-            const uint32_t xi = __builtin_amdgcn_readlane((int)me.y, (int)o);
-            if (xd < md || (xd == md && x1 < m1)) ++rank;
-            else if (xd == md && x1 == m1 && act && o != lane && id_less(xd, xi, md, me.y, a.planes, a.stride, t)) ++rank;
-        }
-        if (act && rank < want) orow[rank] = map_out(me.y, a.gidx, a.base);
-    } else {
+    {
         // running lane-distributed top-`want` list of (w0 distance, w1 distance, index)
         uint32_t ed = DHT_NONE, e1 = DHT_NONE, ei = DHT_NONE, cnt = 0;
         for (uint32_t c = lo; c < hi; c += 64) {
@@ -809,18 +823,20 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
 // Blocks [0, nfb): one workgroup per fallback target: every thread keeps a sorted
 // top-`want` list of its strided share of the ids in LDS (slot-major), then `want` rounds
 // of a block arg-min merge.  Blocks [nfb, nfb + np): the ties F3 partition blockIdx - nfb
-// deferred, one wave per slot (f3_wave_answer on the copied candidates); a slot is freed
+// deferred, a wave per slot (f3_wave_answer on the copied candidates); a slot is freed
 // (count 0) once answered, so the headers are all-zero between calls.
-static_assert(kF4Threads / 64 == (int)kTieSlots, "one F4 wave per deferred-tie slot");
+static_assert(kTieSlots % (kF4Threads / 64) == 0, "F4 waves split a partition's tie slots evenly");
 __global__ __launch_bounds__(kF4Threads) void k_f4_fallback(F3Args a, uint32_t nfb) {
     extern __shared__ uint2 lst[];            // [want][kF4Threads], then red[kF4Threads / 64]
     const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-    if (blockIdx.x >= nfb) {
-        const uint32_t g = (blockIdx.x - nfb) * kTieSlots + wv;
+    if (blockIdx.x >= nfb) {   // one slot per wave; header and candidates in one round trip
+        const uint32_t g = (blockIdx.x - nfb) * (kF4Threads / 64) + wv;
         const uint4 h = a.tie_hdr[g];
-        if (h.z == 0) return;
-        f3_wave_answer(a, a.tie_cand + (uint64_t)g * 64, 0, h.z, h.x, h.y, want, lane);
+        const uint2 c = a.tie_cand[(uint64_t)g * 64 + lane];
+        const uint32_t mm = __builtin_amdgcn_readfirstlane(h.z);
+        if (mm == 0) return;
+        wave_rank_answer(a, c, mm, __builtin_amdgcn_readfirstlane(h.x), __builtin_amdgcn_readfirstlane(h.y), want, lane);
         if (lane == 0) a.tie_hdr[g].z = 0;
         return;
     }
@@ -1104,7 +1120,7 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
     }
     const uint32_t want = n < k ? (uint32_t)n : k;
     constexpr uint32_t kFbBlocks = 64;
-    k_f4_fallback<<<kFbBlocks + np, kF4Threads, ((size_t)want * kF4Threads + kF4Threads / 64) * 8, s>>>(a, kFbBlocks);
+    k_f4_fallback<<<kFbBlocks + np * (kTieSlots / (kF4Threads / 64)), kF4Threads, ((size_t)want * kF4Threads + kF4Threads / 64) * 8, s>>>(a, kFbBlocks);
     if (ev) (void)hipEventRecord(ev[4], s);
     return hipGetLastError();
 }
