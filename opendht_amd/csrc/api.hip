@@ -496,12 +496,12 @@ int dhtgpu_batch_topk_timed(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint
     if (!c->has_ids) return DHTGPU_ENOIDS;
     DHT_TRY(c->bind());
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    hipEvent_t ev[5];
-    for (int i = 0; i < 5; ++i) DHT_TRY(hipEventCreate(&ev[i]));
+    hipEvent_t ev[8];   // start/stop per kernel, recorded by the kernels' dispatches
+    for (int i = 0; i < 8; ++i) DHT_TRY(hipEventCreate(&ev[i]));
     int r = batch_run(c, tp, ts, q, k, out_idx, out_cnt, nullptr, 0, s, ev);
-    hipError_t e = r ? hipSuccess : hipEventSynchronize(ev[4]);
-    for (int i = 0; !r && e == hipSuccess && i < 4; ++i) e = hipEventElapsedTime(&ms4[i], ev[i], ev[i + 1]);
-    for (int i = 0; i < 5; ++i) (void)hipEventDestroy(ev[i]);
+    hipError_t e = r ? hipSuccess : hipEventSynchronize(ev[7]);
+    for (int i = 0; !r && e == hipSuccess && i < 4; ++i) e = hipEventElapsedTime(&ms4[i], ev[2 * i], ev[2 * i + 1]);
+    for (int i = 0; i < 8; ++i) (void)hipEventDestroy(ev[i]);
     if (r) return r;
     DHT_TRY(e);
     if (stats4) {

@@ -31,6 +31,7 @@
 // and re-read as {w0, idx}) + q * k * 4 (results).  On uniform ids the survivor fraction
 // is 1 - exp(-q / 2^Lm) (12 % at the cfg-2 batch).
 #include "dhtgpu_dev.h"
+#include <hip/hip_ext.h>
 #include "dhtgpu_internal.h"
 
 #include <algorithm>
@@ -803,6 +804,10 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         }
         sync_lds();
         if (t0i == 0) F3_STAMP(5);
+        if ((a.dbg & 256) && threadIdx.x == 0 && t0i == 0) {
+            a.stamps[(uint64_t)blockIdx.x * 16 + 13] = mt;
+            a.stamps[(uint64_t)blockIdx.x * 16 + 14] = ntie[0];
+        }
         // B: one wave per target for ties and large subtrees (the level-Lm subtree range)
         const uint32_t ns = slow[kF3Threads];
         for (uint32_t i = wv; i < ns; i += NWV) {
@@ -1032,36 +1037,41 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
         attr_set = true;
     }
     static const uint32_t dbg = getenv("DHTGPU_DBG") ? (uint32_t)atoi(getenv("DHTGPU_DBG")) : 0u;
+    // ev (diagnostics): 8 events, a start/stop pair per kernel recorded by the kernel's own
+    // dispatch (hipExtLaunchKernel), so the pairs time the kernels themselves
+    auto go = [&](int i, auto kern, dim3 g, dim3 b, size_t lds, auto... args) {
+        if (ev) hipExtLaunchKernelGGL(kern, g, b, (uint32_t)lds, s, ev[2 * i], ev[2 * i + 1], 0, args...);
+        else kern<<<g, b, lds, s>>>(args...);
+    };
     static unsigned long long* stamps = nullptr;   // dbg & 256: F3 [8192][16] then F2 [8192][16]
     if ((dbg & 256) && !stamps) (void)hipMalloc(&stamps, (size_t)2 * 8192 * 16 * 8);
     if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)2 * 8192 * 16 * 8, s);
-    if (ev) (void)hipEventRecord(ev[0], s);
-    k_f1_targets<<<P.nblk1, kF1Threads, 0, s>>>(tp, q, P.Lm, P.b1, skip, pval, bitmap, tcount, tbuf, P.tcap, ctr,
-                                                tspill);
-    if (ev) (void)hipEventRecord(ev[1], s);
+    go(0, k_f1_targets, dim3(P.nblk1), dim3(kF1Threads), 0, tp, q, P.Lm, P.b1, skip, pval, bitmap, tcount, tbuf, P.tcap, ctr,
+       tspill);
     if (n) {
         F2Args a2{planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, kF3Cap, ctr, P.stage, dbg,
                   (uint32_t)(5 * stride - 4 < 0xFFFFFFF0ull ? 5 * stride - 4 : 0xFFFFFFF0ull), skip, P.sparse,
                   stamps ? stamps + 8192 * 16 : nullptr};
         const dim3 g2(P.nblk2), b2(kF2Threads);
         const size_t l2 = f2_lds(P);
-        if (dbg & 64) k_f2_filter<kF2Stream, false><<<g2, b2, l2, s>>>(a2);
-        else if (skip + P.Lm > 32 && P.sparse) k_f2_filter<kF2Sparse, true><<<g2, b2, l2, s>>>(a2);
-        else if (skip + P.Lm > 32) k_f2_filter<kF2Dense, true><<<g2, b2, l2, s>>>(a2);
-        else if (P.sparse) k_f2_filter<kF2Sparse, false><<<g2, b2, l2, s>>>(a2);
-        else k_f2_filter<kF2Dense, false><<<g2, b2, l2, s>>>(a2);
+        if (dbg & 64) go(1, k_f2_filter<kF2Stream, false>, g2, b2, l2, a2);
+        else if (skip + P.Lm > 32 && P.sparse) go(1, k_f2_filter<kF2Sparse, true>, g2, b2, l2, a2);
+        else if (skip + P.Lm > 32) go(1, k_f2_filter<kF2Dense, true>, g2, b2, l2, a2);
+        else if (P.sparse) go(1, k_f2_filter<kF2Sparse, false>, g2, b2, l2, a2);
+        else go(1, k_f2_filter<kF2Dense, false>, g2, b2, l2, a2);
+    } else if (ev) {
+        (void)hipEventRecord(ev[2], s);
+        (void)hipEventRecord(ev[3], s);
     }
-    if (ev) (void)hipEventRecord(ev[2], s);
     if (dbg & ~(48u | 256u)) {   // experiments: F1 + F2 only
-        for (int i = 3; ev && i < 5; ++i) (void)hipEventRecord(ev[i], s);
+        for (int i = 4; ev && i < 8; ++i) (void)hipEventRecord(ev[i], s);
         return hipGetLastError();
     }
     F3Args a{pbuf, pcount, kF3Cap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, planes, stride, n,
              tp, ts, k, gidx, base, out_idx, out_cnt, ctr, fb_list, tie_hdr, tie_cand, dbg, stamps};
-    if (k <= 8) k_f3_answer<8><<<np, kF3Threads, f3_lds(P), s>>>(a);
-    else if (k <= 16) k_f3_answer<16><<<np, kF3Threads, f3_lds(P), s>>>(a);
-    else k_f3_answer<32><<<np, kF3Threads, f3_lds(P), s>>>(a);
-    if (ev) (void)hipEventRecord(ev[3], s);
+    if (k <= 8) go(2, k_f3_answer<8>, dim3(np), dim3(kF3Threads), f3_lds(P), a);
+    else if (k <= 16) go(2, k_f3_answer<16>, dim3(np), dim3(kF3Threads), f3_lds(P), a);
+    else go(2, k_f3_answer<32>, dim3(np), dim3(kF3Threads), f3_lds(P), a);
     if (dbg & 256) {   // phase profile of F2 (100 MHz real-time stamps: 10 ns ticks)
         std::vector<unsigned long long> h((size_t)P.nblk2 * 16);
         (void)hipMemcpyAsync(h.data(), stamps + 8192 * 16, h.size() * 8, hipMemcpyDeviceToHost, s);
@@ -1110,6 +1120,16 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
                 for (uint32_t b : live) d.push_back((double)(h[b * 16 + i] - h[b * 16 + i - 1]) / 100.0);
                 fprintf(stderr, "  phase %d %s\n", i, pct(d).c_str());
             }
+            {   // phase A split by group size (G = 4 for <= 64 targets) and by deferred ties
+                std::vector<double> d[2][2];
+                for (uint32_t b : live)
+                    d[h[b * 16 + 13] > 64][h[b * 16 + 14] > 0].push_back((double)(h[b * 16 + 5] - h[b * 16 + 4]) / 100.0);
+                for (int g = 0; g < 2; ++g)
+                    for (int t = 0; t < 2; ++t)
+                        if (!d[g][t].empty())
+                            fprintf(stderr, "  phase A %s %s (%zu blocks): %s\n", g ? "G<=2" : "G=4 ", t ? "ties" : "none",
+                                    d[g][t].size(), pct(d[g][t]).c_str());
+            }
             std::vector<double> en, st;
             for (uint32_t b : live) {
                 en.push_back((double)(h[b * 16 + 7] - t0min) / 100.0);
@@ -1120,8 +1140,8 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
     }
     const uint32_t want = n < k ? (uint32_t)n : k;
     constexpr uint32_t kFbBlocks = 64;
-    k_f4_fallback<<<kFbBlocks + np * (kTieSlots / (kF4Threads / 64)), kF4Threads, ((size_t)want * kF4Threads + kF4Threads / 64) * 8, s>>>(a, kFbBlocks);
-    if (ev) (void)hipEventRecord(ev[4], s);
+    go(3, k_f4_fallback, dim3(kFbBlocks + np * (kTieSlots / (kF4Threads / 64))), dim3(kF4Threads),
+       ((size_t)want * kF4Threads + kF4Threads / 64) * 8, a, kFbBlocks);
     return hipGetLastError();
 }
 
