@@ -505,8 +505,7 @@ int dhtgpu_batch_topk_timed(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint
     if (r) return r;
     DHT_TRY(e);
     if (stats4) {
-        DHT_TRY(hipMemcpyAsync(stats4, batch_stats(c->batch.p), 16, hipMemcpyDeviceToHost, s));
-        DHT_TRY(hipStreamSynchronize(s));
+        DHT_TRY(batch_read_stats(c->batch.p, c->n, q, k, c->num_cus, stats4, s));
     }
     return DHTGPU_OK;
 }

@@ -179,7 +179,7 @@ struct F2Args {
     uint32_t* pcount;             // [np] survivors per partition (all-zero between calls)
     uint2* pbuf;                  // [np][pcap] survivors, partition-major
     uint32_t pcap;
-    uint32_t* ctr;                // ctr[1] = survivor total
+    uint32_t* ctr;                // shared counters (F2 writes none; the survivor total is sum(pcount))
     uint32_t stage;               // LDS stage capacity (entries, <= kStage)
     uint32_t dbg;                 // experiment switches (0 in production)
     uint32_t lim;                 // last 16-B aligned word offset loadable inside the plane allocation
@@ -220,7 +220,6 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
         const uint32_t c = p < np ? hist[p] : 0u;
         res[i] = c && !(a.dbg & 8) ? atomicAdd(a.pcount + p, c) : 0u;
     }
-    if (threadIdx.x == 0) atomicAdd(a.ctr + 1, cnt);
     F2_STAMP(3);
     scan_lds<kF2Threads>(hist, np, wsum);   // hist = partition starts inside the stage
     if (threadIdx.x == 0) hist[np] = cnt;
@@ -301,7 +300,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
             uint32_t ic[4];
 #pragma unroll
             for (uint32_t r = 0; r < 4; ++r) {
-                const uint32_t i = i0 + (r * kF2Threads + threadIdx.x) * 4;
+                uint32_t i = i0 + (r * kF2Threads + threadIdx.x) * 4;
+                if (a.dbg & 512) i = (i + (blockIdx.x & 31) * 512) & (a.nwords - 1);   // experiment: rotated start
                 ic[r] = i < a.nwords ? i : a.nwords - 4;
                 t[r] = *reinterpret_cast<const uint4*>(a.bitmap + ic[r]);
             }
@@ -390,7 +390,6 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                             } else {
                                 const uint32_t p = top_bits(e.x, a.b1);
                                 const uint32_t slot = atomicAdd(a.pcount + p, 1u);
-                                atomicAdd(a.ctr + 1, 1u);
                                 if (slot < a.pcap) a.pbuf[(uint64_t)p * a.pcap + slot] = e;
                             }
                         }
@@ -453,7 +452,7 @@ __device__ __forceinline__ void load_target(const uint32_t* __restrict__ tp, uin
 constexpr uint32_t kLaneMax = 256;   // largest subtree a lane scans alone
 
 __host__ __device__ inline uint32_t f3_words(uint32_t nsub) {
-    return (nsub + 1 + 17 + kF3Threads + 1 + 1 + 1) & ~1u;
+    return (nsub + 1 + 17 + kF3Threads + 1 + 2 + 1) & ~1u;
 }
 
 struct F3Args {
@@ -467,6 +466,7 @@ struct F3Args {
     const uint32_t* gidx; uint32_t base;
     uint32_t* out_idx; uint32_t* out_cnt;
     uint32_t* ctr; uint32_t* fb_list;   // ctr[0] = fallback targets
+    uint32_t* pstat;                     // [np] survivors per partition (statistics; plain stores)
     uint4* tie_hdr;                      // [np][kTieSlots] deferred ties {qi, t0, count, 0} (count 0 = free)
     uint2* tie_cand;                     // [np][kTieSlots][64] their candidates {w0, idx}
     uint32_t dbg;
@@ -582,26 +582,29 @@ __device__ __forceinline__ void f3_merge(uint32_t (&key)[K], uint32_t& lmin) {
 }
 
 #define F3_STAMP(i) \
-    do { if ((a.dbg & 256) && threadIdx.x == 0) a.stamps[(uint64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    do { if (Diag && (a.dbg & 256) && threadIdx.x == 0) a.stamps[(uint64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
-template <int K>
+// Diag: the DHTGPU_DBG build (phase stamps and ablation exits); production launches Diag = false.
+// Exact: k == K and n >= k, so want == K is a compile-time constant (no per-place masks).
+template <int K, bool Diag, bool Exact>
 __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     extern __shared__ uint32_t sh[];
     const uint32_t p = blockIdx.x, np = gridDim.x;
     F3_STAMP(0);
+    if (Diag && (a.dbg & 1024)) __builtin_amdgcn_s_setprio(3);   // experiment: loads/sort first
     // survivors are sorted by their prefix bits [b1, Lq); a target answers from the deepest
     // level L in [Lm, Lq] whose subtree sub(t, L) holds >= want ids (a contiguous range)
     const uint32_t nsub = 1u << (a.Lq - a.b1);
     uint32_t* sofs = sh;                      // [nsub + 1]
     uint32_t* wsum = sofs + nsub + 1;         // [17]
     uint32_t* slow = wsum + 17;               // [kF3Threads + 1] slow-path target slots, count last
-    uint32_t* ntie = slow + kF3Threads + 1;   // [1] deferred-tie slots taken
+    uint32_t* ntie = slow + kF3Threads + 1;   // [0] deferred-tie slots taken, [1] wave-path targets (stat)
     uint2* S = reinterpret_cast<uint2*>(sh + f3_words(nsub));
     uint2* T = S + kF3Cap;
     // the bitmap is no longer read in this call: clear this block's share of it
     for (uint32_t i = p + np * threadIdx.x; i < a.nwords; i += np * kF3Threads) a.bitmap[i] = 0;
     for (uint32_t i = threadIdx.x; i <= nsub; i += kF3Threads) sofs[i] = 0;
-    if (threadIdx.x == 0) ntie[0] = 0;
+    if (threadIdx.x == 0) ntie[0] = ntie[1] = 0;
     const uint32_t m = a.pcount[p];           // survivors of this partition (F2)
     const uint32_t mt0 = a.tcount[p * kCtrStride];   // targets of this partition (F1)
     const uint32_t mt = mt0 < a.tcap ? mt0 : a.tcap;
@@ -612,6 +615,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     }
     sync_lds();   // every thread has read the counts
     if (threadIdx.x == 0) {   // all-zero again for the next call
+        a.pstat[p] = m;
         a.pcount[p] = 0;
         a.tcount[p * kCtrStride] = 0;
         if (p == 0) a.ctr[kSpill] = 0;
@@ -620,7 +624,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     F3_STAMP(1);
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     constexpr uint32_t NWV = kF3Threads / 64;
-    if (a.dbg & 32) return;
+    if (Diag && (a.dbg & 32)) return;
     if (m > kF3Cap || m > a.pcap) {
         // strongly clustered ids: this partition's targets take the exact brute-force path
         for (uint32_t j = threadIdx.x; j < mt; j += kF3Threads) a.fb_list[atomicAdd(a.ctr, 1u)] = tsrc[j].y;
@@ -642,10 +646,13 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         e[u] = src[j < m ? j : 0];
     }
     // counting sort by sub-prefix: LDS histogram (ranks from the atomics), scan, placement
+    // rk[u] = NONE marks an empty slot (the scatter tests the value: no exec masks kept live)
 #pragma unroll
-    for (uint32_t u = 0; u < kF3Per; ++u)
+    for (uint32_t u = 0; u < kF3Per; ++u) {
+        rk[u] = DHT_NONE;
         if (u < nper && u * kF3Threads + threadIdx.x < m)
             rk[u] = atomicAdd(sofs + __builtin_amdgcn_ubfe(e[u].x, sq_sh, a.Lq - a.b1), 1u);
+    }
     sync_lds();
     F3_STAMP(2);
     scan_lds<kF3Threads>(sofs, nsub, wsum);
@@ -653,18 +660,18 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     sync_lds();
 #pragma unroll
     for (uint32_t u = 0; u < kF3Per; ++u)
-        if (u < nper && u * kF3Threads + threadIdx.x < m)
-            S[sofs[__builtin_amdgcn_ubfe(e[u].x, sq_sh, a.Lq - a.b1)] + rk[u]] = e[u];
+        if (rk[u] != DHT_NONE) S[sofs[__builtin_amdgcn_ubfe(e[u].x, sq_sh, a.Lq - a.b1)] + rk[u]] = e[u];
     F3_STAMP(3);
-    if (a.dbg & 16) return;
-    const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
-    const bool full_row = a.k == (uint32_t)K && want == (uint32_t)K && ((uintptr_t)a.out_idx & 15) == 0;
+    if (Diag && (a.dbg & 16)) return;
+    const uint32_t want = Exact ? (uint32_t)K : (a.n < a.k ? (uint32_t)a.n : a.k);
+    const bool full_row = Exact && ((uintptr_t)a.out_idx & 15) == 0;
     for (uint32_t t0i = 0; t0i < mt; t0i += kF3Threads) {
         const uint32_t mtr = mt - t0i < kF3Threads ? mt - t0i : kF3Threads;
         if (threadIdx.x < mtr) T[threadIdx.x] = t0i ? tsrc[t0i + threadIdx.x] : tfirst;
         if (threadIdx.x == 0) slow[kF3Threads] = 0;
         sync_lds();
         if (t0i == 0) F3_STAMP(4);
+        if (Diag && (a.dbg & 1024)) __builtin_amdgcn_s_setprio(0);
         // A: G lanes per target (G = 4 / 2 / 1 as the chunk's targets fill the block).  Lane
         // j of a group scans candidates lo + j, lo + j + G, ... into its own top-K and the
         // group merges its lists with DPP butterflies (f3_merge).  G = 1 deals the targets
@@ -685,12 +692,13 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                 hi = sofs[((sq >> sh_l) + 1) << sh_l];
             } while (hi - lo < want && L > a.Lm);
             const uint32_t mm = hi - lo;
+            if (t0i == 0) F3_STAMP(8);
             if (mm < want) {
                 if (gj == 0) a.fb_list[atomicAdd(a.ctr, 1u)] = qi;
             } else if (mm > kLaneMax || a.Lm == 0) {
                 if (gj == 0) {
                     slow[atomicAdd(slow + kF3Threads, 1u)] = slot;
-                    atomicAdd(a.ctr + 2, 1u);
+                    atomicAdd(ntie + 1, 1u);
                 }
             } else {
                 uint32_t dk[K], ok[K];
@@ -707,12 +715,13 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                     uint32_t nxt = S[o < hi ? o : lo].x;   // next candidate's word, read ahead
                     for (; o < hi; o += G) {
                         const uint32_t c = ((nxt ^ t0) << 12) | o;
-                        nxt = S[o + G < hi ? o + G : o].x;
+                        nxt = (Diag && (a.dbg & 2048)) ? nxt * 2654435761u + o : S[o + G < hi ? o + G : o].x;   // 2048: no LDS (timing only)
                         lmin = min(lmin, max(c, key[K - 1]));
 #pragma unroll
                         for (int r = K - 1; r > 0; --r) key[r] = med3_u32(key[r - 1], key[r], c);
                         key[0] = min(key[0], c);
                     }
+                    if (t0i == 0) F3_STAMP(9);
                     if (G >= 2) f3_merge<K, 0xB1>(key, lmin);   // quad_perm [1,0,3,2]: lane ^ 1
                     if (G == 4) f3_merge<K, 0x4E>(key, lmin);   // quad_perm [2,3,0,1]: lane ^ 2
 #pragma unroll
@@ -745,6 +754,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                 // ties on w0 at or above the want-th place need the full key: equal
                 // neighbours among places [0, want], or a distance that left the list
                 // equal to the want-th
+                if (t0i == 0) F3_STAMP(10);
                 bool tie = rmin == dk[want - 1];
 #pragma unroll
                 for (int r = 0; r + 1 < K; ++r) tie = tie || ((uint32_t)r + 1 <= want && dk[r] == dk[r + 1]);
@@ -753,7 +763,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                     // path) while a slot is free and they fit a wave; else phase B here
                     uint32_t tsl = kTieSlots;
                     if (gj == 0) {
-                        atomicAdd(a.ctr + 2, 1u);
+                        atomicAdd(ntie + 1, 1u);
                         if (mm <= 64) tsl = atomicAdd(ntie, 1u);
                     }
                     if (G > 1) tsl = (uint32_t)__shfl((int)tsl, (int)(lane & ~(G - 1)));
@@ -804,8 +814,11 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         }
         sync_lds();
         if (t0i == 0) F3_STAMP(5);
-        if ((a.dbg & 256) && threadIdx.x == 0 && t0i == 0) {
+        if (Diag && (a.dbg & 256) && threadIdx.x == 0 && t0i == 0) {
+            a.stamps[(uint64_t)blockIdx.x * 16 + 11] = __builtin_amdgcn_s_memrealtime();
             a.stamps[(uint64_t)blockIdx.x * 16 + 13] = mt;
+            a.stamps[(uint64_t)blockIdx.x * 16 + 12] =
+                (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 8 & 0xFFu) | (__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xFu) << 8;
             a.stamps[(uint64_t)blockIdx.x * 16 + 14] = ntie[0];
         }
         // B: one wave per target for ties and large subtrees (the level-Lm subtree range)
@@ -821,6 +834,10 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         if (ns || t0i + kF3Threads < mt) sync_lds();   // T / slow are reused by the next chunk
         if (t0i == 0) F3_STAMP(6);
     }
+    // the wave-path statistic: one global atomic per block (a per-target atomic on one
+    // address serialises at the memory side: 1,000 of them held this kernel ~10 µs)
+    sync_lds();
+    if (threadIdx.x == 0 && ntie[1]) atomicAdd(a.ctr + 2, ntie[1]);
     F3_STAMP(7);
 }
 
@@ -994,12 +1011,25 @@ size_t batch_bytes(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     const BatchPlan P = plan_batch(n, q, k, num_cus);
     const size_t np = 1ull << P.b1;
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    return batch_clean_bytes() + 2 * al((size_t)q * 4) + al(np * P.tcap * 8) + al(np * kTieSlots * 64 * 8) +
+    return batch_clean_bytes() + 2 * al((size_t)q * 4) + al(np * 4) + al(np * P.tcap * 8) + al(np * kTieSlots * 64 * 8) +
            al(np * kF3Cap * 8);
 }
 
-const uint32_t* batch_stats(const void* ws) {
-    return reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(ws) + 65536);
+hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t* stats4,
+                            hipStream_t s) {
+    const BatchPlan P = plan_batch(n, q, k, num_cus);
+    const size_t np = 1ull << P.b1;
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const uint8_t* w = static_cast<const uint8_t*>(ws);
+    std::vector<uint32_t> ps(np);
+    hipError_t e = hipMemcpyAsync(stats4, w + 65536, 16, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(ps.data(), w + batch_clean_bytes() + 2 * al((size_t)q * 4), np * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    uint64_t tot = 0;
+    for (uint32_t v : ps) tot += v;
+    stats4[1] = (uint32_t)tot;   // survivors = sum over partitions
+    return e;
 }
 
 hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp,
@@ -1022,6 +1052,7 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
     uint4* tie_hdr = reinterpret_cast<uint4*>(take((size_t)kMaxParts * kTieSlots * 16));
     uint32_t* fb_list = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
     uint32_t* tspill = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
+    uint32_t* pstat = reinterpret_cast<uint32_t*>(take((size_t)np * 4));
     uint2* tbuf = reinterpret_cast<uint2*>(take((size_t)np * P.tcap * 8));
     uint2* tie_cand = reinterpret_cast<uint2*>(take((size_t)np * kTieSlots * 64 * 8));
     uint2* pbuf = reinterpret_cast<uint2*>(take((size_t)np * kF3Cap * 8));
@@ -1031,9 +1062,13 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
                              (const void*)k_f2_filter<kF2Stream, false>, (const void*)k_f2_filter<kF2Dense, true>,
                              (const void*)k_f2_filter<kF2Sparse, true>};
         for (const void* f : f2s) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
-        (void)hipFuncSetAttribute((const void*)k_f3_answer<8>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
-        (void)hipFuncSetAttribute((const void*)k_f3_answer<16>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
-        (void)hipFuncSetAttribute((const void*)k_f3_answer<32>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
+        const void* f3s[] = {(const void*)k_f3_answer<8, false, true>,  (const void*)k_f3_answer<16, false, true>,
+                             (const void*)k_f3_answer<32, false, true>, (const void*)k_f3_answer<8, true, true>,
+                             (const void*)k_f3_answer<16, true, true>,  (const void*)k_f3_answer<32, true, true>,
+                             (const void*)k_f3_answer<8, false, false>, (const void*)k_f3_answer<16, false, false>,
+                             (const void*)k_f3_answer<32, false, false>, (const void*)k_f3_answer<8, true, false>,
+                             (const void*)k_f3_answer<16, true, false>, (const void*)k_f3_answer<32, true, false>};
+        for (const void* f : f3s) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
         attr_set = true;
     }
     static const uint32_t dbg = getenv("DHTGPU_DBG") ? (uint32_t)atoi(getenv("DHTGPU_DBG")) : 0u;
@@ -1063,15 +1098,32 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
         (void)hipEventRecord(ev[2], s);
         (void)hipEventRecord(ev[3], s);
     }
-    if (dbg & ~(48u | 256u)) {   // experiments: F1 + F2 only
+    if (dbg & ~(48u | 256u | 512u | 1024u | 2048u | 4096u | 8192u)) {   // experiments: F1 + F2 only
         for (int i = 4; ev && i < 8; ++i) (void)hipEventRecord(ev[i], s);
         return hipGetLastError();
     }
     F3Args a{pbuf, pcount, kF3Cap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, planes, stride, n,
-             tp, ts, k, gidx, base, out_idx, out_cnt, ctr, fb_list, tie_hdr, tie_cand, dbg, stamps};
-    if (k <= 8) go(2, k_f3_answer<8>, dim3(np), dim3(kF3Threads), f3_lds(P), a);
-    else if (k <= 16) go(2, k_f3_answer<16>, dim3(np), dim3(kF3Threads), f3_lds(P), a);
-    else go(2, k_f3_answer<32>, dim3(np), dim3(kF3Threads), f3_lds(P), a);
+             tp, ts, k, gidx, base, out_idx, out_cnt, ctr, fb_list, pstat, tie_hdr, tie_cand, dbg, stamps};
+    size_t l3 = f3_lds(P);
+    if (dbg & 4096) l3 = l3 > 81920 ? l3 : 81920;   // experiment: 2 F3 blocks per CU
+    if (dbg & 8192) l3 = l3 > 54000 ? l3 : 54000;   // experiment: 3 F3 blocks per CU
+    const dim3 g3(np), b3(kF3Threads);
+    const bool ex = n >= k && (k == 8 || k == 16 || k == 32);
+#define F3_GO(KK, DD)                                                         \
+    do {                                                                      \
+        if (ex) go(2, k_f3_answer<KK, DD, true>, g3, b3, l3, a);            \
+        else go(2, k_f3_answer<KK, DD, false>, g3, b3, l3, a);              \
+    } while (0)
+    if (dbg) {
+        if (k <= 8) F3_GO(8, true);
+        else if (k <= 16) F3_GO(16, true);
+        else F3_GO(32, true);
+    } else {
+        if (k <= 8) F3_GO(8, false);
+        else if (k <= 16) F3_GO(16, false);
+        else F3_GO(32, false);
+    }
+#undef F3_GO
     if (dbg & 256) {   // phase profile of F2 (100 MHz real-time stamps: 10 ns ticks)
         std::vector<unsigned long long> h((size_t)P.nblk2 * 16);
         (void)hipMemcpyAsync(h.data(), stamps + 8192 * 16, h.size() * 8, hipMemcpyDeviceToHost, s);
@@ -1129,6 +1181,32 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
                         if (!d[g][t].empty())
                             fprintf(stderr, "  phase A %s %s (%zu blocks): %s\n", g ? "G<=2" : "G=4 ", t ? "ties" : "none",
                                     d[g][t].size(), pct(d[g][t]).c_str());
+            }
+            {   // the slowest blocks, phase by phase
+                std::vector<std::pair<unsigned long long, uint32_t>> ord;
+                for (uint32_t b : live) ord.push_back({h[b * 16 + 7] - t0min, b});
+                std::sort(ord.rbegin(), ord.rend());
+                for (size_t ii = 0; ii < ord.size() && ii < 3; ++ii) {   // CU-mates of the slowest blocks
+                    const uint32_t b = ord[ii].second;
+                    fprintf(stderr, "  CU of block %u:\n", b);
+                    for (uint32_t c : live) {
+                        if (h[c * 16 + 12] != h[b * 16 + 12]) continue;
+                        fprintf(stderr, "     block %4u ends of phases:", c);
+                        for (int j = 0; j < 8; ++j) fprintf(stderr, " %.2f", (double)(h[c * 16 + j] - t0min) / 100.0);
+                        fprintf(stderr, "  loop %.2f-%.2f\n", (double)(h[c * 16 + 8] - t0min) / 100.0, (double)(h[c * 16 + 9] - t0min) / 100.0);
+                    }
+                }
+                for (size_t ii = 0; ii < ord.size() && ii < 10; ++ii) {
+                    const size_t i = ii < 5 ? ii : ord.size() - 10 + ii;
+                    const uint32_t b = ord[i].second;
+                    fprintf(stderr, "  slow block %u (mt %llu, ties %llu): start %.2f phases", b, h[b * 16 + 13], h[b * 16 + 14],
+                            (double)(h[b * 16] - t0min) / 100.0);
+                    for (int j = 1; j < 8; ++j) fprintf(stderr, " %.2f", (double)(h[b * 16 + j] - h[b * 16 + j - 1]) / 100.0);
+                    fprintf(stderr, "  A: level %.2f loop %.2f merge %.2f out %.2f",
+                            (double)(h[b * 16 + 8] - h[b * 16 + 4]) / 100.0, (double)(h[b * 16 + 9] - h[b * 16 + 8]) / 100.0,
+                            (double)(h[b * 16 + 10] - h[b * 16 + 9]) / 100.0, (double)(h[b * 16 + 5] - h[b * 16 + 10]) / 100.0);
+                    fprintf(stderr, "\n");
+                }
             }
             std::vector<double> en, st;
             for (uint32_t b : live) {

@@ -89,7 +89,9 @@ size_t batch_bytes(uint64_t n, uint32_t q, uint32_t k, int num_cus);
 // leading workspace bytes that must be zero before the first call (they are left zero)
 size_t batch_clean_bytes();
 // device address of {fallback targets, survivors} of the last call on workspace ws
-const uint32_t* batch_stats(const void* ws);
+// stats4 = {fallback targets, survivors, wave-path targets, 0} of the last call (synchronises s)
+hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t* stats4,
+                            hipStream_t s);
 hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp,
                              uint64_t ts, uint32_t q, uint32_t k, const uint32_t* gidx, uint32_t base,
                              uint32_t* out_idx, uint32_t* out_cnt, int num_cus, uint32_t skip, uint32_t pval,
