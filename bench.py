@@ -35,6 +35,10 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# Two batches in flight (--inflight) need their streams on different hardware queues; HIP's
+# default of 4 queues per process is shared round-robin by every stream the process creates
+# (torch's, the context's), so ask for 8 before the runtime starts.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -78,6 +82,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-scan", action="store_true", help="skip the reference K1 scan measurement (index algo)")
     ap.add_argument("--verify", type=int, default=16, help="targets re-checked against the oracle (rank 0)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="batch algo: consecutive steps alternate over this many streams, so one step's "
+                         "latency-bound F3/F4 overlaps the next step's HBM-bound F2 (1 = strictly serial)")
     return ap.parse_args()
 
 
@@ -176,7 +183,7 @@ def main():
     rec = torch.empty((a.q, a.k, 6), dtype=torch.int32, device=dev) if collective else None
     gathered = torch.empty((world * a.q, a.k, 6), dtype=torch.int32, device=dev) if collective else None
 
-    def local_lookup(out_i, out_c, out_r, base):
+    def local_lookup(out_i, out_c, out_r, base, stream=stream):
         if a.algo == "batch":
             ctx.batch_topk_dev(tp.data_ptr(), ts, q_local, a.k, out_i, out_c, out_r, base, stream)
         elif a.algo == "index":
@@ -185,9 +192,18 @@ def main():
         else:
             ctx.topk_dev(tp.data_ptr(), ts, q_local, a.k, out_i, out_c, out_r, base, stream)
 
+    # in-flight steps: step i runs on stream i % D with its own output buffers
+    D = max(1, a.inflight) if (a.algo == "batch" and not collective) else 1
+    streams = [tstream] + [torch.cuda.Stream(dev) for _ in range(D - 1)]
+    outs = [(out_idx, out_cnt)] + [(torch.empty_like(out_idx), torch.empty_like(out_cnt)) for _ in range(D - 1)]
+    step_no = [0]
+
     def step():
+        i = step_no[0]
+        step_no[0] += 1
         if not collective:
-            local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0)
+            oi, oc = outs[i % D]
+            local_lookup(oi.data_ptr(), oc.data_ptr(), None, 0, streams[i % D].cuda_stream)
         else:
             local_lookup(None, None, rec.data_ptr(), lo)
             sharding.gather_records(rec, out=gathered)
@@ -218,7 +234,7 @@ def main():
     wall = float(t.item())
     ms_per_step = wall * 1e3 / a.steps
     # outputs of the last timed step (for the verification below)
-    got_idx = out_idx[:q_local].cpu().numpy().view(np.uint32).copy()
+    got_idx = outs[(step_no[0] - 1) % D][0][:q_local].cpu().numpy().view(np.uint32).copy()
     got_tg = tgidx[:q_local].cpu().numpy().view(np.uint32).copy() if tgidx is not None else np.arange(q_local)
 
     def ev_time(fn, reps):
@@ -231,6 +247,9 @@ def main():
         return e0.elapsed_time(e1) / reps
 
     reps = max(3, min(a.steps, 20))
+    # single-batch latency: the same step strictly serial on one stream
+    lat_ms = ev_time(lambda: local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0), reps) \
+        if not collective else None
     if a.algo == "batch":
         # per-kernel device times (HIP events between F1..F4 on the bench stream)
         runs = [ctx.batch_topk_timed(tp.data_ptr(), ts, q_local, a.k, out_idx.data_ptr(), out_cnt.data_ptr(), stream)
@@ -316,7 +335,9 @@ def main():
             "data": "synthetic: splitmix64 ids and targets generated in HBM (SURVEY 8(d) spec)",
             "config": {"workload": f"cfg2 batched k-NN: {a.q} targets x {a.n} ids (2^{a.n.bit_length()-1}), k={a.k}",
                        "n_ids": a.n, "n_targets": a.q, "k": a.k, "algo": a.algo, "route": route,
-                       "ids_per_gpu": n_local, "targets_per_gpu": q_local, "parallelism": par},
+                       "ids_per_gpu": n_local, "targets_per_gpu": q_local, "parallelism": par,
+                       "inflight": D},
+            "latency_ms_per_batch": lat_ms,
             "roofline": roof,
         }
         if a.simulate_world:

@@ -75,8 +75,21 @@ struct dhtgpu_ctx {
     DevBuf net_io;          // crawl model: search-batch staging
     uint64_t net_seed = 0;
     bool net_valid = false, net_has_dead = false;
-    DevBuf batch;           // K6 workspace; its 64 KB bitmap head is all-zero between calls
-    bool batch_clean = false;
+    // K6 workspaces: kBatchDepth slots used round-robin, so that up to kBatchDepth calls issued
+    // on different streams run concurrently (one batch's latency-bound F3/F4 overlaps the next
+    // batch's HBM-bound F2).  A call on a slot last used on another stream first waits for
+    // that stream's work so far (an event recorded there at switch time, so calls that stay on
+    // one stream pay nothing); calls on one stream keep plain stream order.
+    struct BatchSlot {
+        DevBuf ws;              // workspace; its zero-between-calls head (bitmap, counters) stays clean
+        DevBuf out_idx, out_cnt;   // record mode: local results before the record conversion
+        bool clean = false;
+        hipEvent_t done = nullptr;
+        hipStream_t last = nullptr;
+    };
+    static constexpr int kBatchDepth = 2;
+    BatchSlot bslot[kBatchDepth];
+    int bnext = 0, blast = 0;
 
     hipError_t bind() { return hipSetDevice(device); }
 
@@ -142,9 +155,14 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
     if (!c) return;
     (void)c->bind();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& b : c->bslot) {   // slots last used on other streams: let that work finish
+        if (b.last && b.last != c->stream) (void)hipStreamSynchronize(b.last);
+        if (b.done) (void)hipEventDestroy(b.done);
+    }
     for (DevBuf* b : {&c->planes, &c->staging, &c->targets, &c->out_idx, &c->out_cnt, &c->rec,
-                      &c->aux, &c->aux2, &c->aux3, &c->index, &c->gidx, &c->batch, &c->wire,
-                      &c->net_sorted, &c->net_dead, &c->net_io})
+                      &c->aux, &c->aux2, &c->aux3, &c->index, &c->gidx, &c->wire,
+                      &c->net_sorted, &c->net_dead, &c->net_io, &c->bslot[0].ws, &c->bslot[0].out_idx,
+                      &c->bslot[0].out_cnt, &c->bslot[1].ws, &c->bslot[1].out_idx, &c->bslot[1].out_cnt})
         b->release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -454,27 +472,38 @@ int dhtgpu_index_topk(dhtgpu_ctx* c, const uint8_t* t20, uint32_t q, uint32_t k,
 static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k, uint32_t* out_idx,
                      uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base, hipStream_t s, hipEvent_t* ev) {
     if (!batch_supported(c->n, q, k, c->num_cus)) return DHTGPU_ERANGE;
+    dhtgpu_ctx::BatchSlot& b = c->bslot[c->bnext];
+    // a slot last used on another stream: wait for that stream's work so far (it includes the
+    // slot's previous call); same stream: stream order suffices
+    if (b.last && b.last != s) {
+        if (!b.done) DHT_TRY(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+        DHT_TRY(hipEventRecord(b.done, b.last));
+        DHT_TRY(hipStreamWaitEvent(s, b.done, 0));
+    }
     const size_t need = batch_bytes(c->n, q, k, c->num_cus);
-    if (need > c->batch.cap) c->batch_clean = false;
-    DHT_TRY(c->batch.ensure(need));
-    if (!c->batch_clean) DHT_TRY(hipMemsetAsync(c->batch.p, 0, batch_clean_bytes(), s));
-    c->batch_clean = false;   // re-established below once every launch went through
+    if (need > b.ws.cap) b.clean = false;
+    DHT_TRY(b.ws.ensure(need));
+    if (!b.clean) DHT_TRY(hipMemsetAsync(b.ws.p, 0, batch_clean_bytes(), s));
+    b.clean = false;   // re-established below once every launch went through
+    c->blast = c->bnext;
+    c->bnext = (c->bnext + 1) % dhtgpu_ctx::kBatchDepth;
     const uint32_t* gidx = c->has_gidx ? c->gidx.as<uint32_t>() : nullptr;
     uint32_t* li = out_idx;
     uint32_t* lc = out_cnt;
     if (out_rec) {   // local indices first, then candidate records for a cross-shard merge
-        DHT_TRY(c->out_idx.ensure((size_t)q * k * 4));
-        DHT_TRY(c->out_cnt.ensure((size_t)q * 4));
-        li = c->out_idx.as<uint32_t>();
-        lc = c->out_cnt.as<uint32_t>();
+        DHT_TRY(b.out_idx.ensure((size_t)q * k * 4));
+        DHT_TRY(b.out_cnt.ensure((size_t)q * 4));
+        li = b.out_idx.as<uint32_t>();
+        lc = b.out_cnt.as<uint32_t>();
     }
-    DHT_TRY(launch_batch_topk(c->batch.p, c->planes.as<uint32_t>(), c->stride, c->n, tp, ts, q, k,
+    DHT_TRY(launch_batch_topk(b.ws.p, c->planes.as<uint32_t>(), c->stride, c->n, tp, ts, q, k,
                               out_rec ? nullptr : gidx, out_rec ? 0u : idx_base, li, lc, c->num_cus, c->shard_pbits,
                               c->shard_pval, s, ev));
     if (out_rec)
         DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
                                     out_rec, s));
-    c->batch_clean = true;
+    b.last = s;
+    b.clean = true;
     return DHTGPU_OK;
 }
 
@@ -505,7 +534,7 @@ int dhtgpu_batch_topk_timed(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint
     if (r) return r;
     DHT_TRY(e);
     if (stats4) {
-        DHT_TRY(batch_read_stats(c->batch.p, c->n, q, k, c->num_cus, stats4, s));
+        DHT_TRY(batch_read_stats(c->bslot[c->blast].ws.p, c->n, q, k, c->num_cus, stats4, s));
     }
     return DHTGPU_OK;
 }
