@@ -144,15 +144,19 @@ int dhtgpu_index_topk(dhtgpu_ctx* ctx, const uint8_t* targets20_be, uint32_t q, 
  * the ids that share the batch targets' level-Lm prefixes (Lm ~ log2(n / 4k)), and answers
  * every target from its complete prefix subtree in LDS; targets whose subtree holds fewer
  * than min(k, n) ids take an exact brute-force pass.  Same output forms as
- * dhtgpu_topk_dev.  DHTGPU_ERANGE when n > 2^28 or q > 2^22 (use dhtgpu_index_topk_dev).
- * Stream-ordered, no host sync. */
+ * dhtgpu_topk_dev.  DHTGPU_ERANGE when n >= 2^31 or q > 2^22 (use dhtgpu_index_topk_dev).
+ * Stream-ordered, no host sync.  A context keeps two workspaces used in turn, so two
+ * consecutive calls issued on different streams run concurrently (one batch's
+ * latency-bound answer phase overlaps the next batch's HBM-bound id stream); a call that
+ * reuses a workspace last used on another stream first waits for that stream. */
 int dhtgpu_batch_topk_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
                           uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec,
                           uint32_t idx_base, void* stream);
-/* Diagnostics: the same call with HIP events between its kernels; synchronises and returns
- * per-phase device milliseconds ms4 = {F1 mark targets, F2 filter ids, F3 answer,
- * F4 fallback} and (nullable) stats4 = {targets answered by the F4 fallback, surviving ids,
- * targets answered by F3's exact wave path (w0 ties, large subtrees), 0}. */
+/* Diagnostics: the same call with a start/stop HIP event pair recorded by each kernel's own
+ * dispatch; synchronises and returns per-kernel device milliseconds ms4 = {F1 bucket
+ * targets, F2 filter ids, F3 answer, F4 ties + fallback} and (nullable) stats4 = {targets
+ * answered by the brute-force fallback, surviving ids, targets answered by an exact wave
+ * (w0 ties, large subtrees), 0}. */
 int dhtgpu_batch_topk_timed(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
                             uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, void* stream, float* ms4,
                             uint32_t* stats4);
