@@ -70,6 +70,19 @@ __device__ __forceinline__ void sync_lds() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Inclusive scan over the 64 lanes of a wave with DPP (no LDS): row_shr 1/2/4/8 inside each
+// 16-lane row, then row_bcast 15 / 31 across rows.  Lanes whose DPP source is out of range
+// take `old` = 0.  Needs the whole wave active.
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return x;
+}
+
 // Exclusive scan of a[0, len) in LDS by a block of NT threads; returns the total.  Every
 // thread must call it.  wsum: NT / 64 + 1 words of LDS scratch.
 template <int NT>
@@ -81,22 +94,12 @@ __device__ uint32_t scan_lds(uint32_t* a, uint32_t len, uint32_t* wsum) {
     const uint32_t e = b + per < len ? b + per : len;
     uint32_t s = 0;
     for (uint32_t i = b; i < e; ++i) s += a[i];
-    uint32_t x = s;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o);
-        if (lane >= (uint32_t)o) x += y;
-    }
+    const uint32_t x = wave_scan_incl(s);
     if (lane == 63) wsum[w] = x;
     sync_lds();
     if (threadIdx.x < 64) {
         const uint32_t v = lane < (uint32_t)NW ? wsum[lane] : 0u;
-        uint32_t xv = v;
-#pragma unroll
-        for (int o = 1; o < NW; o <<= 1) {
-            const uint32_t y = __shfl_up(xv, o);
-            if (lane >= (uint32_t)o) xv += y;
-        }
+        const uint32_t xv = wave_scan_incl(v);
         if (lane < (uint32_t)NW) wsum[lane] = xv - v;
         if (lane == (uint32_t)NW - 1) wsum[NW] = xv;
     }
