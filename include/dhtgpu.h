@@ -145,7 +145,7 @@ int dhtgpu_index_topk(dhtgpu_ctx* ctx, const uint8_t* targets20_be, uint32_t q, 
  * every target from its complete prefix subtree in LDS; targets whose subtree holds fewer
  * than min(k, n) ids take an exact brute-force pass.  Same output forms as
  * dhtgpu_topk_dev.  DHTGPU_ERANGE when n >= 2^31 or q > 2^22 (use dhtgpu_index_topk_dev).
- * Stream-ordered, no host sync.  A context keeps two workspaces used in turn, so two
+ * Stream-ordered, no host sync.  A context keeps four workspaces used in turn, so up to four
  * consecutive calls issued on different streams run concurrently (one batch's
  * latency-bound answer phase overlaps the next batch's HBM-bound id stream); a call that
  * reuses a workspace last used on another stream first waits for that stream. */

@@ -87,7 +87,7 @@ struct dhtgpu_ctx {
         hipEvent_t done = nullptr;
         hipStream_t last = nullptr;
     };
-    static constexpr int kBatchDepth = 2;
+    static constexpr int kBatchDepth = 4;
     BatchSlot bslot[kBatchDepth];
     int bnext = 0, blast = 0;
 
@@ -161,9 +161,10 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
     }
     for (DevBuf* b : {&c->planes, &c->staging, &c->targets, &c->out_idx, &c->out_cnt, &c->rec,
                       &c->aux, &c->aux2, &c->aux3, &c->index, &c->gidx, &c->wire,
-                      &c->net_sorted, &c->net_dead, &c->net_io, &c->bslot[0].ws, &c->bslot[0].out_idx,
-                      &c->bslot[0].out_cnt, &c->bslot[1].ws, &c->bslot[1].out_idx, &c->bslot[1].out_cnt})
+                      &c->net_sorted, &c->net_dead, &c->net_io})
         b->release();
+    for (auto& b : c->bslot)
+        for (DevBuf* d : {&b.ws, &b.out_idx, &b.out_cnt}) d->release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
