@@ -23,7 +23,10 @@ Multi-GPU (one process per GPU, torch.distributed over RCCL; --route):
              minimum shard size with one all-reduce and refuses otherwise.
   broadcast  ids range-sharded, all targets on every rank, per-rank candidate records
              exchanged by one RCCL all-gather, merged by K3 (SURVEY §8(e) north-star scheme).
-Total work is fixed as N grows ("scaling": "strong").
+Scaling (--scaling): "weak" (default with the prefix route: the path partitions into
+independent prefix shards, so every rank keeps the one-GPU workload -- --n ids and --q
+targets per GPU out of a global problem N times as large; value = all ranks' targets / the
+slowest rank's time) or "strong" (--n and --q are the global totals, split across ranks).
 
 Prints ONE JSON line on rank 0.
 """
@@ -72,6 +75,12 @@ def parse():
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--algo", choices=["batch", "index", "scan"], default="batch")
     ap.add_argument("--route", choices=["auto", "prefix", "broadcast"], default="auto")
+    ap.add_argument("--shard-index", choices=["local", "global"], default="local",
+                    help="prefix shards: results as shard-local node indices (the rank owns its shard's "
+                         "node table) or mapped to global stream indices (one gather per result)")
+    ap.add_argument("--scaling", choices=["auto", "weak", "strong"], default="auto",
+                    help="weak: --n/--q per GPU (global problem grows with N); strong: --n/--q global. "
+                         "auto = weak for the prefix route, strong for broadcast")
     ap.add_argument("--sharded", action="store_true",
                     help="use the multi-GPU code path (and its collectives) even with one rank")
     ap.add_argument("--simulate-world", type=int, default=0,
@@ -133,6 +142,12 @@ def main():
         route = "prefix" if (a.algo in ("index", "batch") and pow2(world)) else "broadcast"
     if a.simulate_world:
         assert world == 1 and route == "prefix" and pow2(a.simulate_world)
+    scaling = a.scaling if a.scaling != "auto" else ("weak" if route == "prefix" else "strong")
+    G_eff = a.simulate_world if a.simulate_world else world
+    if scaling == "weak":   # --n / --q are per GPU: the global problem is G times larger
+        a.n_total, a.q_total = a.n * G_eff, a.q * G_eff
+    else:
+        a.n_total, a.q_total = a.n, a.q
     use_dist = world > 1 or a.sharded
     if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -150,19 +165,20 @@ def main():
 
     G, R = (a.simulate_world, a.simulate_rank) if a.simulate_world else (world, rank)
     pbits = G.bit_length() - 1 if route == "prefix" else 0
-    ts_all = (a.q + 63) // 64 * 64
+    ts_all = (a.q_total + 63) // 64 * 64
     tp_all = torch.empty(5 * ts_all, dtype=torch.int32, device=dev)
-    assert L.dhtgpu_gen_dev(a.seed + 1, 0, a.q, tp_all.data_ptr(), ts_all, stream) == 0
+    assert L.dhtgpu_gen_dev(a.seed + 1, 0, a.q_total, tp_all.data_ptr(), ts_all, stream) == 0
     if route == "prefix":
         if pbits:
-            ctx.gen_ids_prefix(a.seed, a.n, pbits, R)         # this rank's prefix shard, global indices
+            ctx.gen_ids_prefix(a.seed, a.n_total, pbits, R)         # this rank's prefix shard
+            ctx.set_global_indices(a.shard_index == "global")
             tp = torch.empty_like(tp_all)
             tgidx = torch.empty(ts_all, dtype=torch.int32, device=dev)
-            q_local = ctx.select_prefix_dev(tp_all.data_ptr(), ts_all, a.q, pbits, R, tp.data_ptr(), ts_all,
+            q_local = ctx.select_prefix_dev(tp_all.data_ptr(), ts_all, a.q_total, pbits, R, tp.data_ptr(), ts_all,
                                             tgidx.data_ptr(), stream)
         else:                                                 # one shard: the whole set
-            ctx.gen_ids(a.seed, a.n)
-            tp, q_local, tgidx = tp_all, a.q, None
+            ctx.gen_ids(a.seed, a.n_total)
+            tp, q_local, tgidx = tp_all, a.q_total, None
         ts = ts_all
         shard_min = torch.tensor([ctx.num_ids], dtype=torch.int64, device=dev)
         if use_dist:
@@ -172,16 +188,16 @@ def main():
         n_local = ctx.num_ids
         lo = 0
     else:
-        lo, hi = sharding.shard_range(a.n, world, rank)
+        lo, hi = sharding.shard_range(a.n_total, world, rank)
         ctx.gen_ids(a.seed, hi - lo, start=lo)      # this rank's contiguous slice of the global id stream
-        tp, ts, q_local, tgidx = tp_all, ts_all, a.q, None
+        tp, ts, q_local, tgidx = tp_all, ts_all, a.q_total, None
         n_local = hi - lo
     collective = use_dist and route == "broadcast"
     qk = max(q_local, 1)
     out_idx = torch.empty((qk, a.k), dtype=torch.int32, device=dev)
     out_cnt = torch.empty(qk, dtype=torch.int32, device=dev)
-    rec = torch.empty((a.q, a.k, 6), dtype=torch.int32, device=dev) if collective else None
-    gathered = torch.empty((world * a.q, a.k, 6), dtype=torch.int32, device=dev) if collective else None
+    rec = torch.empty((a.q_total, a.k, 6), dtype=torch.int32, device=dev) if collective else None
+    gathered = torch.empty((world * a.q_total, a.k, 6), dtype=torch.int32, device=dev) if collective else None
 
     def local_lookup(out_i, out_c, out_r, base, stream=stream):
         if a.algo == "batch":
@@ -207,7 +223,7 @@ def main():
         else:
             local_lookup(None, None, rec.data_ptr(), lo)
             sharding.gather_records(rec, out=gathered)
-            assert L.dhtgpu_merge_dev(gathered.data_ptr(), world, a.q, a.k, tp.data_ptr(), ts, a.k,
+            assert L.dhtgpu_merge_dev(gathered.data_ptr(), world, a.q_total, a.k, tp.data_ptr(), ts, a.k,
                                       out_idx.data_ptr(), out_cnt.data_ptr(), stream) == 0
 
     for _ in range(a.warmup):
@@ -250,6 +266,12 @@ def main():
     # single-batch latency: the same step strictly serial on one stream
     lat_ms = ev_time(lambda: local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0), reps) \
         if not collective else None
+    lat_global_ms = None
+    if route == "prefix" and pbits and a.shard_index == "local":
+        # the same batch with results mapped to global stream indices (for comparison)
+        ctx.set_global_indices(True)
+        lat_global_ms = ev_time(lambda: local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0), reps)
+        ctx.set_global_indices(False)
     if a.algo == "batch":
         # per-kernel device times (HIP events between F1..F4 on the bench stream)
         runs = [ctx.batch_topk_timed(tp.data_ptr(), ts, q_local, a.k, out_idx.data_ptr(), out_cnt.data_ptr(), stream)
@@ -322,24 +344,30 @@ def main():
                "broadcast": f"id-range shards x{world}" + (" + RCCL all-gather + K3 merge" if collective else "")}[route]
         res = {
             "metric": METRIC,
-            "value": (a.q if not a.simulate_world else q_local) / (ms_per_step * 1e-3),
+            "value": (a.q_total if not a.simulate_world else q_local) / (ms_per_step * 1e-3),
             "unit": "queries/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic: splitmix64 ids and targets generated in HBM (SURVEY 8(d) spec)",
-            "config": {"workload": f"cfg2 batched k-NN: {a.q} targets x {a.n} ids (2^{a.n.bit_length()-1}), k={a.k}",
-                       "n_ids": a.n, "n_targets": a.q, "k": a.k, "algo": a.algo, "route": route,
+            "config": {"workload": f"cfg2 batched k-NN: {a.q} targets x {a.n} ids (2^{a.n.bit_length()-1}), k={a.k}"
+                                   + (f" per GPU ({a.q_total} x {a.n_total} over {G_eff} GPUs)" if scaling == "weak" and G_eff > 1
+                                      else ""),
+                       "n_ids": a.n_total, "n_targets": a.q_total, "k": a.k, "algo": a.algo, "route": route,
                        "ids_per_gpu": n_local, "targets_per_gpu": q_local, "parallelism": par,
-                       "inflight": D},
+                       "inflight": D,
+                       "result_indices": ("shard-local" if a.shard_index == "local" else "global")
+                       if route == "prefix" and pbits else "global"},
             "latency_ms_per_batch": lat_ms,
             "roofline": roof,
         }
+        if lat_global_ms is not None:
+            res["latency_ms_per_batch_global_indices"] = lat_global_ms
         if a.simulate_world:
             res["simulated"] = f"rank {R} of {G} on one GPU; value = this rank's targets / its step time"
         res.update(extra)
@@ -347,17 +375,22 @@ def main():
         # leg (rank 0, N = 1 only)
         if not a.no_cpu and (a.verify or world == 1):
             O = oracle()
-            ids = O.gen_ids(a.seed, a.n)
+            ids = O.gen_ids(a.seed, a.n_total)
             nv = min(q_local, max(a.verify, a.cpu_targets if world == 1 else 0))
-            tg_all = O.gen_ids(a.seed + 1, a.q)
+            tg_all = O.gen_ids(a.seed + 1, a.q_total)
             tg = tg_all[got_tg[:nv]]
             if world == 1 and not a.simulate_world:
                 cb, want = cpu_baseline(ids, tg, a.k, a.cpu_threads)
                 res["cpu_baseline"] = cb
             else:
                 want, _ = O.topk(ids, tg, a.k, threads=a.cpu_threads)
+            got_v = got_idx[:nv]
+            if route == "prefix" and pbits and a.shard_index == "local":
+                # shard-local results -> global stream indices (outside the timed region)
+                gl = np.nonzero((ids[:, 0].astype(np.uint32) >> (8 - pbits)) == R)[0].astype(np.uint32)
+                got_v = np.where(got_v == 0xFFFFFFFF, got_v, gl[np.minimum(got_v, max(gl.size, 1) - 1)])
             res["verified_targets"] = int(nv)
-            res["verified_exact"] = bool(np.array_equal(got_idx[:nv], want))
+            res["verified_exact"] = bool(np.array_equal(got_v, want))
         print(json.dumps(res), flush=True)
     ctx.close()
     if use_dist:

@@ -78,6 +78,11 @@ int dhtgpu_gen_ids(dhtgpu_ctx* ctx, uint64_t seed, uint64_t start, uint64_t n);
  * order.  pbits <= 16. */
 int dhtgpu_gen_ids_prefix(dhtgpu_ctx* ctx, uint64_t seed, uint64_t start, uint64_t n, uint32_t pbits,
                           uint32_t pval);
+/* Prefix shard contexts (dhtgpu_gen_ids_prefix): on != 0 (the default) makes every
+ * lookup return indices into the global stream; on == 0 returns shard-local indices
+ * (positions in get_ids order) -- the handle a rank that owns its shard's node table
+ * keeps, without the per-result gather through the index map. */
+int dhtgpu_set_global_indices(dhtgpu_ctx* ctx, int on);
 uint64_t dhtgpu_num_ids(const dhtgpu_ctx* ctx);
 /* Read back ids [first, first+n) as 20-byte big-endian. */
 int dhtgpu_get_ids(dhtgpu_ctx* ctx, uint64_t first, uint64_t n, uint8_t* out20_be);

@@ -63,6 +63,7 @@ def lib():
         "dhtgpu_set_ids": ([_vp, _u8p, ctypes.c_uint64], ctypes.c_int),
         "dhtgpu_gen_ids": ([_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64], ctypes.c_int),
         "dhtgpu_num_ids": ([_vp], ctypes.c_uint64),
+        "dhtgpu_set_global_indices": ([_vp, ctypes.c_int], ctypes.c_int),
         "dhtgpu_get_ids": ([_vp, ctypes.c_uint64, ctypes.c_uint64, _u8p], ctypes.c_int),
         "dhtgpu_ids_dev": ([_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
         "dhtgpu_topk": ([_vp, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p], ctypes.c_int),
@@ -125,7 +126,7 @@ def exported_symbols():
             "dhtgpu_index_build_timed", "dhtgpu_gen_ids_prefix", "dhtgpu_select_prefix_dev",
             "dhtgpu_batch_topk_dev", "dhtgpu_batch_topk_timed", "dhtgpu_batch_topk", "dhtgpu_table_depth",
             "dhtgpu_buffer_nodes_dev", "dhtgpu_buffer_nodes", "dhtgpu_deserialize_nodes", "dhtgpu_net_prepare",
-            "dhtgpu_search_batch", "dhtgpu_search_batch_dev"]
+            "dhtgpu_search_batch", "dhtgpu_search_batch_dev", "dhtgpu_set_global_indices"]
 
 
 def _ids(a, name="ids"):
@@ -188,6 +189,10 @@ class Context:
         """Keep the ids of the stream [start, start+n) whose top pbits bits == pval
         (a prefix shard); result indices refer to the global stream."""
         _check(lib().dhtgpu_gen_ids_prefix(self._h, seed, start, n, pbits, pval), "gen_ids_prefix")
+
+    def set_global_indices(self, on):
+        """Prefix shards: results as global stream indices (True, default) or shard-local."""
+        _check(lib().dhtgpu_set_global_indices(self._h, int(bool(on))), "set_global_indices")
 
     def select_prefix_dev(self, planes_ptr, stride, n, pbits, pval, out_planes_ptr, out_stride, out_gidx_ptr=None,
                           stream=None):

@@ -65,7 +65,10 @@ struct dhtgpu_ctx {
     bool has_ids = false;
     DevBuf gidx;            // shard -> global index map (dhtgpu_gen_ids_prefix), else unused
     bool has_gidx = false;
-    uint32_t shard_pbits = 0, shard_pval = 0;   // every id's top pbits bits == pval (prefix shard)
+    bool map_global = true;  // prefix shard results: global stream indices (else shard-local)
+    const uint32_t* out_map() const { return has_gidx && map_global ? gidx.as<uint32_t>() : nullptr; }
+    uint32_t shard_pbits = 0;   // prefix shard: every id shares its top shard_pbits bits
+    DevBuf w0s;                 // prefix shard: word 0 shifted left by shard_pbits (stride u32)
     DevBuf index;           // K4 workspace: entries | directory | partition scratch
     uint32_t index_B = 0;
     bool index_valid = false;
@@ -195,7 +198,7 @@ static int alloc_ids(dhtgpu_ctx* c, uint64_t n) {
     c->has_ids = false;
     c->index_valid = false;
     c->net_valid = false;
-    c->shard_pbits = c->shard_pval = 0;
+    c->shard_pbits = 0;
     c->has_gidx = false;
     c->stride = pad_ids(n ? n : 1);
     DHT_TRY(c->planes.ensure((size_t)c->stride * 5 * 4));
@@ -252,8 +255,17 @@ int dhtgpu_gen_ids_prefix(dhtgpu_ctx* c, uint64_t seed, uint64_t start, uint64_t
     r = finish_ids(c, m);
     if (r) return r;
     c->has_gidx = true;
-    c->shard_pbits = pbits;
-    c->shard_pval = pval;
+    if (pbits) {
+        DHT_TRY(c->w0s.ensure((size_t)c->stride * 4));
+        DHT_TRY(launch_shift_w0(c->planes.as<uint32_t>(), c->stride, pbits, c->w0s.as<uint32_t>(), c->stream));
+        c->shard_pbits = pbits;
+    }
+    return DHTGPU_OK;
+}
+
+int dhtgpu_set_global_indices(dhtgpu_ctx* c, int on) {
+    if (!c) return DHTGPU_EINVAL;
+    c->map_global = on != 0;
     return DHTGPU_OK;
 }
 
@@ -310,7 +322,7 @@ int dhtgpu_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, 
     DHT_TRY(c->bind());
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     const ScanPlan p = plan_scan(c->n, q, c->num_cus);
-    const uint32_t* gidx = c->has_gidx ? c->gidx.as<uint32_t>() : nullptr;
+    const uint32_t* gidx = c->out_map();
     if ((p.splits == 1 || c->n == 0) && !gidx) {   // one pass writes the final form directly
         DHT_TRY(launch_scan(c->planes.as<uint32_t>(), c->stride, c->n, p, tp, ts, q, k, out_idx,
                             out_cnt, out_rec, idx_base, s));
@@ -428,7 +440,7 @@ int dhtgpu_index_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     if (!q) return DHTGPU_OK;
     DHT_TRY(c->bind());
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    const uint32_t* gidx = c->has_gidx ? c->gidx.as<uint32_t>() : nullptr;
+    const uint32_t* gidx = c->out_map();
     uint32_t* li = out_idx;
     uint32_t* lc = out_cnt;
     if (out_rec) {   // candidate records for a cross-shard merge
@@ -488,7 +500,7 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     b.clean = false;   // re-established below once every launch went through
     c->blast = c->bnext;
     c->bnext = (c->bnext + 1) % dhtgpu_ctx::kBatchDepth;
-    const uint32_t* gidx = c->has_gidx ? c->gidx.as<uint32_t>() : nullptr;
+    const uint32_t* gidx = c->out_map();
     uint32_t* li = out_idx;
     uint32_t* lc = out_cnt;
     if (out_rec) {   // local indices first, then candidate records for a cross-shard merge
@@ -499,7 +511,7 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     }
     DHT_TRY(launch_batch_topk(b.ws.p, c->planes.as<uint32_t>(), c->stride, c->n, tp, ts, q, k,
                               out_rec ? nullptr : gidx, out_rec ? 0u : idx_base, li, lc, c->num_cus, c->shard_pbits,
-                              c->shard_pval, s, ev));
+                              c->shard_pbits ? c->w0s.as<uint32_t>() : nullptr, s, ev));
     if (out_rec)
         DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
                                     out_rec, s));
@@ -677,7 +689,7 @@ int dhtgpu_cached_nodes(dhtgpu_ctx* c, const uint8_t* accept, const uint8_t* t20
     DHT_TRY(c->aux3.ensure((size_t)q * 4));
     DHT_TRY(launch_cached(c->planes.as<uint32_t>(), c->stride, c->n, d_acc, c->targets.as<uint32_t>(),
                           ts, q, count, c->aux2.as<uint32_t>(), c->aux3.as<uint32_t>(), c->stream));
-    if (c->has_gidx)
+    if (c->out_map())
         DHT_TRY(launch_map_idx(c->aux2.as<uint32_t>(), (uint64_t)q * count, c->gidx.as<uint32_t>(), 0, c->stream));
     DHT_TRY(hipMemcpyAsync(out_idx, c->aux2.p, (size_t)q * count * 4, hipMemcpyDeviceToHost, c->stream));
     DHT_TRY(hipMemcpyAsync(out_cnt, c->aux3.p, (size_t)q * 4, hipMemcpyDeviceToHost, c->stream));

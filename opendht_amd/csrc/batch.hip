@@ -124,33 +124,33 @@ __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
 
 // ---- F1: mark target prefixes, bucket the targets by partition ----------------------------
 // One thread per target: it sets the target's level-Lm prefix bit in the bitmap and appends
-// {w0 << skip, index} to its partition's bucket tbuf[p][...] (slot from a returning atomic on
-// tcount[p]; F3 reads the bucket as one coalesced run).  Shard contexts
-// (dhtgpu_gen_ids_prefix): every id carries the same top `skip` bits `pval`; all kernels work
-// on w0 << skip (order-preserving inside the shard).  A target whose top bits differ
-// (foreign), or whose bucket is full, goes to the spill list (count ctr[kSpill]); F3 moves
-// the spill list to the F4 fallback list.
+// {w0, index} to its partition's bucket tbuf[p][...] (slot from a returning atomic on
+// tcount[p]; F3 reads the bucket as one coalesced run).  Prefix-shard contexts
+// (dhtgpu_gen_ids_prefix: every id shares its top `shift` bits) keep a second word-0 plane
+// shifted left by `shift` (the next bits of word 1 shifted in), and the targets' word 0 is
+// shifted the same way here: inside the shard the dropped bits XOR to one constant for every
+// id, so the order is unchanged -- for targets of other prefixes too -- and word 0 keeps 32
+// distinguishing bits.  A target whose bucket is full goes to the spill list (count
+// ctr[kSpill]); F3 moves the spill list to the F4 fallback list.
 constexpr uint32_t kSpill = 8;   // ctr word: spilled targets (all-zero between calls)
 
-__global__ __launch_bounds__(kF1Threads) void k_f1_targets(const uint32_t* __restrict__ tw0, uint32_t q, uint32_t Lm,
-                                                          uint32_t b1, uint32_t skip, uint32_t pval,
-                                                          uint32_t* __restrict__ bitmap, uint32_t* __restrict__ tcount,
-                                                          uint2* __restrict__ tbuf, uint32_t tcap,
-                                                          uint32_t* __restrict__ ctr, uint32_t* __restrict__ tspill) {
+__global__ __launch_bounds__(kF1Threads) void k_f1_targets(const uint32_t* __restrict__ tw0,
+                                                          const uint32_t* __restrict__ tw1, uint32_t q, uint32_t Lm,
+                                                          uint32_t b1, uint32_t shift, uint32_t* __restrict__ bitmap,
+                                                          uint32_t* __restrict__ tcount, uint2* __restrict__ tbuf,
+                                                          uint32_t tcap, uint32_t* __restrict__ ctr,
+                                                          uint32_t* __restrict__ tspill) {
     if (blockIdx.x == 0 && threadIdx.x < 4) ctr[threadIdx.x] = 0;   // fallback, survivors, wave path, -
     const uint32_t i = blockIdx.x * kF1Threads + threadIdx.x;
     if (i >= q) return;
-    const uint32_t w = tw0[i];
-    const uint32_t v = w << skip;
-    if (skip == 0 || (w >> (32 - skip)) == pval) {
-        const uint32_t pre = top_bits(v, Lm);
-        atomicOr(bitmap + (pre >> 5), 1u << (pre & 31));
-        const uint32_t p = top_bits(v, b1);
-        const uint32_t slot = atomicAdd(tcount + p * kCtrStride, 1u);
-        if (slot < tcap) {
-            tbuf[(uint64_t)p * tcap + slot] = make_uint2(v, i);
-            return;
-        }
+    const uint32_t v = shift ? (tw0[i] << shift) | (tw1[i] >> (32 - shift)) : tw0[i];
+    const uint32_t pre = top_bits(v, Lm);
+    atomicOr(bitmap + (pre >> 5), 1u << (pre & 31));
+    const uint32_t p = top_bits(v, b1);
+    const uint32_t slot = atomicAdd(tcount + p * kCtrStride, 1u);
+    if (slot < tcap) {
+        tbuf[(uint64_t)p * tcap + slot] = make_uint2(v, i);
+        return;
     }
     // spill: one atomic per wave (a single counter would serialise every lane's add)
     const uint64_t sp = __ballot(1);   // the lanes still here (the others returned)
@@ -186,7 +186,6 @@ struct F2Args {
     uint32_t stage;               // LDS stage capacity (entries, <= kStage)
     uint32_t dbg;                 // experiment switches (0 in production)
     uint32_t lim;                 // last 16-B aligned word offset loadable inside the plane allocation
-    uint32_t skip;                // shard prefix bits (see F1)
     uint32_t sparse;              // 1: no per-sub-step barrier (plan: the stage holds a block's survivors)
     unsigned long long* stamps;   // dbg & 256: per-block phase timestamps [nblk2][16]
 };
@@ -274,7 +273,7 @@ __device__ __forceinline__ uint4 f2_load1(const uint32_t* __restrict__ w0, uint3
 // ablation (DHTGPU_DBG & 64).
 constexpr uint32_t kF2Dense = 0, kF2Sparse = 1, kF2Stream = 2;
 
-template <uint32_t Mode, bool Wide>
+template <uint32_t Mode>
 __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     extern __shared__ uint32_t sh[];   // (32 spare) | misc[8] | bm[nwords] | hist[np + 1] | wsum[17] | stage
     const uint32_t np = 1u << a.b1;
@@ -289,9 +288,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     const uint32_t lo = (uint32_t)lo64;
     const uint32_t hi = (uint32_t)(lo64 + a.per_blk < a.n ? lo64 + a.per_blk : a.n);
     const uint32_t lane = lane_id();
-    // level-Lm prefix of (w0 << skip) = bits [32 - skip - Lm, 32 - skip) of w0: one v_bfe
-    // (Wide: skip + Lm > 32, the prefix runs into the zeros shifted in)
-    const uint32_t pre_off = 32 - a.skip - a.Lm;
+    // level-Lm prefix = bits [32 - Lm, 32) of w0: one v_bfe
+    const uint32_t pre_off = 32 - a.Lm;
     const uint32_t lm5 = a.Lm > 5 ? a.Lm - 5 : 0u;   // word index width
     const uint32_t tid4 = 4 * threadIdx.x;
     // the prefix bitmap first (ahead of the ring, its loads land first: measured 1 µs better
@@ -350,9 +348,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
 #pragma unroll
                 for (uint32_t f = 0; f < 4; ++f) {
                     // prefix bit: word pre >> 5 of the bitmap, bit pre & 31 (v_bfe masks it)
-                    const uint32_t pre = Wide ? (v4[f] << a.skip) >> (32 - a.Lm)
-                                              : __builtin_amdgcn_ubfe(v4[f], pre_off, a.Lm);
-                    const uint32_t wi = Wide ? pre >> 5 : __builtin_amdgcn_ubfe(v4[f], pre_off + 5, lm5);
+                    const uint32_t pre = __builtin_amdgcn_ubfe(v4[f], pre_off, a.Lm);
+                    const uint32_t wi = __builtin_amdgcn_ubfe(v4[f], pre_off + 5, lm5);
                     const bool hit = __builtin_amdgcn_ubfe(bm[wi], pre, 1) != 0, in = tid4 + f < rem;
                     sv[f] = hit && in;
                     bal[f] = __builtin_amdgcn_ballot_w64(hit) & __builtin_amdgcn_ballot_w64(in);
@@ -375,7 +372,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                         if (sv[f]) {
                             const uint32_t at = __builtin_amdgcn_mbcnt_hi(
                                 (uint32_t)(bal[f] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[f], pos));
-                            stage[at] = make_uint2(v4[f] << a.skip, j0 + f);
+                            stage[at] = make_uint2(v4[f], j0 + f);
                         }
                         pos += (uint32_t)__popcll(bal[f]);
                     }
@@ -387,7 +384,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                         if (sv[f]) {
                             const uint32_t at = __builtin_amdgcn_mbcnt_hi(
                                 (uint32_t)(bal[f] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[f], pos));
-                            const uint2 e = make_uint2(v4[f] << a.skip, j0 + f);
+                            const uint2 e = make_uint2(v4[f], j0 + f);
                             if (at < a.stage) {
                                 stage[at] = e;
                             } else {
@@ -935,11 +932,26 @@ uint32_t floor_log2(uint64_t x) {
     return r;
 }
 
+// P(X < k) for X ~ Poisson(m)
+double poisson_below(double m, uint32_t k) {
+    double term = std::exp(-m), sum = 0.0;
+    for (uint32_t j = 0; j < k; ++j) {
+        sum += term;
+        term *= m / (double)(j + 1);
+    }
+    return sum;
+}
+
 BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     BatchPlan P;
-    // mark level: about 4k ids per level-Lm subtree
+    // mark level: 4k or more ids per level-Lm subtree -- or one level finer (2k..4k) when, on
+    // uniform ids, fewer than 0.01 of the q targets are expected to land in a subtree with
+    // under k ids (those go to the F4 brute force).  Without the finer step a prefix shard
+    // just under a power of two (n = 2^24 - few) would mark at half the resolution and
+    // double the survivors.
     const uint64_t per = 4ull * k;
     P.Lm = n >= per ? floor_log2(n / per) : 0;
+    if (n >= per && P.Lm < kMaxLm && poisson_below((double)n / (double)(1ull << (P.Lm + 1)), k) * q <= 0.01) ++P.Lm;
     if (P.Lm > kMaxLm) P.Lm = kMaxLm;
     // survivors on uniform ids: n (1 - exp(-q / 2^Lm)); partitions of about kF3Cap / 2
     const double f = 1.0 - std::exp(-(double)q / (double)(1ull << P.Lm));
@@ -1035,10 +1047,23 @@ hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t k, 
     return e;
 }
 
+__global__ void k_shift_w0(const uint32_t* __restrict__ planes, uint64_t stride, uint32_t shift,
+                           uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < stride) out[i] = (planes[i] << shift) | (planes[stride + i] >> (32 - shift));
+}
+
+hipError_t launch_shift_w0(const uint32_t* planes, uint64_t stride, uint32_t shift, uint32_t* out, hipStream_t s) {
+    if (shift == 0 || shift >= 32) return hipErrorInvalidValue;
+    k_shift_w0<<<dim3((uint32_t)((stride + 255) / 256)), dim3(256), 0, s>>>(planes, stride, shift, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp,
                              uint64_t ts, uint32_t q, uint32_t k, const uint32_t* gidx, uint32_t base,
-                             uint32_t* out_idx, uint32_t* out_cnt, int num_cus, uint32_t skip, uint32_t pval,
-                             hipStream_t s, hipEvent_t* ev) {
+                             uint32_t* out_idx, uint32_t* out_cnt, int num_cus, uint32_t skip,
+                             const uint32_t* w0s, hipStream_t s, hipEvent_t* ev) {
+    if (skip && !w0s) return hipErrorInvalidValue;
     if (!q) return hipSuccess;
     const BatchPlan P = plan_batch(n, q, k, num_cus);
     const uint32_t np = 1u << P.b1;
@@ -1061,9 +1086,8 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
     uint2* pbuf = reinterpret_cast<uint2*>(take((size_t)np * kF3Cap * 8));
     static bool attr_set = false;
     if (!attr_set) {
-        const void* f2s[] = {(const void*)k_f2_filter<kF2Dense, false>, (const void*)k_f2_filter<kF2Sparse, false>,
-                             (const void*)k_f2_filter<kF2Stream, false>, (const void*)k_f2_filter<kF2Dense, true>,
-                             (const void*)k_f2_filter<kF2Sparse, true>};
+        const void* f2s[] = {(const void*)k_f2_filter<kF2Dense>, (const void*)k_f2_filter<kF2Sparse>,
+                             (const void*)k_f2_filter<kF2Stream>};
         for (const void* f : f2s) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
         const void* f3s[] = {(const void*)k_f3_answer<8, false, true>,  (const void*)k_f3_answer<16, false, true>,
                              (const void*)k_f3_answer<32, false, true>, (const void*)k_f3_answer<8, true, true>,
@@ -1084,19 +1108,19 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
     static unsigned long long* stamps = nullptr;   // dbg & 256: F3 [8192][16] then F2 [8192][16]
     if ((dbg & 256) && !stamps) (void)hipMalloc(&stamps, (size_t)2 * 8192 * 16 * 8);
     if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)2 * 8192 * 16 * 8, s);
-    go(0, k_f1_targets, dim3(P.nblk1), dim3(kF1Threads), 0, tp, q, P.Lm, P.b1, skip, pval, bitmap, tcount, tbuf, P.tcap, ctr,
-       tspill);
+    go(0, k_f1_targets, dim3(P.nblk1), dim3(kF1Threads), 0, tp, tp + ts, q, P.Lm, P.b1, skip, bitmap, tcount, tbuf,
+       P.tcap, ctr, tspill);
     if (n) {
-        F2Args a2{planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, kF3Cap, ctr, P.stage, dbg,
-                  (uint32_t)(5 * stride - 4 < 0xFFFFFFF0ull ? 5 * stride - 4 : 0xFFFFFFF0ull), skip, P.sparse,
+        // F2 streams word 0, or the shifted word-0 plane of a prefix shard (stride words)
+        const uint64_t lim = (w0s ? stride : 5 * stride) - 4;
+        F2Args a2{w0s ? w0s : planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, kF3Cap, ctr, P.stage, dbg,
+                  (uint32_t)(lim < 0xFFFFFFF0ull ? lim : 0xFFFFFFF0ull), P.sparse,
                   stamps ? stamps + 8192 * 16 : nullptr};
         const dim3 g2(P.nblk2), b2(kF2Threads);
         const size_t l2 = f2_lds(P);
-        if (dbg & 64) go(1, k_f2_filter<kF2Stream, false>, g2, b2, l2, a2);
-        else if (skip + P.Lm > 32 && P.sparse) go(1, k_f2_filter<kF2Sparse, true>, g2, b2, l2, a2);
-        else if (skip + P.Lm > 32) go(1, k_f2_filter<kF2Dense, true>, g2, b2, l2, a2);
-        else if (P.sparse) go(1, k_f2_filter<kF2Sparse, false>, g2, b2, l2, a2);
-        else go(1, k_f2_filter<kF2Dense, false>, g2, b2, l2, a2);
+        if (dbg & 64) go(1, k_f2_filter<kF2Stream>, g2, b2, l2, a2);
+        else if (P.sparse) go(1, k_f2_filter<kF2Sparse>, g2, b2, l2, a2);
+        else go(1, k_f2_filter<kF2Dense>, g2, b2, l2, a2);
     } else if (ev) {
         (void)hipEventRecord(ev[2], s);
         (void)hipEventRecord(ev[3], s);

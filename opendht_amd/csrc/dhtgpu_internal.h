@@ -92,10 +92,12 @@ size_t batch_clean_bytes();
 // stats4 = {fallback targets, survivors, wave-path targets, 0} of the last call (synchronises s)
 hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t* stats4,
                             hipStream_t s);
+// prefix shards: out[i] = planes word 0 << shift | word 1 >> (32 - shift), i < stride
+hipError_t launch_shift_w0(const uint32_t* planes, uint64_t stride, uint32_t shift, uint32_t* out, hipStream_t s);
 hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp,
                              uint64_t ts, uint32_t q, uint32_t k, const uint32_t* gidx, uint32_t base,
-                             uint32_t* out_idx, uint32_t* out_cnt, int num_cus, uint32_t skip, uint32_t pval,
-                             hipStream_t s, hipEvent_t* ev = nullptr);
+                             uint32_t* out_idx, uint32_t* out_cnt, int num_cus, uint32_t skip,
+                             const uint32_t* w0s, hipStream_t s, hipEvent_t* ev = nullptr);
 
 // wire.hip: NetworkEngine::bufferNodes / deserializeNodes (compact node records)
 hipError_t launch_wire_encode(const uint32_t* planes, uint64_t stride, const uint8_t* tail, uint32_t alen,

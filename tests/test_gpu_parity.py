@@ -255,14 +255,48 @@ def test_prefix_shard_matches_global_topk(ctx, pbits, pval):
         got, cnt = fn(mine, 8)
         assert np.array_equal(cnt, wcnt) and np.array_equal(got, want)
     if pbits:
-        # targets of other prefixes: the shard's own top-k (K6 answers them by brute force)
+        # targets of other prefixes: the shard's own top-k (K6 answers them in the shifted
+        # word-0 space like its own targets), alone and mixed into one batch with its own
         other = tg[top(tg) != pval][:200]
         gl = np.nonzero(top(ids) == pval)[0].astype(np.uint32)
-        w2, c2 = O.topk(shard, other, 8)
-        w2 = np.where(w2 == 0xFFFFFFFF, w2, gl[np.minimum(w2, gl.size - 1)])
-        for fn in (ctx.topk, ctx.batch_topk):
-            got, cnt = fn(other, 8)
-            assert np.array_equal(cnt, c2) and np.array_equal(got, w2)
+        for tset in (other, tg):
+            w2, c2 = O.topk(shard, tset, 8)
+            w2 = np.where(w2 == 0xFFFFFFFF, w2, gl[np.minimum(w2, gl.size - 1)])
+            for fn in (ctx.topk, ctx.batch_topk):
+                got, cnt = fn(tset, 8)
+                assert np.array_equal(cnt, c2) and np.array_equal(got, w2)
+
+
+@pytest.mark.parametrize("pbits,pval", [(1, 0), (3, 6)])
+def test_prefix_shard_weak_shape(ctx, pbits, pval):
+    """The weak-scaling bench shape: rank pval of 2^pbits holds its prefix shard of a 2^24
+    id stream (just under 2^(24 - pbits) ids: K6 marks at the finer level) and answers its
+    own targets plus foreign ones; K6 == K1 scan on the whole batch, oracle on a sample."""
+    n = 1 << 24
+    ctx.gen_ids_prefix(4242, n, pbits, pval)
+    m = ctx.num_ids
+    tg = O.gen_ids(4243, 65536 >> pbits)
+    tg[: tg.shape[0] - 64, 0] = (tg[: tg.shape[0] - 64, 0] & (0xFF >> pbits)) | (pval << (8 - pbits))
+    got, cnt = ctx.batch_topk(tg, 8)
+    sc, scnt = ctx.topk(tg, 8)
+    assert np.array_equal(cnt, scnt) and np.array_equal(got, sc)
+    assert np.all(cnt == 8)
+    ids = O.gen_ids(4242, n)
+    top = ids[:, 0].astype(np.uint32) >> (8 - pbits)
+    gl = np.nonzero(top == pval)[0].astype(np.uint32)
+    assert gl.size == m
+    sample = np.r_[np.arange(0, tg.shape[0] - 64, 997), np.arange(tg.shape[0] - 64, tg.shape[0])]
+    want, wcnt = O.topk(ids[gl], tg[sample], 8)
+    assert np.array_equal(cnt[sample], wcnt) and np.array_equal(got[sample], gl[want])
+    # shard-local result indices (what a rank owning its shard's node table keeps)
+    ctx.set_global_indices(False)
+    try:
+        loc, lcnt = ctx.batch_topk(tg, 8)
+        sl, slcnt = ctx.topk(tg, 8)
+    finally:
+        ctx.set_global_indices(True)
+    assert np.array_equal(lcnt, cnt) and np.array_equal(slcnt, cnt)
+    assert np.array_equal(gl[loc], got) and np.array_equal(sl, loc)
 
 
 def test_select_prefix_dev(ctx):
