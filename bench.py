@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--scaling", choices=["auto", "weak", "strong"], default="auto",
                     help="weak: --n/--q per GPU (global problem grows with N); strong: --n/--q global. "
                          "auto = weak for the prefix route, strong for broadcast")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="multi-rank correctness rehearsal on a one-GPU box: every rank on cuda:0, gloo "
+                         "process group (timings are contended; not a scaling measurement)")
     ap.add_argument("--sharded", action="store_true",
                     help="use the multi-GPU code path (and its collectives) even with one rank")
     ap.add_argument("--simulate-world", type=int, default=0,
@@ -136,6 +139,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.rehearse_one_gpu:
+        local = 0
     pow2 = lambda g: g > 0 and (g & (g - 1)) == 0
     route = a.route
     if route == "auto":
@@ -154,7 +159,10 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     tstream = torch.cuda.Stream(dev)              # every kernel and event of the bench runs here
