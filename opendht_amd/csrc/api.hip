@@ -254,6 +254,11 @@ int dhtgpu_gen_ids_prefix(dhtgpu_ctx* c, uint64_t seed, uint64_t start, uint64_t
                                  c->gidx.as<uint32_t>(), start, c->stream));
     r = finish_ids(c, m);
     if (r) return r;
+    // the generation scratch (20 B per id of the whole stream) is not kept: a device may
+    // hold several shard contexts of one large stream
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    if (c->staging.cap > ((size_t)1 << 28)) c->staging.release();
+    if (c->aux.cap > ((size_t)1 << 28)) c->aux.release();
     c->has_gidx = true;
     if (pbits) {
         DHT_TRY(c->w0s.ensure((size_t)c->stride * 4));

@@ -921,6 +921,7 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_fallback(F3Args a, uint32_t n
 
 struct BatchPlan {
     uint32_t Lm, b1, Lq, nwords, nblk1, nblk2, stage, sparse, tcap;
+    bool fits;   // partitions' survivors fit the F3 stage on uniform ids
     uint64_t per_blk;
 };
 
@@ -960,6 +961,18 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     while (b1 < P.Lm && surv / (double)(1ull << b1) > kF3Cap / 2) ++b1;
     if (P.Lm > kMaxSubBits && b1 < P.Lm - kMaxSubBits) b1 = P.Lm - kMaxSubBits;
     if (b1 > 13) b1 = 13;   // kMaxParts
+    // a partition's survivors come in whole level-Lm subtrees (n / 2^Lm ids each, marked
+    // with probability f): on uniform ids mean s f mu, variance s f (1 - f) mu^2 + s f mu
+    // over its s = 2^(Lm - b1) subtrees.  Split further until mean + 6 sigma fits the F3
+    // stage (an overflowing partition sends its targets to the brute force); plans that
+    // cannot are refused (batch_supported), e.g. n >> 2^24 with its 256-id subtrees.
+    P.fits = false;
+    for (;; ++b1) {
+        const double sub = (double)(1ull << (P.Lm - b1)), mu = (double)n / (double)(1ull << P.Lm);
+        const double mean = sub * f * mu, var = sub * f * (1.0 - f) * mu * mu + sub * f * mu;
+        if (mean + 6.0 * std::sqrt(var) + 64.0 <= (double)kF3Cap) { P.fits = true; break; }
+        if (b1 >= 13 || b1 >= P.Lm) break;
+    }
     P.b1 = b1;
     // F3 sorts by up to 1 bit below the mark level (finer candidate ranges), <= 4096 bins
     P.Lq = P.Lm + 1 < 32 ? P.Lm + 1 : 32;
@@ -1010,7 +1023,8 @@ bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     if (k == 0 || k > DHTGPU_MAX_K_DEV || n >= (1ull << 31)) return false;
     const BatchPlan P = plan_batch(n, q, k, num_cus);
     if (q > kMaxQ) return false;
-    if (P.Lm - P.b1 > 13 || P.stage < 2 * kF2Sub) return false;
+    // dense mode flushes whenever less than one sub-step of room is left
+    if (!P.fits || P.Lm - P.b1 > 13 || (!P.sparse && P.stage < kF2Sub + 1024)) return false;
     return f3_lds(P) <= kLdsMax && f2_lds(P) <= kLdsMax;
 }
 

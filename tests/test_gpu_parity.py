@@ -299,6 +299,22 @@ def test_prefix_shard_weak_shape(ctx, pbits, pval):
     assert np.array_equal(gl[loc], got) and np.array_equal(sl, loc)
 
 
+def test_batch_refuses_unsafe_plan(ctx):
+    """n = 2^27 with 131,072 targets: the level-19 subtrees hold 256 ids, so a partition's
+    survivors would overflow the F3 stage on uniform ids; K6 refuses the plan (ERANGE)
+    instead of sending thousands of targets to the brute force.  Split into prefix
+    sub-shards (bench --sub-shards, cfg 3) each part is planned normally."""
+    import opendht_amd
+    ctx.gen_ids(777, 1 << 27)
+    tg = O.gen_ids(778, 131072)
+    with pytest.raises(opendht_amd.DhtGpuError) as ei:
+        ctx.batch_topk(tg, 8)
+    assert ei.value.code == -6
+    idx, cnt = ctx.batch_topk(tg[:16], 8)   # a small batch plans fine (few marked subtrees)
+    want, wcnt = O.topk(O.gen_ids(777, 1 << 27), tg[:16], 8)
+    assert np.array_equal(cnt, wcnt) and np.array_equal(idx, want)
+
+
 def test_select_prefix_dev(ctx):
     import torch
     n, stride = 50000, 50048
