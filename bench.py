@@ -67,8 +67,8 @@ OPS_PER_PAIR = 1.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=1000)   # ~41 ms timed: steady state, not ramp-up
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--n", type=int, default=1 << 24, help="node ids (total over all ranks)")
     ap.add_argument("--q", type=int, default=65536, help="targets per step (total over all ranks)")
     ap.add_argument("--k", type=int, default=8)
