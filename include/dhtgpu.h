@@ -50,7 +50,7 @@ enum {
     DHTGPU_ENOMEM = -2,              /* device allocation failed */
     DHTGPU_EDEVICE = -3,             /* HIP runtime / kernel launch error */
     DHTGPU_ENOIDS = -4,              /* no id set uploaded */
-    DHTGPU_EUNSORTED = -5,           /* cached_nodes needs a lexicographically sorted, unique id set */
+    DHTGPU_EUNSORTED = -5,           /* cached_nodes / cache_set: the id set holds duplicate ids */
     DHTGPU_ERANGE = -6               /* size out of range (e.g. more than 2^32-1 ids) */
 };
 
@@ -148,20 +148,28 @@ int dhtgpu_index_topk(dhtgpu_ctx* ctx, const uint8_t* targets20_be, uint32_t q, 
 /* Nothing persists between calls: each call streams the id word plane w0 once, keeps only
  * the ids that share the batch targets' level-Lm prefixes (Lm ~ log2(n / 4k)), and answers
  * every target from its complete prefix subtree in LDS; targets whose subtree holds fewer
- * than min(k, n) ids take an exact brute-force pass.  Same output forms as
- * dhtgpu_topk_dev.  DHTGPU_ERANGE when n >= 2^31 or q > 2^22 (use dhtgpu_index_topk_dev).
- * Stream-ordered, no host sync.  A context keeps four workspaces used in turn, so up to four
- * consecutive calls issued on different streams run concurrently (one batch's
- * latency-bound answer phase overlaps the next batch's HBM-bound id stream); a call that
- * reuses a workspace last used on another stream first waits for that stream. */
+ * than min(k, n) ids, or whose partition overflows (clustered ids), are answered by the K1
+ * scan over all ids inside the same call.  Same output forms as dhtgpu_topk_dev.
+ * Large sets (n > 2^24 where one plan cannot cover the batch, e.g. the 2^27-id cfg-3 shard at
+ * 131,072 targets): the set is split once into 2^s prefix sub-partitions of <= 2^24 ids (built
+ * on the first such call, kept until the set changes: 28 B/id of extra HBM) and every call runs
+ * one K6 pass per sub-partition, each answering the targets of its prefix; a sub-partition
+ * with fewer than k ids sends its targets to the K1 scan over the whole set.
+ * DHTGPU_ERANGE only when q > 2^22 (or n >= 2^32).
+ * Stream-ordered, no host sync (except the one-time sub-partition build).  A context keeps four
+ * workspaces used in turn, so up to four consecutive calls issued on different streams run
+ * concurrently (one batch's latency-bound answer phase overlaps the next batch's HBM-bound id
+ * stream); a call that reuses a workspace last used on another stream first waits for that
+ * stream.  Sub-partitioned calls fork onto two context-internal streams and join back. */
 int dhtgpu_batch_topk_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
                           uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec,
                           uint32_t idx_base, void* stream);
 /* Diagnostics: the same call with a start/stop HIP event pair recorded by each kernel's own
  * dispatch; synchronises and returns per-kernel device milliseconds ms4 = {F1 bucket
- * targets, F2 filter ids, F3 answer, F4 ties + fallback} and (nullable) stats4 = {targets
- * answered by the brute-force fallback, surviving ids, targets answered by an exact wave
- * (w0 ties, large subtrees), 0}. */
+ * targets, F2 filter ids, F3 answer, F4 ties + fallback scan} and (nullable) stats4 =
+ * {targets answered by the fallback scan, surviving ids, targets answered by an exact wave
+ * (w0 ties, large subtrees), 0}.  Sub-partitioned calls: the kernels and statistics of
+ * sub-partition 0. */
 int dhtgpu_batch_topk_timed(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
                             uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, void* stream, float* ms4,
                             uint32_t* stats4);
@@ -190,11 +198,27 @@ int dhtgpu_classify_dev(const uint32_t* planes, uint64_t stride, uint64_t n, uin
                         const uint32_t* myid_words /* host, 5 words */, uint8_t* out_bucket,
                         unsigned long long* d_hist161, void* stream);
 
-/* ---- a8: NodeCache::getCachedNodes walk over the context's (sorted) id set ------- */
+/* ---- a8: NodeCache::getCachedNodes walk over the context's id set --------------------- */
 /* accept[n] (nullable = all) = lock() && !isExpired() && !isClient().  Output in
- * the reference's walk order (not sorted), indices into the id set. */
+ * the reference's walk order (not sorted), indices into the id set.  An id set uploaded
+ * unsorted is sorted on the device on the first call (f2: LSD radix over the 160-bit keys,
+ * kept until the set changes); DHTGPU_EUNSORTED if it holds duplicate ids. */
 int dhtgpu_cached_nodes(dhtgpu_ctx* ctx, const uint8_t* accept, const uint8_t* targets20_be,
                         uint32_t q, uint32_t count, uint32_t* out_idx, uint32_t* out_cnt);
+
+/* ---- f2: the NodeCache mirror (a second, context-private id set) ------------------------ */
+/* NodeCache::NodeMap (include/opendht/node_cache.h:43: std::map<InfoHash, weak_ptr<Node>>,
+ * src/node_cache.cpp:42-74) as n unique 20-byte keys in the CALLER's order (e.g. a walk of
+ * the map, or any order): sorted lexicographically on the device; it does not touch the
+ * context's k-NN id set.  version != 0 equal to the last upload's (same n) skips the upload:
+ * the caller bumps it whenever the map changes.  DHTGPU_EUNSORTED on duplicate keys. */
+int dhtgpu_cache_set(dhtgpu_ctx* ctx, const uint8_t* ids20, uint64_t n, uint64_t version);
+/* getCachedNodes(target, af, count) for q targets over the mirror: accept[n] (nullable) and
+ * the output indices are in the caller's order of the last dhtgpu_cache_set. */
+int dhtgpu_cache_nodes(dhtgpu_ctx* ctx, const uint8_t* accept, const uint8_t* targets20_be, uint32_t q,
+                       uint32_t count, uint32_t* out_idx, uint32_t* out_cnt);
+/* The mirror's lexicographic order: perm[j] = caller index of the j-th smallest key. */
+int dhtgpu_cache_sorted(dhtgpu_ctx* ctx, uint32_t* perm);
 
 /* ---- a6: RoutingTable::depth (src/routing_table.cpp:100-107) over a table snapshot ---- */
 /* *out_depth = max(lowbit(first[b]), lowbit(first[b+1])) + 1 (0 for an empty table);
@@ -208,12 +232,19 @@ int dhtgpu_table_depth(uint32_t nb, const uint8_t* firsts20, uint32_t b, uint32_
  * SEND_NODES = 8 are kept and written as 26-byte (af 4) / 38-byte (af 6) records
  * id || address || port to out[qi * 8 * rec ..]; out_len[qi] = bytes written.
  * node_tail[i*(alen+2)] = node i's address || port bytes as its sockaddr holds them
- * (network order), alen = 4 / 16.  Equal ids (never in OpenDHT) keep candidate order. */
+ * (network order), alen = 4 / 16.  Equal ids (never in OpenDHT) keep candidate order.
+ * Every candidate must be DHTGPU_NONE or < the number of ids: the host form returns
+ * DHTGPU_EINVAL otherwise; the _dev form does not check (device pointers). */
 int dhtgpu_buffer_nodes_dev(dhtgpu_ctx* ctx, const uint8_t* node_tail, uint32_t af, const uint32_t* t_planes,
                             uint64_t t_stride, uint32_t q, const uint32_t* cand, uint32_t c, uint8_t* out,
                             uint32_t* out_len, void* stream);
 int dhtgpu_buffer_nodes(dhtgpu_ctx* ctx, const uint8_t* node_tail, uint32_t af, const uint8_t* targets20,
                         uint32_t q, const uint32_t* cand, uint32_t c, uint8_t* out, uint32_t* out_len);
+/* The same over the caller's own nodes: cand indexes node_ids20[nn * 20] / node_tail (the
+ * context's id set is not used or changed). */
+int dhtgpu_buffer_nodes_ids(dhtgpu_ctx* ctx, const uint8_t* node_ids20, const uint8_t* node_tail, uint32_t nn,
+                            uint32_t af, const uint8_t* targets20, uint32_t q, const uint32_t* cand, uint32_t c,
+                            uint8_t* out, uint32_t* out_len);
 /* NetworkEngine::deserializeNodes (src/network_engine.cpp:849-887), batched over m received
  * n4 (af 4) / n6 (af 6) blobs: message i is blob[msg_off[i] .. msg_off[i+1]), received from
  * from_addr[i*16 ..] (family from_af[i]: 4, 6 or 0).  msg_status[i] = 1 when its length is

@@ -62,6 +62,8 @@ public:
     Context(const Context&) = delete;
     Context& operator=(const Context&) = delete;
     dhtgpu_ctx* get() const { return ctx_; }
+    uint64_t cache_version_ = 0;   // NodeCache mirror: version and size of the last upload
+    size_t cache_size_ = 0;
 private:
     dhtgpu_ctx* ctx_;
 };
@@ -131,40 +133,50 @@ findClosestNodes(Context& ctx, const Table& table, const HashT& id, TimePoint no
     return std::move(findClosestNodesBatch(ctx, table, &id, 1, now, count)[0]);
 }
 
-/* Drop-in for NodeCache::getCachedNodes over one address family's map
- * (std::map<InfoHash, std::weak_ptr<Node>>, already lexicographically sorted).
- * Accepted = lock() succeeds && !isExpired() && !isClient(); walk order preserved. */
+/* NodeCache::getCachedNodes over one address family's map (std::map<InfoHash, weak_ptr<Node>>,
+ * include/opendht/node_cache.h:43, src/node_cache.cpp:42-74), batched.  The map's keys go to
+ * the context's NodeCache mirror (dhtgpu_cache_set: a set of its own, sorted on the device --
+ * the context's k-NN id set is not touched); `version` != 0 equal to the previous call's skips
+ * that upload (the caller bumps it whenever the map changes).  Accepted = lock() succeeds &&
+ * !isExpired() && !isClient(), evaluated at call time; walk order preserved. */
 template <class NodeMap, class HashT>
 void getCachedNodesRaw(Context& ctx, const NodeMap& map, const HashT* targets, size_t q, size_t count,
-                  std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>>& locked,
-                  std::vector<std::vector<uint32_t>>& out) {
+                       std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>>& locked,
+                       std::vector<std::vector<uint32_t>>& out, uint64_t version = 0) {
     std::vector<uint8_t> ids, accept;
-    ids.reserve(map.size() * DHTGPU_HASH_LEN);
+    const bool upload = version == 0 || version != ctx.cache_version_ || map.size() != ctx.cache_size_;
+    if (upload) ids.reserve(map.size() * DHTGPU_HASH_LEN);
     locked.clear();
+    accept.reserve(map.size());
     for (const auto& kv : map) {
-        detail::put_id(ids, kv.first);
+        if (upload) detail::put_id(ids, kv.first);
         auto n = kv.second.lock();
         accept.push_back(n && !n->isExpired() && !n->isClient() ? 1 : 0);
         locked.push_back(n);
     }
-    check(dhtgpu_set_ids(ctx.get(), ids.empty() ? nullptr : ids.data(), map.size()), "set_ids");
+    if (upload) {
+        check(dhtgpu_cache_set(ctx.get(), ids.empty() ? nullptr : ids.data(), map.size(), version), "cache_set");
+        ctx.cache_version_ = version;
+        ctx.cache_size_ = map.size();
+    }
     std::vector<uint8_t> t;
     for (size_t i = 0; i < q; ++i) detail::put_id(t, targets[i]);
     std::vector<uint32_t> idx(q * count), cnt(q);
     out.assign(q, std::vector<uint32_t>());
     if (q == 0) return;
-    check(dhtgpu_cached_nodes(ctx.get(), accept.empty() ? nullptr : accept.data(), t.data(), (uint32_t)q,
-                              (uint32_t)count, idx.data(), cnt.data()),
-          "cached_nodes");
+    check(dhtgpu_cache_nodes(ctx.get(), accept.empty() ? nullptr : accept.data(), t.data(), (uint32_t)q,
+                             (uint32_t)count, idx.data(), cnt.data()),
+          "cache_nodes");
     for (size_t i = 0; i < q; ++i) out[i].assign(idx.begin() + i * count, idx.begin() + i * count + cnt[i]);
 }
 
+/* Drop-in for NodeCache::getCachedNodes(id, af, count). */
 template <class NodeMap, class HashT>
 std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>>
-getCachedNodes(Context& ctx, const NodeMap& map, const HashT& id, size_t count) {
+getCachedNodes(Context& ctx, const NodeMap& map, const HashT& id, size_t count, uint64_t version = 0) {
     std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>> locked, res;
     std::vector<std::vector<uint32_t>> out;
-    getCachedNodesRaw(ctx, map, &id, 1, count, locked, out);
+    getCachedNodesRaw(ctx, map, &id, 1, count, locked, out, version);
     for (uint32_t i : out[0]) res.push_back(locked[i]);
     return res;
 }
@@ -190,7 +202,8 @@ public:
         std::vector<uint32_t> idx(q * k), cnt(q);
         std::vector<std::vector<uint32_t>> res(q);
         if (q == 0) return res;
-        // K6 per-batch prefix filter; the K1 streaming scan where K6's limits are exceeded
+        // K6 per-batch prefix filter (large sets run over prefix sub-partitions inside the
+        // library); the K1 streaming scan where K6's limits are exceeded (q > 2^22)
         int rc = dhtgpu_batch_topk(ctx_.get(), t.data(), (uint32_t)q, (uint32_t)k, idx.data(), cnt.data());
         if (rc == DHTGPU_ERANGE) rc = dhtgpu_topk(ctx_.get(), t.data(), (uint32_t)q, (uint32_t)k, idx.data(), cnt.data());
         check(rc, "topk");
@@ -241,11 +254,12 @@ std::vector<std::vector<uint8_t>> bufferNodesBatch(Context& ctx, int af_inet6, c
             cand[i * c + j] = n;
         }
     }
-    check(dhtgpu_set_ids(ctx.get(), ids.empty() ? nullptr : ids.data(), n), "set_ids");
     std::vector<uint8_t> out(q * 8 * rec);
     std::vector<uint32_t> len(q);
-    check(dhtgpu_buffer_nodes(ctx.get(), tail.empty() ? nullptr : tail.data(), af_inet6 ? 6u : 4u, t.data(),
-                              (uint32_t)q, cand.data(), (uint32_t)c, out.data(), len.data()),
+    // the candidates' own ids (the context's k-NN id set is not touched)
+    check(dhtgpu_buffer_nodes_ids(ctx.get(), ids.empty() ? nullptr : ids.data(), tail.empty() ? nullptr : tail.data(), n,
+                                  af_inet6 ? 6u : 4u, t.data(), (uint32_t)q, cand.data(), (uint32_t)c, out.data(),
+                                  len.data()),
           "buffer_nodes");
     for (size_t i = 0; i < q; ++i) res[i].assign(out.begin() + i * 8 * rec, out.begin() + i * 8 * rec + len[i]);
     return res;

@@ -10,6 +10,7 @@ Reference interfaces mirrored (OpenDHT tree paths):
   Context.topk            std::partial_sort(.., InfoHash::xorCmp)  (include/opendht/infohash.h:179-194)
   Context.find_closest    RoutingTable::findClosestNodes            (src/routing_table.cpp:110-150)
   Context.cached_nodes    NodeCache::getCachedNodes                 (src/node_cache.cpp:42-74)
+  Context.cache_set/_nodes  the NodeCache mirror: unsorted keys sorted on the device (node_cache.h:43)
   Context.classify        RoutingTable::findBucket + InfoHash::commonBits
 """
 import ctypes
@@ -81,6 +82,11 @@ def lib():
                                  _vp], ctypes.c_int),
         "dhtgpu_cached_nodes": ([_vp, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p],
                                 ctypes.c_int),
+        "dhtgpu_cache_set": ([_vp, _u8p, ctypes.c_uint64, ctypes.c_uint64], ctypes.c_int),
+        "dhtgpu_cache_nodes": ([_vp, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p], ctypes.c_int),
+        "dhtgpu_cache_sorted": ([_vp, _u32p], ctypes.c_int),
+        "dhtgpu_buffer_nodes_ids": ([_vp, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_uint32, _u32p,
+                                     ctypes.c_uint32, _u8p, _u32p], ctypes.c_int),
         "dhtgpu_index_build": ([_vp, _vp], ctypes.c_int),
         "dhtgpu_index_topk_dev": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp,
                                    ctypes.c_uint32, _vp], ctypes.c_int),
@@ -126,7 +132,8 @@ def exported_symbols():
             "dhtgpu_index_build_timed", "dhtgpu_gen_ids_prefix", "dhtgpu_select_prefix_dev",
             "dhtgpu_batch_topk_dev", "dhtgpu_batch_topk_timed", "dhtgpu_batch_topk", "dhtgpu_table_depth",
             "dhtgpu_buffer_nodes_dev", "dhtgpu_buffer_nodes", "dhtgpu_deserialize_nodes", "dhtgpu_net_prepare",
-            "dhtgpu_search_batch", "dhtgpu_search_batch_dev", "dhtgpu_set_global_indices"]
+            "dhtgpu_search_batch", "dhtgpu_search_batch_dev", "dhtgpu_set_global_indices", "dhtgpu_cache_set",
+            "dhtgpu_cache_nodes", "dhtgpu_cache_sorted", "dhtgpu_buffer_nodes_ids"]
 
 
 def _ids(a, name="ids"):
@@ -380,6 +387,52 @@ class Context:
         _check(lib().dhtgpu_cached_nodes(self._h, _p(acc, _u8p) if acc is not None else None, _p(t, _u8p), q,
                                          count, _p(out, _u32p), _p(cnt, _u32p)), "cached_nodes")
         return out, cnt
+
+
+    # ---- f2: the NodeCache mirror (a second id set, sorted on the device) ----------------
+    def cache_set(self, ids, version=0):
+        """Upload NodeCache map keys in any order (unique); version != 0 equal to the last
+        upload's skips the upload."""
+        ids = _ids(ids)
+        _check(lib().dhtgpu_cache_set(self._h, _p(ids, _u8p), ids.shape[0], int(version)), "cache_set")
+        self._cache_n = ids.shape[0]
+
+    def cache_nodes(self, targets, count=14, accept=None):
+        """getCachedNodes over the mirror: (q, count) caller-order indices (NONE padded), (q,) counts."""
+        t = _ids(targets, "targets")
+        q = t.shape[0]
+        out = np.empty((q, count), dtype=np.uint32)
+        cnt = np.empty(q, dtype=np.uint32)
+        acc = None
+        if accept is not None:
+            acc = np.ascontiguousarray(accept, dtype=np.uint8)
+            if acc.shape[0] != getattr(self, "_cache_n", acc.shape[0]):
+                raise ValueError("accept mask must have one byte per cache key")
+        _check(lib().dhtgpu_cache_nodes(self._h, _p(acc, _u8p) if acc is not None else None, _p(t, _u8p), q, count,
+                                        _p(out, _u32p), _p(cnt, _u32p)), "cache_nodes")
+        return out, cnt
+
+    def cache_sorted(self):
+        """The mirror's lexicographic order as caller indices."""
+        perm = np.empty(max(getattr(self, "_cache_n", 0), 1), dtype=np.uint32)
+        _check(lib().dhtgpu_cache_sorted(self._h, _p(perm, _u32p)), "cache_sorted")
+        return perm[: getattr(self, "_cache_n", 0)]
+
+    def buffer_nodes_ids(self, node_ids, node_tail, af, targets, cand):
+        """bufferNodes over the caller's own nodes (the context's id set is not used)."""
+        t = _ids(targets, "targets")
+        q = t.shape[0]
+        nodes = _ids(node_ids, "node_ids")
+        cand = np.ascontiguousarray(cand, dtype=np.uint32).reshape(q, -1)
+        alen = 4 if af == 4 else 16
+        tail = np.ascontiguousarray(node_tail, dtype=np.uint8).reshape(-1, alen + 2)
+        rec = 20 + alen + 2
+        out = np.zeros((q, 8 * rec), dtype=np.uint8)
+        ln = np.zeros(q, dtype=np.uint32)
+        _check(lib().dhtgpu_buffer_nodes_ids(self._h, _p(nodes, _u8p), _p(tail, _u8p), nodes.shape[0], af,
+                                             _p(t, _u8p), q, _p(cand, _u32p), cand.shape[1], _p(out, _u8p),
+                                             _p(ln, _u32p)), "buffer_nodes_ids")
+        return out, ln
 
 
 def table_depth(firsts, b):

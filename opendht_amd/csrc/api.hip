@@ -93,8 +93,44 @@ struct dhtgpu_ctx {
     static constexpr int kBatchDepth = 4;
     BatchSlot bslot[kBatchDepth];
     int bnext = 0, blast = 0;
+    // Prefix sub-partitions of a large id set (built on the first K6 call K6 cannot plan in
+    // one piece, e.g. the 2^27-id cfg-3 shard): the ids whose next sub_bits bits (after the
+    // shard's own prefix) equal i, compacted in order, with their shifted word-0 plane; each
+    // K6 call then runs one sub-call per sub-partition on the two internal streams.
+    struct SubPart {
+        DevBuf planes, map, gmap, w0s;   // planes: 5 * stride u32; map: sub -> ctx-local; gmap: sub -> global
+        uint64_t n = 0, stride = 0;
+    };
+    std::vector<SubPart> subs;
+    uint32_t sub_bits = 0;
+    bool subs_valid = false;
+    DevBuf sub_mask, sub_list, sub_scratch;   // deficient / unplannable sub-partitions: routed to the scan
+    bool sub_scratch_clean = false;
+    hipStream_t side[2] = {nullptr, nullptr};  // internal streams for sub-calls
+    hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+    uint32_t shard_pval = 0;
+    // lexicographically sorted views (sort.hip): of the main set when it was uploaded unsorted
+    // (built on the first cached_nodes call), and the NodeCache mirror (dhtgpu_cache_set)
+    struct SortedSet {
+        DevBuf planes, perm;
+        uint64_t n = 0, stride = 0;
+        bool valid = false, unique = true;
+    };
+    SortedSet sview, cache;
+    uint64_t cache_version = 0;
+    DevBuf cache_in, sort_scratch, cache_acc;
+    // diagnostics (DHTGPU_DBG, read once at creation; phase stamps per context)
+    uint32_t dbg = 0;
+    DevBuf stamps;
 
     hipError_t bind() { return hipSetDevice(device); }
+    void invalidate_subs() {
+        subs_valid = false;
+        for (auto& sp : subs)
+            for (DevBuf* b : {&sp.planes, &sp.map, &sp.gmap, &sp.w0s}) b->release();
+        subs.clear();
+        sub_bits = 0;
+    }
 
     // upload q targets (20-byte big-endian, host) into target planes; returns stride
     hipError_t upload_targets(const uint8_t* t20, uint32_t q, uint64_t* ts) {
@@ -118,7 +154,7 @@ const char* dhtgpu_strerror(int code) {
         case DHTGPU_ENOMEM: return "device out of memory";
         case DHTGPU_EDEVICE: return "HIP device or kernel error";
         case DHTGPU_ENOIDS: return "no id set uploaded";
-        case DHTGPU_EUNSORTED: return "id set is not lexicographically sorted and unique";
+        case DHTGPU_EUNSORTED: return "id set holds duplicate ids (NodeCache keys are unique)";
         case DHTGPU_ERANGE: return "size out of range";
         default: return "unknown error";
     }
@@ -142,12 +178,16 @@ int dhtgpu_ctx_create(int device, dhtgpu_ctx** out) {
     c->device = device;
     hipError_t e = c->bind();
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming);
+    if (const char* d = getenv("DHTGPU_DBG")) c->dbg = (uint32_t)atoi(d);
     if (e == hipSuccess) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
     }
     if (e != hipSuccess) {
-        delete c;
+        dhtgpu_ctx_destroy(c);
         return map_err(e);
     }
     *out = c;
@@ -158,6 +198,8 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
     if (!c) return;
     (void)c->bind();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (hipStream_t x : c->side)
+        if (x) (void)hipStreamSynchronize(x);
     for (auto& b : c->bslot) {   // slots last used on other streams: let that work finish
         if (b.last && b.last != c->stream) (void)hipStreamSynchronize(b.last);
         if (b.done) (void)hipEventDestroy(b.done);
@@ -168,6 +210,15 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
         b->release();
     for (auto& b : c->bslot)
         for (DevBuf* d : {&b.ws, &b.out_idx, &b.out_cnt}) d->release();
+    c->invalidate_subs();
+    for (DevBuf* b : {&c->sub_mask, &c->sub_list, &c->sub_scratch, &c->stamps, &c->w0s, &c->sview.planes, &c->sview.perm,
+                      &c->cache.planes, &c->cache.perm, &c->cache_in, &c->sort_scratch, &c->cache_acc})
+        b->release();
+    for (hipStream_t x : c->side)
+        if (x) (void)hipStreamDestroy(x);
+    if (c->fork) (void)hipEventDestroy(c->fork);
+    for (hipEvent_t x : c->join)
+        if (x) (void)hipEventDestroy(x);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -199,7 +250,10 @@ static int alloc_ids(dhtgpu_ctx* c, uint64_t n) {
     c->index_valid = false;
     c->net_valid = false;
     c->shard_pbits = 0;
+    c->shard_pval = 0;
     c->has_gidx = false;
+    c->invalidate_subs();
+    c->sview.valid = false;
     c->stride = pad_ids(n ? n : 1);
     DHT_TRY(c->planes.ensure((size_t)c->stride * 5 * 4));
     return DHTGPU_OK;
@@ -264,6 +318,7 @@ int dhtgpu_gen_ids_prefix(dhtgpu_ctx* c, uint64_t seed, uint64_t start, uint64_t
         DHT_TRY(c->w0s.ensure((size_t)c->stride * 4));
         DHT_TRY(launch_shift_w0(c->planes.as<uint32_t>(), c->stride, pbits, c->w0s.as<uint32_t>(), c->stream));
         c->shard_pbits = pbits;
+        c->shard_pval = pval;
     }
     return DHTGPU_OK;
 }
@@ -326,15 +381,16 @@ int dhtgpu_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, 
     if (!q) return DHTGPU_OK;
     DHT_TRY(c->bind());
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    const ScanPlan p = plan_scan(c->n, q, c->num_cus);
+    const ScanPlan p = plan_scan(c->n, q, k, c->num_cus);
     const uint32_t* gidx = c->out_map();
-    if ((p.splits == 1 || c->n == 0) && !gidx) {   // one pass writes the final form directly
-        DHT_TRY(launch_scan(c->planes.as<uint32_t>(), c->stride, c->n, p, tp, ts, q, k, out_idx,
-                            out_cnt, out_rec, idx_base, s));
+    const bool one = p.splits == 1 || c->n == 0;
+    if (one && !(out_rec && gidx)) {   // one pass writes the final form directly
+        DHT_TRY(launch_scan(c->planes.as<uint32_t>(), c->stride, c->n, p, tp, ts, q, k, out_idx, out_cnt, out_rec,
+                            gidx, idx_base, s));
         return DHTGPU_OK;
     }
-    // local indices (merged over id-range splits when the batch is too small to fill
-    // the chip), then mapped to global indices or turned into candidate records
+    // local indices (merged over id-range splits when the batch is too small to fill the
+    // chip), then turned into candidate records or mapped to the final form
     uint32_t* li = out_idx;
     uint32_t* lc = out_cnt;
     if (out_rec) {
@@ -343,12 +399,13 @@ int dhtgpu_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, 
         li = c->out_idx.as<uint32_t>();
         lc = c->out_cnt.as<uint32_t>();
     }
-    if (p.splits == 1 || c->n == 0) {
-        DHT_TRY(launch_scan(c->planes.as<uint32_t>(), c->stride, c->n, p, tp, ts, q, k, li, lc, nullptr, 0, s));
+    if (one) {
+        DHT_TRY(launch_scan(c->planes.as<uint32_t>(), c->stride, c->n, p, tp, ts, q, k, li, lc, nullptr, nullptr, 0,
+                            s));
     } else {
         DHT_TRY(c->rec.ensure((size_t)p.splits * q * k * 6 * 4));
         DHT_TRY(launch_scan(c->planes.as<uint32_t>(), c->stride, c->n, p, tp, ts, q, k, nullptr, nullptr,
-                            c->rec.as<uint32_t>(), 0, s));
+                            c->rec.as<uint32_t>(), nullptr, 0, s));
         DHT_TRY(launch_merge(c->rec.as<uint32_t>(), p.splits, q, k, tp, ts, k, li, lc, s));
     }
     if (out_rec)
@@ -487,10 +544,11 @@ int dhtgpu_index_topk(dhtgpu_ctx* c, const uint8_t* t20, uint32_t q, uint32_t k,
     return DHTGPU_OK;
 }
 
-static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k, uint32_t* out_idx,
-                     uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base, hipStream_t s, hipEvent_t* ev) {
-    if (!batch_supported(c->n, q, k, c->num_cus)) return DHTGPU_ERANGE;
-    dhtgpu_ctx::BatchSlot& b = c->bslot[c->bnext];
+// ---- K6 -------------------------------------------------------------------------------------
+// One K6 launch sequence on workspace slot `si` (stream s): waits for the slot's previous user
+// when that was another stream, cleans the workspace head when needed.
+static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hipEvent_t* ev) {
+    dhtgpu_ctx::BatchSlot& b = c->bslot[si];
     // a slot last used on another stream: wait for that stream's work so far (it includes the
     // slot's previous call); same stream: stream order suffices
     if (b.last && b.last != s) {
@@ -498,13 +556,180 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
         DHT_TRY(hipEventRecord(b.done, b.last));
         DHT_TRY(hipStreamWaitEvent(s, b.done, 0));
     }
-    const size_t need = batch_bytes(c->n, q, k, c->num_cus);
+    const size_t need = batch_bytes(bc.n, bc.q, bc.q_plan, bc.k, c->num_cus);
     if (need > b.ws.cap) b.clean = false;
     DHT_TRY(b.ws.ensure(need));
     if (!b.clean) DHT_TRY(hipMemsetAsync(b.ws.p, 0, batch_clean_bytes(), s));
     b.clean = false;   // re-established below once every launch went through
-    c->blast = c->bnext;
+    if (bc.dbg & 256) {
+        DHT_TRY(c->stamps.ensure((size_t)2 * 8192 * 16 * 8));
+        bc.stamps = c->stamps.as<unsigned long long>();
+    }
+    bc.ws = b.ws.p;
+    bool dirty = false;
+    DHT_TRY(launch_batch_topk(bc, s, &dirty));
+    b.last = s;
+    b.clean = !dirty;
+    c->blast = si;
+    return DHTGPU_OK;
+}
+
+// Build the prefix sub-partitions: the smallest split into 2^s parts of <= 2^24 expected ids
+// (s <= 8), each compacted in id order (so index ties break the same way) from the context's
+// planes, with its shifted word-0 plane and its index maps.
+static int build_subs(dhtgpu_ctx* c) {
+    if (c->subs_valid) return DHTGPU_OK;
+    c->invalidate_subs();
+    uint32_t sb = 1;
+    while (sb < 8 && (c->n >> sb) > (1ull << 24)) ++sb;
+    const uint32_t P = c->shard_pbits + sb;   // prefix bits every id of a sub-partition shares
+    if (P > 24) return DHTGPU_ERANGE;
+    hipStream_t s = c->stream;
+    DHT_TRY(c->aux.ensure((size_t)select_scratch_words(c->n) * 4 + 16));
+    unsigned long long* d_total = reinterpret_cast<unsigned long long*>(c->aux.as<uint8_t>());
+    uint32_t* scratch = reinterpret_cast<uint32_t*>(c->aux.as<uint8_t>() + 8);
+    const uint32_t* planes = c->planes.as<uint32_t>();
+    c->subs.resize((size_t)1 << sb);
+    for (uint32_t i = 0; i < (1u << sb); ++i) {
+        const uint32_t pv = (c->shard_pval << sb) | i;
+        DHT_TRY(launch_select_prefix(planes, c->stride, c->n, P, pv, scratch, d_total, nullptr, 0, nullptr, 0, s));
+        unsigned long long m = 0;
+        DHT_TRY(hipMemcpyAsync(&m, d_total, 8, hipMemcpyDeviceToHost, s));
+        DHT_TRY(hipStreamSynchronize(s));
+        dhtgpu_ctx::SubPart& sp = c->subs[i];
+        sp.n = m;
+        sp.stride = pad_ids(m ? m : 1);
+        DHT_TRY(sp.planes.ensure((size_t)sp.stride * 5 * 4));
+        DHT_TRY(sp.map.ensure((size_t)sp.stride * 4));
+        DHT_TRY(sp.w0s.ensure((size_t)sp.stride * 4));
+        for (int w = 0; w < 5; ++w)   // deterministic padding words (F2 may read them, masked)
+            DHT_TRY(launch_fill(sp.planes.as<uint32_t>() + (uint64_t)w * sp.stride + m, sp.stride - m, 0u, s));
+        DHT_TRY(launch_select_prefix(planes, c->stride, c->n, P, pv, scratch, d_total, sp.planes.as<uint32_t>(),
+                                     sp.stride, sp.map.as<uint32_t>(), 0, s));
+        DHT_TRY(launch_shift_w0(sp.planes.as<uint32_t>(), sp.stride, P, sp.w0s.as<uint32_t>(), s));
+        if (c->has_gidx) {   // sub -> global stream index, composed once
+            DHT_TRY(sp.gmap.ensure((size_t)sp.stride * 4));
+            DHT_TRY(hipMemcpyAsync(sp.gmap.p, sp.map.p, (size_t)m * 4, hipMemcpyDeviceToDevice, s));
+            DHT_TRY(launch_map_idx(sp.gmap.as<uint32_t>(), m, c->gidx.as<uint32_t>(), 0, s));
+        }
+    }
+    DHT_TRY(hipStreamSynchronize(s));
+    c->sub_bits = sb;
+    c->subs_valid = true;
+    return DHTGPU_OK;
+}
+
+// A K6 call over prefix sub-partitions.  Sub-partition i answers the targets of its prefix
+// (F1 selects them) from its own ids: when it holds >= k ids, every id of it is XOR-closer to
+// such a target than every id outside it, so its top-k is the set's.  Sub-partitions with fewer
+// than k ids (their targets need ids outside), or that K6 cannot plan, send their targets to the
+// K1 scan (over the whole set, resp. the sub-partition).  The sub-calls alternate over the two
+// internal streams, forked from and joined back into s.
+static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k, uint32_t* out_idx,
+                          uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base, hipStream_t s, hipEvent_t* ev) {
+    int r = build_subs(c);
+    if (r) return r;
+    const uint32_t sb = c->sub_bits, S = 1u << sb;
+    const uint32_t P = c->shard_pbits + sb;
+    const bool global = c->has_gidx && c->map_global && !out_rec;
+    // record mode: context-local indices first (then records from the context's planes)
+    dhtgpu_ctx::BatchSlot& b0 = c->bslot[0];
+    uint32_t* li = out_idx;
+    uint32_t* lc = out_cnt;
+    if (out_rec) {
+        DHT_TRY(b0.out_idx.ensure((size_t)q * k * 4));
+        DHT_TRY(b0.out_cnt.ensure((size_t)q * 4));
+        li = b0.out_idx.as<uint32_t>();
+        lc = b0.out_cnt.as<uint32_t>();
+    }
+    DHT_TRY(hipEventRecord(c->fork, s));
+    for (hipStream_t x : c->side) DHT_TRY(hipStreamWaitEvent(x, c->fork, 0));
+    const uint32_t q_plan = std::max<uint32_t>(1u, (uint32_t)(((uint64_t)q + S - 1) >> sb));
+    std::vector<uint32_t> deficient, scan_subs;
+    for (uint32_t i = 0; i < S; ++i) {
+        const dhtgpu_ctx::SubPart& sp = c->subs[i];
+        if (sp.n < k) { deficient.push_back(i); continue; }
+        if (!batch_supported(sp.n, q_plan, k, c->num_cus)) { scan_subs.push_back(i); continue; }
+        BatchCall bc{};
+        bc.planes = sp.planes.as<uint32_t>();
+        bc.stride = sp.stride;
+        bc.n = sp.n;
+        bc.tp = tp;
+        bc.ts = ts;
+        bc.q = q;
+        bc.q_plan = q_plan;
+        bc.k = k;
+        bc.sel_shift = c->shard_pbits;
+        bc.sel_bits = sb;
+        bc.sel_val = i;
+        bc.skip = P;
+        bc.w0s = sp.w0s.as<uint32_t>();
+        bc.gidx = global ? sp.gmap.as<uint32_t>() : sp.map.as<uint32_t>();
+        bc.base = 0;
+        bc.out_idx = li;
+        bc.out_cnt = lc;
+        bc.num_cus = c->num_cus;
+        bc.dbg = c->dbg;
+        bc.ev = i == 0 ? ev : nullptr;   // diagnostics time sub-partition 0's kernels
+        r = batch_slot_run(c, (int)(i % dhtgpu_ctx::kBatchDepth), bc, c->side[i & 1], nullptr);
+        if (r) return r;
+    }
+    if (!deficient.empty() || !scan_subs.empty()) {   // rare: strongly non-uniform id sets
+        hipStream_t x = c->side[0];
+        const size_t mwords = ((size_t)S + 31) / 32;
+        DHT_TRY(c->sub_mask.ensure(mwords * 4));
+        DHT_TRY(c->sub_list.ensure((size_t)q * 4 + 256));
+        if (c->sub_scratch.cap < list_scan_bytes(k)) c->sub_scratch_clean = false;
+        DHT_TRY(c->sub_scratch.ensure(list_scan_bytes(k)));
+        if (!c->sub_scratch_clean) DHT_TRY(hipMemsetAsync(c->sub_scratch.p, 0, list_scan_bytes(k), x));
+        c->sub_scratch_clean = true;
+        uint32_t* list = c->sub_list.as<uint32_t>();
+        uint32_t* d_cnt = reinterpret_cast<uint32_t*>(c->sub_list.as<uint8_t>() + (((size_t)q * 4 + 255) & ~size_t(255)));
+        auto route = [&](const std::vector<uint32_t>& which, const uint32_t* planes, uint64_t stride, uint64_t n,
+                         const uint32_t* gidx) -> int {
+            std::vector<uint32_t> mask(mwords, 0u);
+            for (uint32_t i : which) mask[i >> 5] |= 1u << (i & 31);
+            DHT_TRY(hipMemcpyAsync(c->sub_mask.p, mask.data(), mwords * 4, hipMemcpyHostToDevice, x));
+            DHT_TRY(launch_select_targets(tp, q, c->shard_pbits, sb, c->sub_mask.as<uint32_t>(), list, d_cnt, x));
+            DHT_TRY(launch_list_scan(planes, stride, n, tp, ts, k, list, d_cnt, gidx, 0, li, lc, c->sub_scratch.p, x));
+            DHT_TRY(hipStreamSynchronize(x));   // the host mask and the list are reused
+            return DHTGPU_OK;
+        };
+        if (!deficient.empty()) {
+            r = route(deficient, c->planes.as<uint32_t>(), c->stride, c->n, global ? c->gidx.as<uint32_t>() : nullptr);
+            if (r) return r;
+        }
+        for (uint32_t i : scan_subs) {
+            const dhtgpu_ctx::SubPart& sp = c->subs[i];
+            r = route(std::vector<uint32_t>{i}, sp.planes.as<uint32_t>(), sp.stride, sp.n,
+                      global ? sp.gmap.as<uint32_t>() : sp.map.as<uint32_t>());
+            if (r) return r;
+        }
+    }
+    for (int i = 0; i < 2; ++i) {
+        DHT_TRY(hipEventRecord(c->join[i], c->side[i]));
+        DHT_TRY(hipStreamWaitEvent(s, c->join[i], 0));
+    }
+    if (out_rec) {
+        DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, c->out_map(),
+                                    out_rec, s));
+    } else if (!global && idx_base) {
+        DHT_TRY(launch_map_idx(out_idx, (uint64_t)q * k, nullptr, idx_base, s));
+    }
+    return DHTGPU_OK;
+}
+
+static bool needs_subs(const dhtgpu_ctx* c, uint32_t q, uint32_t k) {
+    return c->n > (1ull << 24) && !batch_supported(c->n, q, k, c->num_cus) && q <= (1u << 22);
+}
+
+static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k, uint32_t* out_idx,
+                     uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base, hipStream_t s, hipEvent_t* ev) {
+    if (needs_subs(c, q, k)) return batch_run_subs(c, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s, ev);
+    if (!batch_supported(c->n, q, k, c->num_cus)) return DHTGPU_ERANGE;
+    const int si = c->bnext;
     c->bnext = (c->bnext + 1) % dhtgpu_ctx::kBatchDepth;
+    dhtgpu_ctx::BatchSlot& b = c->bslot[si];
     const uint32_t* gidx = c->out_map();
     uint32_t* li = out_idx;
     uint32_t* lc = out_cnt;
@@ -514,14 +739,29 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
         li = b.out_idx.as<uint32_t>();
         lc = b.out_cnt.as<uint32_t>();
     }
-    DHT_TRY(launch_batch_topk(b.ws.p, c->planes.as<uint32_t>(), c->stride, c->n, tp, ts, q, k,
-                              out_rec ? nullptr : gidx, out_rec ? 0u : idx_base, li, lc, c->num_cus, c->shard_pbits,
-                              c->shard_pbits ? c->w0s.as<uint32_t>() : nullptr, s, ev));
+    BatchCall bc{};
+    bc.planes = c->planes.as<uint32_t>();
+    bc.stride = c->stride;
+    bc.n = c->n;
+    bc.tp = tp;
+    bc.ts = ts;
+    bc.q = q;
+    bc.q_plan = q;
+    bc.k = k;
+    bc.skip = c->shard_pbits;
+    bc.w0s = c->shard_pbits ? c->w0s.as<uint32_t>() : nullptr;
+    bc.gidx = out_rec ? nullptr : gidx;
+    bc.base = out_rec ? 0u : idx_base;
+    bc.out_idx = li;
+    bc.out_cnt = lc;
+    bc.num_cus = c->num_cus;
+    bc.dbg = c->dbg;
+    bc.ev = ev;
+    int r = batch_slot_run(c, si, bc, s, ev);
+    if (r) return r;
     if (out_rec)
         DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
                                     out_rec, s));
-    b.last = s;
-    b.clean = true;
     return DHTGPU_OK;
 }
 
@@ -543,16 +783,24 @@ int dhtgpu_batch_topk_timed(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint
     if (!c->has_ids) return DHTGPU_ENOIDS;
     DHT_TRY(c->bind());
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    hipEvent_t ev[8];   // start/stop per kernel, recorded by the kernels' dispatches
+    hipEvent_t ev[8];   // start/stop per kernel, recorded by the kernels' own dispatches
     for (int i = 0; i < 8; ++i) DHT_TRY(hipEventCreate(&ev[i]));
+    const bool subs = needs_subs(c, q, k);
     int r = batch_run(c, tp, ts, q, k, out_idx, out_cnt, nullptr, 0, s, ev);
-    hipError_t e = r ? hipSuccess : hipEventSynchronize(ev[7]);
+    hipError_t e = r ? hipSuccess : hipStreamSynchronize(s);
+    if (!r && e == hipSuccess) e = hipEventSynchronize(ev[7]);
     for (int i = 0; !r && e == hipSuccess && i < 4; ++i) e = hipEventElapsedTime(&ms4[i], ev[2 * i], ev[2 * i + 1]);
     for (int i = 0; i < 8; ++i) (void)hipEventDestroy(ev[i]);
     if (r) return r;
     DHT_TRY(e);
     if (stats4) {
-        DHT_TRY(batch_read_stats(c->bslot[c->blast].ws.p, c->n, q, k, c->num_cus, stats4, s));
+        if (subs) {   // sub-partition 0's call (slot 0)
+            const auto& sp = c->subs[0];
+            const uint32_t qp = std::max<uint32_t>(1u, (uint32_t)(((uint64_t)q + (1u << c->sub_bits) - 1) >> c->sub_bits));
+            DHT_TRY(batch_read_stats(c->bslot[0].ws.p, sp.n, q, qp, k, c->num_cus, stats4, s));
+        } else {
+            DHT_TRY(batch_read_stats(c->bslot[c->blast].ws.p, c->n, q, q, k, c->num_cus, stats4, s));
+        }
     }
     return DHTGPU_OK;
 }
@@ -675,29 +923,111 @@ int dhtgpu_classify(dhtgpu_ctx* c, uint32_t nb, const uint8_t* firsts20, const u
     return DHTGPU_OK;
 }
 
-int dhtgpu_cached_nodes(dhtgpu_ctx* c, const uint8_t* accept, const uint8_t* t20, uint32_t q,
-                        uint32_t count, uint32_t* out_idx, uint32_t* out_cnt) {
-    if (!c || count == 0 || count > DHTGPU_MAX_K || (q && (!t20 || !out_idx || !out_cnt))) return DHTGPU_EINVAL;
-    if (!c->has_ids) return DHTGPU_ENOIDS;
-    if (!c->sorted) return DHTGPU_EUNSORTED;
-    if (!q) return DHTGPU_OK;
-    DHT_TRY(c->bind());
+// Sort n ids (planes, stride) into `out` (sorted planes + permutation); synchronises.
+static int sort_into(dhtgpu_ctx* c, const uint32_t* planes, uint64_t stride, uint64_t n, dhtgpu_ctx::SortedSet& out) {
+    out.valid = false;
+    out.n = n;
+    out.stride = pad_ids(n ? n : 1);
+    DHT_TRY(out.planes.ensure((size_t)out.stride * 5 * 4));
+    DHT_TRY(out.perm.ensure((size_t)out.stride * 4));
+    DHT_TRY(c->sort_scratch.ensure(sort_scratch_bytes(n)));
+    int unique = 1;
+    DHT_TRY(launch_sort_ids(planes, stride, n, out.planes.as<uint32_t>(), out.stride, out.perm.as<uint32_t>(),
+                            c->sort_scratch.p, &unique, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    if (c->sort_scratch.cap > ((size_t)1 << 30)) c->sort_scratch.release();   // large sorts: do not keep GBs
+    out.unique = unique != 0;
+    out.valid = true;
+    return DHTGPU_OK;
+}
+
+// The getCachedNodes walk of q targets over a sorted set (perm nullable), accept[] in caller order.
+static int cached_walk(dhtgpu_ctx* c, const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* perm,
+                       const uint8_t* accept, const uint8_t* t20, uint32_t q, uint32_t count, const uint32_t* gidx,
+                       uint32_t* out_idx, uint32_t* out_cnt) {
     uint8_t* d_acc = nullptr;
-    if (accept && c->n) {
-        DHT_TRY(c->aux.ensure((size_t)c->n + 16));
-        d_acc = c->aux.as<uint8_t>();
-        DHT_TRY(hipMemcpyAsync(d_acc, accept, (size_t)c->n, hipMemcpyHostToDevice, c->stream));
+    if (accept && n) {
+        DHT_TRY(c->cache_acc.ensure((size_t)n + 16));
+        d_acc = c->cache_acc.as<uint8_t>();
+        DHT_TRY(hipMemcpyAsync(d_acc, accept, (size_t)n, hipMemcpyHostToDevice, c->stream));
     }
     uint64_t ts = 0;
     DHT_TRY(c->upload_targets(t20, q, &ts));
     DHT_TRY(c->aux2.ensure((size_t)q * count * 4));
     DHT_TRY(c->aux3.ensure((size_t)q * 4));
-    DHT_TRY(launch_cached(c->planes.as<uint32_t>(), c->stride, c->n, d_acc, c->targets.as<uint32_t>(),
-                          ts, q, count, c->aux2.as<uint32_t>(), c->aux3.as<uint32_t>(), c->stream));
-    if (c->out_map())
-        DHT_TRY(launch_map_idx(c->aux2.as<uint32_t>(), (uint64_t)q * count, c->gidx.as<uint32_t>(), 0, c->stream));
+    DHT_TRY(launch_cached(planes, stride, n, perm, d_acc, c->targets.as<uint32_t>(), ts, q, count,
+                          c->aux2.as<uint32_t>(), c->aux3.as<uint32_t>(), c->stream));
+    if (gidx) DHT_TRY(launch_map_idx(c->aux2.as<uint32_t>(), (uint64_t)q * count, gidx, 0, c->stream));
     DHT_TRY(hipMemcpyAsync(out_idx, c->aux2.p, (size_t)q * count * 4, hipMemcpyDeviceToHost, c->stream));
     DHT_TRY(hipMemcpyAsync(out_cnt, c->aux3.p, (size_t)q * 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_cached_nodes(dhtgpu_ctx* c, const uint8_t* accept, const uint8_t* t20, uint32_t q,
+                        uint32_t count, uint32_t* out_idx, uint32_t* out_cnt) {
+    if (!c || count == 0 || count > DHTGPU_MAX_K || (q && (!t20 || !out_idx || !out_cnt))) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    DHT_TRY(c->bind());
+    if (c->sorted) {
+        if (!q) return DHTGPU_OK;
+        return cached_walk(c, c->planes.as<uint32_t>(), c->stride, c->n, nullptr, accept, t20, q, count, c->out_map(),
+                           out_idx, out_cnt);
+    }
+    // an unsorted upload: walk its lexicographically sorted view (built once per id set)
+    if (!c->sview.valid) {
+        int r = sort_into(c, c->planes.as<uint32_t>(), c->stride, c->n, c->sview);
+        if (r) return r;
+    }
+    if (!c->sview.unique) return DHTGPU_EUNSORTED;
+    if (!q) return DHTGPU_OK;
+    return cached_walk(c, c->sview.planes.as<uint32_t>(), c->sview.stride, c->n, c->sview.perm.as<uint32_t>(), accept,
+                       t20, q, count, c->out_map(), out_idx, out_cnt);
+}
+
+int dhtgpu_cache_set(dhtgpu_ctx* c, const uint8_t* ids20, uint64_t n, uint64_t version) {
+    if (!c || (!ids20 && n)) return DHTGPU_EINVAL;
+    if (n >= 0xFFFFFFFFull) return DHTGPU_ERANGE;
+    if (version && c->cache.valid && version == c->cache_version && n == c->cache.n) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    c->cache.valid = false;
+    c->cache_version = 0;
+    const uint64_t st = pad_ids(n ? n : 1);
+    DHT_TRY(c->cache_in.ensure((size_t)st * 5 * 4));
+    const uint64_t chunk = 1ull << 22;
+    DHT_TRY(c->staging.ensure((size_t)std::min<uint64_t>(n ? n : 1, chunk) * 20));
+    for (uint64_t i = 0; i < n; i += chunk) {
+        const uint64_t m = std::min(chunk, n - i);
+        DHT_TRY(hipMemcpyAsync(c->staging.p, ids20 + i * 20, (size_t)m * 20, hipMemcpyHostToDevice, c->stream));
+        DHT_TRY(launch_pack(c->staging.as<uint8_t>(), m, c->cache_in.as<uint32_t>() + i, st, c->stream));
+        DHT_TRY(hipStreamSynchronize(c->stream));   // staging is reused
+    }
+    int r = sort_into(c, c->cache_in.as<uint32_t>(), st, n, c->cache);
+    if (r) return r;
+    if (!c->cache.unique) {
+        c->cache.valid = false;
+        return DHTGPU_EUNSORTED;
+    }
+    c->cache_version = version;
+    return DHTGPU_OK;
+}
+
+int dhtgpu_cache_nodes(dhtgpu_ctx* c, const uint8_t* accept, const uint8_t* t20, uint32_t q, uint32_t count,
+                       uint32_t* out_idx, uint32_t* out_cnt) {
+    if (!c || count == 0 || count > DHTGPU_MAX_K || (q && (!t20 || !out_idx || !out_cnt))) return DHTGPU_EINVAL;
+    if (!c->cache.valid) return DHTGPU_ENOIDS;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    return cached_walk(c, c->cache.planes.as<uint32_t>(), c->cache.stride, c->cache.n, c->cache.perm.as<uint32_t>(),
+                       accept, t20, q, count, nullptr, out_idx, out_cnt);
+}
+
+int dhtgpu_cache_sorted(dhtgpu_ctx* c, uint32_t* perm) {
+    if (!c || (!perm && c->cache.n)) return DHTGPU_EINVAL;
+    if (!c->cache.valid) return DHTGPU_ENOIDS;
+    if (!c->cache.n) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    DHT_TRY(hipMemcpyAsync(perm, c->cache.perm.p, (size_t)c->cache.n * 4, hipMemcpyDeviceToHost, c->stream));
     DHT_TRY(hipStreamSynchronize(c->stream));
     return DHTGPU_OK;
 }
@@ -718,17 +1048,16 @@ int dhtgpu_buffer_nodes_dev(dhtgpu_ctx* c, const uint8_t* node_tail, uint32_t af
     return DHTGPU_OK;
 }
 
-int dhtgpu_buffer_nodes(dhtgpu_ctx* c, const uint8_t* node_tail, uint32_t af, const uint8_t* t20, uint32_t q,
-                        const uint32_t* cand, uint32_t nc, uint8_t* out, uint32_t* out_len) {
-    if (!c || (af != 4 && af != 6) || nc > 64) return DHTGPU_EINVAL;
-    if (q && (!t20 || !out || !out_len || (nc && (!cand || !node_tail)))) return DHTGPU_EINVAL;
-    if (!c->has_ids) return DHTGPU_ENOIDS;
-    if (!q) return DHTGPU_OK;
-    DHT_TRY(c->bind());
+static int buffer_nodes_impl(dhtgpu_ctx* c, const uint32_t* planes, uint64_t stride, uint64_t n,
+                             const uint8_t* node_tail, uint32_t af, const uint8_t* t20, uint32_t q,
+                             const uint32_t* cand, uint32_t nc, uint8_t* out, uint32_t* out_len, size_t lead) {
+    // every candidate must name a node (the kernel reads its planes and tail)
+    for (size_t i = 0; i < (size_t)q * nc; ++i)
+        if (cand[i] != DHTGPU_NONE && cand[i] >= n) return DHTGPU_EINVAL;
     const uint32_t alen = af == 4 ? 4u : 16u, rec = 20 + alen + 2;
-    const size_t tl = (size_t)c->n * (alen + 2), cl = (size_t)q * nc * 4, ol = (size_t)q * 8 * rec, ll = (size_t)q * 4;
-    DHT_TRY(c->wire.ensure(al256(tl) + al256(cl) + al256(ol) + al256(ll) + 256));
-    uint8_t* base = c->wire.as<uint8_t>();
+    const size_t tl = (size_t)n * (alen + 2), cl = (size_t)q * nc * 4, ol = (size_t)q * 8 * rec, ll = (size_t)q * 4;
+    DHT_TRY(c->wire.ensure(lead + al256(tl) + al256(cl) + al256(ol) + al256(ll) + 256));
+    uint8_t* base = c->wire.as<uint8_t>() + lead;
     uint8_t* d_tail = base;
     uint32_t* d_cand = reinterpret_cast<uint32_t*>(base + al256(tl));
     uint8_t* d_out = base + al256(tl) + al256(cl);
@@ -737,12 +1066,47 @@ int dhtgpu_buffer_nodes(dhtgpu_ctx* c, const uint8_t* node_tail, uint32_t af, co
     if (cl) DHT_TRY(hipMemcpyAsync(d_cand, cand, cl, hipMemcpyHostToDevice, c->stream));
     uint64_t ts = 0;
     DHT_TRY(c->upload_targets(t20, q, &ts));
-    DHT_TRY(launch_wire_encode(c->planes.as<uint32_t>(), c->stride, d_tail, alen, c->targets.as<uint32_t>(), ts, q,
-                               d_cand, nc, d_out, d_len, c->stream));
+    DHT_TRY(launch_wire_encode(planes, stride, d_tail, alen, c->targets.as<uint32_t>(), ts, q, d_cand, nc, d_out,
+                               d_len, c->stream));
     DHT_TRY(hipMemcpyAsync(out, d_out, ol, hipMemcpyDeviceToHost, c->stream));
     DHT_TRY(hipMemcpyAsync(out_len, d_len, ll, hipMemcpyDeviceToHost, c->stream));
     DHT_TRY(hipStreamSynchronize(c->stream));
     return DHTGPU_OK;
+}
+
+int dhtgpu_buffer_nodes(dhtgpu_ctx* c, const uint8_t* node_tail, uint32_t af, const uint8_t* t20, uint32_t q,
+                        const uint32_t* cand, uint32_t nc, uint8_t* out, uint32_t* out_len) {
+    if (!c || (af != 4 && af != 6) || nc > 64) return DHTGPU_EINVAL;
+    if (q && (!t20 || !out || !out_len || (nc && (!cand || !node_tail)))) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    return buffer_nodes_impl(c, c->planes.as<uint32_t>(), c->stride, c->n, node_tail, af, t20, q, cand, nc, out,
+                             out_len, 0);
+}
+
+int dhtgpu_buffer_nodes_ids(dhtgpu_ctx* c, const uint8_t* node_ids20, const uint8_t* node_tail, uint32_t nn,
+                            uint32_t af, const uint8_t* t20, uint32_t q, const uint32_t* cand, uint32_t nc,
+                            uint8_t* out, uint32_t* out_len) {
+    if (!c || (af != 4 && af != 6) || nc > 64) return DHTGPU_EINVAL;
+    if (q && (!t20 || !out || !out_len || (nc && (!cand || !node_tail)))) return DHTGPU_EINVAL;
+    if (nn && (!node_ids20 || !node_tail)) return DHTGPU_EINVAL;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    // the nodes' planes lead the wire scratch (sized for the whole call first: ensure() may
+    // reallocate); the context's id set is left alone
+    const uint64_t ns = pad_q(nn ? nn : 1);
+    const size_t lead = al256((size_t)ns * 5 * 4);
+    const uint32_t alen = af == 4 ? 4u : 16u, rec = 20 + alen + 2;
+    DHT_TRY(c->wire.ensure(lead + al256((size_t)nn * (alen + 2)) + al256((size_t)q * nc * 4) +
+                           al256((size_t)q * 8 * rec) + al256((size_t)q * 4) + 256));
+    if (nn) {
+        DHT_TRY(c->staging.ensure((size_t)nn * 20));
+        DHT_TRY(hipMemcpyAsync(c->staging.p, node_ids20, (size_t)nn * 20, hipMemcpyHostToDevice, c->stream));
+        DHT_TRY(launch_pack(c->staging.as<uint8_t>(), nn, c->wire.as<uint32_t>(), ns, c->stream));
+        DHT_TRY(hipStreamSynchronize(c->stream));   // staging is reused for the targets
+    }
+    return buffer_nodes_impl(c, c->wire.as<uint32_t>(), ns, nn, node_tail, af, t20, q, cand, nc, out, out_len, lead);
 }
 
 int dhtgpu_deserialize_nodes(dhtgpu_ctx* c, uint32_t af, const uint8_t* myid20, const uint8_t* blob,

@@ -23,16 +23,20 @@
 //       words 1..4 are read from the planes only when two w0 distances tie.  A target
 //       whose subtree holds fewer than min(k, n) ids (or whose partition overflows the
 //       LDS stage -- strongly clustered ids) is appended to a fallback list;
-//   F4  answers the fallback list by an exact brute-force pass over all ids (one
-//       workgroup per target; on uniform ids the list is empty and F4 exits at once).
+//   F4  answers the fallback list with the K1 streaming scan (scan_dev.h) over all ids,
+//       its roles sized at run time from the list's device-side count (target groups of
+//       128 x id-range splits, split lists merged by the last split of each group), and
+//       the ties F3 deferred (one wave each).  On uniform ids the list is empty and the
+//       scan roles exit at once.
 // F3 also clears the bitmap words it owns, so the bitmap is all-zero between calls.
 //
 // Algorithmic bytes per call: n * 4 (w0) + q * 4 (target w0) + survivors * 16 (written
 // and re-read as {w0, idx}) + q * k * 4 (results).  On uniform ids the survivor fraction
 // is 1 - exp(-q / 2^Lm) (12 % at the cfg-2 batch).
-#include "dhtgpu_dev.h"
+#include "scan_dev.h"
 #include <hip/hip_ext.h>
-#include "dhtgpu_internal.h"
+
+#include <mutex>
 
 #include <algorithm>
 #include <cmath>
@@ -48,7 +52,6 @@ constexpr int kF1Threads = 256;                      // one thread per target
 constexpr int kF3Threads = 256;
 constexpr uint32_t kF3Cap = 4096;                    // survivors per partition staged in LDS
 constexpr uint32_t kF3Per = kF3Cap / kF3Threads;
-constexpr int kF4Threads = 256;
 constexpr uint32_t kMaxLm = 19;                      // 2^19-bit bitmap = 64 KB of LDS in F2
 constexpr uint32_t kMaxSubBits = 11;                 // F3 sub-prefix histogram <= 2048 bins
 constexpr uint32_t kMaxQ = 1u << 22;                 // targets per call
@@ -134,16 +137,22 @@ __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
 // ctr[kSpill]); F3 moves the spill list to the F4 fallback list.
 constexpr uint32_t kSpill = 8;   // ctr word: spilled targets (all-zero between calls)
 
+// Sub-partition calls (dhtgpu_ctx's prefix sub-partitions of a large id set) keep only the
+// targets whose bits [sel_shift, sel_shift + sel_bits) equal sel_val; the others belong to
+// another sub-partition's call.
 __global__ __launch_bounds__(kF1Threads) void k_f1_targets(const uint32_t* __restrict__ tw0,
                                                           const uint32_t* __restrict__ tw1, uint32_t q, uint32_t Lm,
-                                                          uint32_t b1, uint32_t shift, uint32_t* __restrict__ bitmap,
-                                                          uint32_t* __restrict__ tcount, uint2* __restrict__ tbuf,
-                                                          uint32_t tcap, uint32_t* __restrict__ ctr,
-                                                          uint32_t* __restrict__ tspill) {
+                                                          uint32_t b1, uint32_t shift, uint32_t sel_shift,
+                                                          uint32_t sel_bits, uint32_t sel_val,
+                                                          uint32_t* __restrict__ bitmap, uint32_t* __restrict__ tcount,
+                                                          uint2* __restrict__ tbuf, uint32_t tcap,
+                                                          uint32_t* __restrict__ ctr, uint32_t* __restrict__ tspill) {
     if (blockIdx.x == 0 && threadIdx.x < 4) ctr[threadIdx.x] = 0;   // fallback, survivors, wave path, -
     const uint32_t i = blockIdx.x * kF1Threads + threadIdx.x;
     if (i >= q) return;
-    const uint32_t v = shift ? (tw0[i] << shift) | (tw1[i] >> (32 - shift)) : tw0[i];
+    const uint32_t w = tw0[i];
+    if (sel_bits && ((w << sel_shift) >> (32 - sel_bits)) != sel_val) return;
+    const uint32_t v = shift ? (w << shift) | (tw1[i] >> (32 - shift)) : w;
     const uint32_t pre = top_bits(v, Lm);
     atomicOr(bitmap + (pre >> 5), 1u << (pre & 31));
     const uint32_t p = top_bits(v, b1);
@@ -172,7 +181,7 @@ constexpr uint32_t kF2Step = 4 * kF2Sub;             // ids per chunk
 constexpr uint32_t kStage = 11264;                   // LDS stage entries (88 KB)
 
 __host__ __device__ inline uint32_t f2_fixed_words(uint32_t nwords, uint32_t np) {
-    return (36 + nwords + np + 1 + 17 + 3) & ~3u;
+    return (36 + nwords + np + 1 + 17 + np / 32 + 1 + 3) & ~3u;
 }
 
 struct F2Args {
@@ -275,12 +284,13 @@ constexpr uint32_t kF2Dense = 0, kF2Sparse = 1, kF2Stream = 2;
 
 template <uint32_t Mode>
 __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
-    extern __shared__ uint32_t sh[];   // (32 spare) | misc[8] | bm[nwords] | hist[np + 1] | wsum[17] | stage
+    extern __shared__ uint32_t sh[];   // (32 spare) | misc[8] | bm[nwords] | hist[np + 1] | wsum[17] | lost[np/32 + 1] | stage
     const uint32_t np = 1u << a.b1;
     uint32_t* misc = sh + 28;
     uint32_t* bm = sh + 36;
     uint32_t* hist = bm + a.nwords;
     uint32_t* wsum = hist + np + 1;
+    uint32_t* lost = wsum + 17;   // sparse mode: partitions that lost survivors past a full stage
     uint2* stage = reinterpret_cast<uint2*>(sh + f2_fixed_words(a.nwords, np));
     const uint64_t lo64 = (uint64_t)blockIdx.x * a.per_blk;
     if (lo64 >= a.n) return;
@@ -319,6 +329,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
 #pragma unroll
     for (uint32_t r = 0; r < kRing; ++r) ring[r] = f2_load1(a.w0, lo + r * kF2Sub, lim);
     if (threadIdx.x < 3) misc[threadIdx.x] = 0;
+    for (uint32_t i = threadIdx.x; i <= np / 32; i += kF2Threads) lost[i] = 0;
     sync_lds();
     F2_STAMP(1);
     // Dense mode: stage fill `cnt` is block-uniform.  Sub-step s reserves slots with one
@@ -377,20 +388,20 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                         pos += (uint32_t)__popcll(bal[f]);
                     }
                 } else {
-                    // sparse-mode overflow (never on the planned workload): the entries past
-                    // the stage go straight to their partition buckets
+                    // sparse-mode overflow (never on uniform ids; clustered ids): an entry past
+                    // the stage is dropped and its partition marked lost -- the block then
+                    // pushes that partition's count past the F3 stage, so F3 sends its targets
+                    // to the exact fallback scan (no per-entry global atomics on a hot counter)
 #pragma unroll
                     for (uint32_t f = 0; f < 4; ++f) {
                         if (sv[f]) {
                             const uint32_t at = __builtin_amdgcn_mbcnt_hi(
                                 (uint32_t)(bal[f] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[f], pos));
-                            const uint2 e = make_uint2(v4[f], j0 + f);
                             if (at < a.stage) {
-                                stage[at] = e;
+                                stage[at] = make_uint2(v4[f], j0 + f);
                             } else {
-                                const uint32_t p = top_bits(e.x, a.b1);
-                                const uint32_t slot = atomicAdd(a.pcount + p, 1u);
-                                if (slot < a.pcap) a.pbuf[(uint64_t)p * a.pcap + slot] = e;
+                                const uint32_t p = top_bits(v4[f], a.b1);
+                                atomicOr(lost + (p >> 5), 1u << (p & 31));
                             }
                         }
                         pos += (uint32_t)__popcll(bal[f]);
@@ -411,6 +422,16 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     }
     F2_STAMP(2);
     if (cnt) f2_flush(a, cnt, stage, hist, wsum);
+    if (Mode == kF2Sparse) {   // partitions that lost entries: count past any stage (F3 -> fallback)
+        for (uint32_t i = threadIdx.x; i <= np / 32; i += kF2Threads) {
+            uint32_t m = lost[i];
+            while (m) {
+                const uint32_t b = (uint32_t)__ffs(m) - 1;
+                m &= m - 1;
+                atomicAdd(a.pcount + 32 * i + b, a.pcap + 1u);
+            }
+        }
+    }
     F2_STAMP(5);
 }
 
@@ -611,7 +632,11 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     const uint2* tsrc = a.tbuf + (uint64_t)p * a.tcap;
     if (p == 0) {   // spilled targets (foreign, or a full bucket) join the fallback list
         const uint32_t nsp = a.ctr[kSpill];
-        for (uint32_t j = threadIdx.x; j < nsp; j += kF3Threads) a.fb_list[atomicAdd(a.ctr, 1u)] = a.tspill[j];
+        if (nsp) {   // one reservation for the block
+            if (threadIdx.x == 0) ntie[2] = atomicAdd(a.ctr, nsp);
+            sync_lds();
+            for (uint32_t j = threadIdx.x; j < nsp; j += kF3Threads) a.fb_list[ntie[2] + j] = a.tspill[j];
+        }
     }
     sync_lds();   // every thread has read the counts
     if (threadIdx.x == 0) {   // all-zero again for the next call
@@ -627,7 +652,9 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     if (Diag && (a.dbg & 32)) return;
     if (m > kF3Cap || m > a.pcap) {
         // strongly clustered ids: this partition's targets take the exact brute-force path
-        for (uint32_t j = threadIdx.x; j < mt; j += kF3Threads) a.fb_list[atomicAdd(a.ctr, 1u)] = tsrc[j].y;
+        if (threadIdx.x == 0) ntie[2] = atomicAdd(a.ctr, mt);   // one reservation for the block
+        sync_lds();
+        for (uint32_t j = threadIdx.x; j < mt; j += kF3Threads) a.fb_list[ntie[2] + j] = tsrc[j].y;
         return;
     }
     // first chunk of targets and the partition's survivors: both loads in flight together
@@ -841,19 +868,102 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     F3_STAMP(7);
 }
 
-// ---- F4: deferred ties and the exact brute force for the fallback targets ---------------
-// Blocks [0, nfb): one workgroup per fallback target: every thread keeps a sorted
-// top-`want` list of its strided share of the ids in LDS (slot-major), then `want` rounds
-// of a block arg-min merge.  Blocks [nfb, nfb + np): the ties F3 partition blockIdx - nfb
-// deferred, a wave per slot (f3_wave_answer on the copied candidates); a slot is freed
-// (count 0) once answered, so the headers are all-zero between calls.
-static_assert(kTieSlots % (kF4Threads / 64) == 0, "F4 waves split a partition's tie slots evenly");
-__global__ __launch_bounds__(kF4Threads) void k_f4_fallback(F3Args a, uint32_t nfb) {
-    extern __shared__ uint2 lst[];            // [want][kF4Threads], then red[kF4Threads / 64]
-    const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
+// ---- F4: the fallback targets (K1 scan, run-time roles) and the deferred ties -------------
+// Blocks [0, nfb): the fallback list (count ctr[0], known only on the device) is answered by
+// the K1 streaming scan over all ids: target groups of 128 (8 waves x 16) x id-range splits,
+// S = min(nfb / groups, 256 / k) so that the chip fills however short the list is; with
+// S > 1 every split writes its sorted candidate records and the last split of a group to
+// finish (agent-scope counter, sc1 records: MI355X_MICROARCH inter-workgroup hand-off)
+// merges the group's S lists per target (a k-way merge over the list heads, one wave per
+// target).  Blocks [nfb, nfb + np): the ties F3 partition blockIdx - nfb deferred, one wave
+// per slot (wave_rank_answer on the copied candidates); a slot is freed (count 0) once
+// answered, so the headers are all-zero between calls.
+constexpr uint32_t kF4Threads = scan::WAVES * 64;                 // 512
+constexpr uint32_t kFbGroup = scan::WAVES * kScanTargets;          // targets per scan role
+constexpr uint32_t kFbBlocks = 256;                                // fallback-scan workgroups
+constexpr uint32_t kFbCands = 256;                                 // merge: splits * k <= 256
+static_assert(kTieSlots == kF4Threads / 64, "one F4 tie block per partition, a wave per slot");
+
+struct FbArgs {
+    uint32_t* rec;    // [kFbBlocks * kFbGroup * k * 6] split lists (S > 1 only)
+    uint32_t* done;   // [kFbBlocks] per-group split completion counters (all-zero between calls)
+    uint32_t nfb;     // fallback-scan blocks at the front of the grid
+};
+
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o));
+    return x;
+}
+
+// merge the S sorted split lists of every target of group g (one wave per target)
+__device__ void fb_merge(const F3Args& a, const FbArgs& f, uint32_t g, uint32_t S, uint32_t cnt, uint32_t* lds) {
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-    if (blockIdx.x >= nfb) {   // one slot per wave; header and candidates in one round trip
-        const uint32_t g = (blockIdx.x - nfb) * (kF4Threads / 64) + wv;
+    const uint32_t k = a.k, nt = cnt - g * kFbGroup < kFbGroup ? cnt - g * kFbGroup : kFbGroup;
+    uint32_t* buf = lds + wv * 2 * kFbCands;   // this wave's candidates: {w0 distance, local index}
+    for (uint32_t j = wv; j < nt; j += scan::WAVES) {
+        const uint32_t qr = __builtin_amdgcn_readfirstlane(a.fb_list[g * kFbGroup + j]);
+        uint32_t t[DHT_W];
+        load_target(a.tp, a.ts, qr, t);
+        for (uint32_t c = lane; c < S * k; c += 64) {
+            const uint32_t l = c / k, r = c - l * k;
+            const uint32_t* src = f.rec + ((((uint64_t)g * S + l) * kFbGroup + j) * k + r) * 6;
+            const uint32_t w0 = ld_sc1(src), ix = ld_sc1(src + 5);
+            buf[2 * c] = ix == DHT_NONE ? DHT_NONE : w0 ^ t[0];
+            buf[2 * c + 1] = ix;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // lane l < S walks list l; each round takes the closest head (full key on a w0 tie)
+        uint32_t p = 0, hd = DHT_NONE, hi = DHT_NONE;
+        if (lane < S) {
+            hd = buf[2 * lane * k];
+            hi = buf[2 * lane * k + 1];
+        }
+        uint32_t* orow = a.out_idx + (uint64_t)qr * k;
+        uint32_t r = 0;
+        for (; r < k; ++r) {
+            const bool valid = hi != DHT_NONE;
+            const uint32_t m = wave_min_u32(valid ? hd : DHT_NONE);
+            const uint64_t cand = __ballot(valid && hd == m);
+            if (!cand) break;
+            uint32_t win = (uint32_t)__ffsll((long long)cand) - 1;
+            if (__popcll(cand) > 1) {
+                uint64_t rest = cand & (cand - 1);
+                while (rest) {
+                    const uint32_t l2 = (uint32_t)__ffsll((long long)rest) - 1;
+                    rest &= rest - 1;
+                    const uint32_t ib = __builtin_amdgcn_readlane((int)hi, (int)win);
+                    const uint32_t i2 = __builtin_amdgcn_readlane((int)hi, (int)l2);
+                    if (id_less(m, i2, m, ib, a.planes, a.stride, t)) win = l2;
+                }
+            }
+            const uint32_t wi = __builtin_amdgcn_readlane((int)hi, (int)win);
+            if (lane == 0) orow[r] = map_out(wi, a.gidx, a.base);
+            if (lane == win) {
+                ++p;
+                hd = p < k ? buf[2 * (lane * k + p)] : DHT_NONE;
+                hi = p < k ? buf[2 * (lane * k + p) + 1] : DHT_NONE;
+            }
+        }
+        for (uint32_t x = r + lane; x < k; x += 64) orow[x] = DHT_NONE;
+        if (lane == 0) a.out_cnt[qr] = r;
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[scan::lds_words<kScanTargets>()];
+    __shared__ uint32_t last;
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    if (blockIdx.x >= f.nfb) {   // deferred ties: one slot per wave, header and candidates in one round trip
+        const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
+        const uint32_t g = (blockIdx.x - f.nfb) * kTieSlots + wv;
         const uint4 h = a.tie_hdr[g];
         const uint2 c = a.tie_cand[(uint64_t)g * 64 + lane];
         const uint32_t mm = __builtin_amdgcn_readfirstlane(h.z);
@@ -862,60 +972,35 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_fallback(F3Args a, uint32_t n
         if (lane == 0) a.tie_hdr[g].z = 0;
         return;
     }
-    const uint32_t cntq = a.ctr[0];
-    const uint32_t* __restrict__ planes = a.planes;
-    const uint64_t stride = a.stride, n = a.n;
-    const uint32_t k = a.k;
-    uint2* red = lst + (size_t)want * kF4Threads;
-    for (uint32_t f = blockIdx.x; f < cntq; f += nfb) {
-        const uint32_t qi = a.fb_list[f];
-        uint32_t t[DHT_W];
-        load_target(a.tp, a.ts, qi, t);
-        uint32_t c = 0, wd = DHT_NONE, wi = DHT_NONE;   // own list length and its worst entry
-        for (uint64_t i = threadIdx.x; i < n; i += kF4Threads) {
-            const uint32_t d = planes[i] ^ t[0];
-            if (c == want && !id_less(d, (uint32_t)i, wd, wi, planes, stride, t)) continue;
-            uint32_t pos = c < want ? c : want - 1;
-            while (pos > 0) {
-                const uint2 prev = lst[(pos - 1) * kF4Threads + threadIdx.x];
-                if (!id_less(d, (uint32_t)i, prev.x, prev.y, planes, stride, t)) break;
-                lst[pos * kF4Threads + threadIdx.x] = prev;
-                --pos;
-            }
-            lst[pos * kF4Threads + threadIdx.x] = make_uint2(d, (uint32_t)i);
-            if (c < want) ++c;
-            if (c == want) {
-                const uint2 w = lst[(want - 1) * kF4Threads + threadIdx.x];
-                wd = w.x;
-                wi = w.y;
-            }
-        }
-        // merge: `want` rounds of block arg-min over the list heads
-        uint32_t ptr = 0;
-        for (uint32_t r = 0; r < want; ++r) {
-            uint2 h = ptr < c ? lst[ptr * kF4Threads + threadIdx.x] : make_uint2(DHT_NONE, DHT_NONE);
-            // wave arg-min (NONE idx = empty, farthest)
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                const uint2 x = make_uint2(__shfl_xor(h.x, o), __shfl_xor(h.y, o));
-                const bool take = x.y != DHT_NONE && (h.y == DHT_NONE || id_less(x.x, x.y, h.x, h.y, planes, stride, t));
-                if (take) h = x;
-            }
-            if (lane == 0) red[wv] = h;
-            __syncthreads();
-            uint2 best = red[0];
-            for (uint32_t w = 1; w < kF4Threads / 64; ++w) {
-                const uint2 x = red[w];
-                if (x.y != DHT_NONE && (best.y == DHT_NONE || id_less(x.x, x.y, best.x, best.y, planes, stride, t)))
-                    best = x;
-            }
-            __syncthreads();
-            if (ptr < c && lst[ptr * kF4Threads + threadIdx.x].y == best.y) ++ptr;   // indices are unique
-            if (threadIdx.x == 0) a.out_idx[(uint64_t)qi * k + r] = map_out(best.y, a.gidx, a.base);
-        }
-        for (uint32_t r = want + threadIdx.x; r < k; r += kF4Threads) a.out_idx[(uint64_t)qi * k + r] = DHT_NONE;
-        if (threadIdx.x == 0) a.out_cnt[qi] = want;
+    const uint32_t cnt = a.ctr[0];
+    if (cnt == 0) return;
+    const uint32_t groups = (cnt + kFbGroup - 1) / kFbGroup;
+    const uint64_t ntiles = (a.n + scan::TILE - 1) / scan::TILE;
+    uint32_t S = f.nfb / groups;
+    const uint32_t smax = kFbCands / a.k;
+    S = S < 1 ? 1u : S > smax ? smax : S;
+    if ((uint64_t)S > ntiles) S = ntiles ? (uint32_t)ntiles : 1u;
+    const uint64_t split_len = (ntiles ? (ntiles + S - 1) / S : 1) * scan::TILE;
+    if (ntiles) S = (uint32_t)((a.n + split_len - 1) / split_len);
+    const uint32_t roles = groups * S;
+    for (uint32_t role = blockIdx.x; role < roles; role += f.nfb) {
+        const uint32_t g = role / S, sp = role - g * S;
+        const uint64_t lo = (uint64_t)sp * split_len, hi = lo + split_len < a.n ? lo + split_len : a.n;
+        const scan::ScanOut o{a.out_idx, a.out_cnt, a.gidx, a.base, S > 1 ? f.rec : nullptr,
+                              (uint64_t)g * kFbGroup * (S - 1) + (uint64_t)sp * kFbGroup, 0u};
+        scan::scan_run<K, kScanTargets>(lds, a.planes, a.stride, lo, hi, a.tp, a.ts, a.fb_list,
+                                        g * kFbGroup + wv * kScanTargets, cnt, a.k, o);
+        if (S == 1) continue;
+        // hand-off: every wave's sc1 record stores drained, then one agent-scope add per block;
+        // the block whose add completes the group merges it (its waves load after the barrier)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (threadIdx.x == 0) last = atomicAdd(f.done + g, 1u) == S - 1 ? 1u : 0u;
+        __syncthreads();
+        if (!last) continue;
+        fb_merge(a, f, g, S, cnt, lds);
+        if (threadIdx.x == 0) f.done[g] = 0;   // all-zero again for the next call
+        __syncthreads();                       // lds is reused by this block's next role
     }
 }
 
@@ -1017,154 +1102,11 @@ size_t f3_lds(const BatchPlan& P) {
     return (size_t)f3_words(nsub) * 4 + (size_t)(kF3Cap + kF3Threads) * 8;
 }
 
-}  // namespace
-
-bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
-    if (k == 0 || k > DHTGPU_MAX_K_DEV || n >= (1ull << 31)) return false;
-    const BatchPlan P = plan_batch(n, q, k, num_cus);
-    if (q > kMaxQ) return false;
-    // dense mode flushes whenever less than one sub-step of room is left
-    if (!P.fits || P.Lm - P.b1 > 13 || (!P.sparse && P.stage < kF2Sub + 1024)) return false;
-    return f3_lds(P) <= kLdsMax && f2_lds(P) <= kLdsMax;
-}
-
-// workspace: bitmap (64 KB) | ctr[64] | pcount[kMaxParts] | tcount[kMaxParts * kCtrStride] |
-// tie_hdr[kMaxParts * kTieSlots] -- all-zero between calls -- | fb_list[q] | tspill[q] |
-// tbuf[np * tcap] | tie_cand[np * kTieSlots * 64] | pbuf[np * kF3Cap]
-constexpr uint32_t kMaxParts = 1u << 13;
-size_t batch_clean_bytes() {
-    return 65536 + 256 + (size_t)kMaxParts * 4 + (size_t)kMaxParts * kCtrStride * 4 + (size_t)kMaxParts * kTieSlots * 16;
-}
-
-size_t batch_bytes(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
-    const BatchPlan P = plan_batch(n, q, k, num_cus);
-    const size_t np = 1ull << P.b1;
-    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    return batch_clean_bytes() + 2 * al((size_t)q * 4) + al(np * 4) + al(np * P.tcap * 8) + al(np * kTieSlots * 64 * 8) +
-           al(np * kF3Cap * 8);
-}
-
-hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t* stats4,
-                            hipStream_t s) {
-    const BatchPlan P = plan_batch(n, q, k, num_cus);
-    const size_t np = 1ull << P.b1;
-    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const uint8_t* w = static_cast<const uint8_t*>(ws);
-    std::vector<uint32_t> ps(np);
-    hipError_t e = hipMemcpyAsync(stats4, w + 65536, 16, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(ps.data(), w + batch_clean_bytes() + 2 * al((size_t)q * 4), np * 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    uint64_t tot = 0;
-    for (uint32_t v : ps) tot += v;
-    stats4[1] = (uint32_t)tot;   // survivors = sum over partitions
-    return e;
-}
-
-__global__ void k_shift_w0(const uint32_t* __restrict__ planes, uint64_t stride, uint32_t shift,
-                           uint32_t* __restrict__ out) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < stride) out[i] = (planes[i] << shift) | (planes[stride + i] >> (32 - shift));
-}
-
-hipError_t launch_shift_w0(const uint32_t* planes, uint64_t stride, uint32_t shift, uint32_t* out, hipStream_t s) {
-    if (shift == 0 || shift >= 32) return hipErrorInvalidValue;
-    k_shift_w0<<<dim3((uint32_t)((stride + 255) / 256)), dim3(256), 0, s>>>(planes, stride, shift, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp,
-                             uint64_t ts, uint32_t q, uint32_t k, const uint32_t* gidx, uint32_t base,
-                             uint32_t* out_idx, uint32_t* out_cnt, int num_cus, uint32_t skip,
-                             const uint32_t* w0s, hipStream_t s, hipEvent_t* ev) {
-    if (skip && !w0s) return hipErrorInvalidValue;
-    if (!q) return hipSuccess;
-    const BatchPlan P = plan_batch(n, q, k, num_cus);
-    const uint32_t np = 1u << P.b1;
-    uint8_t* w = static_cast<uint8_t*>(ws);
-    auto take = [&](size_t bytes) {
-        uint8_t* r = w;
-        w += (bytes + 255) & ~size_t(255);
-        return r;
-    };
-    uint32_t* bitmap = reinterpret_cast<uint32_t*>(take(65536));
-    uint32_t* ctr = reinterpret_cast<uint32_t*>(take(256));
-    uint32_t* pcount = reinterpret_cast<uint32_t*>(take((size_t)kMaxParts * 4));
-    uint32_t* tcount = reinterpret_cast<uint32_t*>(take((size_t)kMaxParts * kCtrStride * 4));
-    uint4* tie_hdr = reinterpret_cast<uint4*>(take((size_t)kMaxParts * kTieSlots * 16));
-    uint32_t* fb_list = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
-    uint32_t* tspill = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
-    uint32_t* pstat = reinterpret_cast<uint32_t*>(take((size_t)np * 4));
-    uint2* tbuf = reinterpret_cast<uint2*>(take((size_t)np * P.tcap * 8));
-    uint2* tie_cand = reinterpret_cast<uint2*>(take((size_t)np * kTieSlots * 64 * 8));
-    uint2* pbuf = reinterpret_cast<uint2*>(take((size_t)np * kF3Cap * 8));
-    static bool attr_set = false;
-    if (!attr_set) {
-        const void* f2s[] = {(const void*)k_f2_filter<kF2Dense>, (const void*)k_f2_filter<kF2Sparse>,
-                             (const void*)k_f2_filter<kF2Stream>};
-        for (const void* f : f2s) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
-        const void* f3s[] = {(const void*)k_f3_answer<8, false, true>,  (const void*)k_f3_answer<16, false, true>,
-                             (const void*)k_f3_answer<32, false, true>, (const void*)k_f3_answer<8, true, true>,
-                             (const void*)k_f3_answer<16, true, true>,  (const void*)k_f3_answer<32, true, true>,
-                             (const void*)k_f3_answer<8, false, false>, (const void*)k_f3_answer<16, false, false>,
-                             (const void*)k_f3_answer<32, false, false>, (const void*)k_f3_answer<8, true, false>,
-                             (const void*)k_f3_answer<16, true, false>, (const void*)k_f3_answer<32, true, false>};
-        for (const void* f : f3s) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
-        attr_set = true;
-    }
-    static const uint32_t dbg = getenv("DHTGPU_DBG") ? (uint32_t)atoi(getenv("DHTGPU_DBG")) : 0u;
-    // ev (diagnostics): 8 events, a start/stop pair per kernel recorded by the kernel's own
-    // dispatch (hipExtLaunchKernel), so the pairs time the kernels themselves
-    auto go = [&](int i, auto kern, dim3 g, dim3 b, size_t lds, auto... args) {
-        if (ev) hipExtLaunchKernelGGL(kern, g, b, (uint32_t)lds, s, ev[2 * i], ev[2 * i + 1], 0, args...);
-        else kern<<<g, b, lds, s>>>(args...);
-    };
-    static unsigned long long* stamps = nullptr;   // dbg & 256: F3 [8192][16] then F2 [8192][16]
-    if ((dbg & 256) && !stamps) (void)hipMalloc(&stamps, (size_t)2 * 8192 * 16 * 8);
-    if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)2 * 8192 * 16 * 8, s);
-    go(0, k_f1_targets, dim3(P.nblk1), dim3(kF1Threads), 0, tp, tp + ts, q, P.Lm, P.b1, skip, bitmap, tcount, tbuf,
-       P.tcap, ctr, tspill);
-    if (n) {
-        // F2 streams word 0, or the shifted word-0 plane of a prefix shard (stride words)
-        const uint64_t lim = (w0s ? stride : 5 * stride) - 4;
-        F2Args a2{w0s ? w0s : planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, kF3Cap, ctr, P.stage, dbg,
-                  (uint32_t)(lim < 0xFFFFFFF0ull ? lim : 0xFFFFFFF0ull), P.sparse,
-                  stamps ? stamps + 8192 * 16 : nullptr};
-        const dim3 g2(P.nblk2), b2(kF2Threads);
-        const size_t l2 = f2_lds(P);
-        if (dbg & 64) go(1, k_f2_filter<kF2Stream>, g2, b2, l2, a2);
-        else if (P.sparse) go(1, k_f2_filter<kF2Sparse>, g2, b2, l2, a2);
-        else go(1, k_f2_filter<kF2Dense>, g2, b2, l2, a2);
-    } else if (ev) {
-        (void)hipEventRecord(ev[2], s);
-        (void)hipEventRecord(ev[3], s);
-    }
-    if (dbg & ~(48u | 256u | 512u | 1024u | 2048u | 4096u | 8192u)) {   // experiments: F1 + F2 only
-        for (int i = 4; ev && i < 8; ++i) (void)hipEventRecord(ev[i], s);
-        return hipGetLastError();
-    }
-    F3Args a{pbuf, pcount, kF3Cap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, planes, stride, n,
-             tp, ts, k, gidx, base, out_idx, out_cnt, ctr, fb_list, pstat, tie_hdr, tie_cand, dbg, stamps};
-    size_t l3 = f3_lds(P);
-    if (dbg & 4096) l3 = l3 > 81920 ? l3 : 81920;   // experiment: 2 F3 blocks per CU
-    if (dbg & 8192) l3 = l3 > 54000 ? l3 : 54000;   // experiment: 3 F3 blocks per CU
-    const dim3 g3(np), b3(kF3Threads);
-    const bool ex = n >= k && (k == 8 || k == 16 || k == 32);
-#define F3_GO(KK, DD)                                                         \
-    do {                                                                      \
-        if (ex) go(2, k_f3_answer<KK, DD, true>, g3, b3, l3, a);            \
-        else go(2, k_f3_answer<KK, DD, false>, g3, b3, l3, a);              \
-    } while (0)
-    if (dbg) {
-        if (k <= 8) F3_GO(8, true);
-        else if (k <= 16) F3_GO(16, true);
-        else F3_GO(32, true);
-    } else {
-        if (k <= 8) F3_GO(8, false);
-        else if (k <= 16) F3_GO(16, false);
-        else F3_GO(32, false);
-    }
-#undef F3_GO
+// DHTGPU_DBG=256: per-block phase profiles of F2 and F3 from their s_memrealtime stamps
+// (100 MHz real-time counter: 10 ns ticks), printed to stderr (synchronises s)
+void print_phase_profile(const BatchPlan& P, uint32_t np, unsigned long long* stamps, hipStream_t s) {
+    if (!stamps) return;
+    const uint32_t dbg = 256;
     if (dbg & 256) {   // phase profile of F2 (100 MHz real-time stamps: 10 ns ticks)
         std::vector<unsigned long long> h((size_t)P.nblk2 * 16);
         (void)hipMemcpyAsync(h.data(), stamps + 8192 * 16, h.size() * 8, hipMemcpyDeviceToHost, s);
@@ -1257,10 +1199,231 @@ hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, 
             fprintf(stderr, "  start %s\n  end   %s\n", pct(st).c_str(), pct(en).c_str());
         }
     }
-    const uint32_t want = n < k ? (uint32_t)n : k;
-    constexpr uint32_t kFbBlocks = 64;
-    go(3, k_f4_fallback, dim3(kFbBlocks + np * (kTieSlots / (kF4Threads / 64))), dim3(kF4Threads),
-       ((size_t)want * kF4Threads + kF4Threads / 64) * 8, a, kFbBlocks);
+}
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) applies to the device current at the call:
+// once per device, from whichever thread gets there first
+constexpr int kMaxDevices = 64;
+std::once_flag g_attr_once[kMaxDevices];
+
+void set_lds_attributes() {
+    const void* fs[] = {(const void*)k_f2_filter<kF2Dense>, (const void*)k_f2_filter<kF2Sparse>,
+                        (const void*)k_f2_filter<kF2Stream>,
+                        (const void*)k_f3_answer<8, false, true>,  (const void*)k_f3_answer<16, false, true>,
+                        (const void*)k_f3_answer<32, false, true>, (const void*)k_f3_answer<8, true, true>,
+                        (const void*)k_f3_answer<16, true, true>,  (const void*)k_f3_answer<32, true, true>,
+                        (const void*)k_f3_answer<8, false, false>, (const void*)k_f3_answer<16, false, false>,
+                        (const void*)k_f3_answer<32, false, false>, (const void*)k_f3_answer<8, true, false>,
+                        (const void*)k_f3_answer<16, true, false>, (const void*)k_f3_answer<32, true, false>};
+    for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
+}
+
+// workspace: bitmap (64 KB) | ctr[64] | pcount[kMaxParts] | tcount[kMaxParts * kCtrStride] |
+// tie_hdr[kMaxParts * kTieSlots] | fb done[kFbBlocks] -- all-zero between calls -- | fb_list[q] |
+// tspill[q] | pstat[np] | tbuf[np * tcap] | tie_cand[np * kTieSlots * 64] | pbuf[np * kF3Cap] |
+// fb rec[kFbBlocks * kFbGroup * k * 6]
+constexpr uint32_t kMaxParts = 1u << 13;
+inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
+
+}  // namespace
+
+bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
+    if (k == 0 || k > DHTGPU_MAX_K_DEV || n >= (1ull << 31)) return false;
+    const BatchPlan P = plan_batch(n, q, k, num_cus);
+    if (q > kMaxQ) return false;
+    // dense mode flushes whenever less than one sub-step of room is left
+    if (!P.fits || P.Lm - P.b1 > 13 || (!P.sparse && P.stage < kF2Sub + 1024)) return false;
+    return f3_lds(P) <= kLdsMax && f2_lds(P) <= kLdsMax;
+}
+
+size_t batch_clean_bytes() {
+    return 65536 + 256 + (size_t)kMaxParts * 4 + (size_t)kMaxParts * kCtrStride * 4 + (size_t)kMaxParts * kTieSlots * 16 +
+           al256((size_t)kFbBlocks * 4);
+}
+
+size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus) {
+    const BatchPlan P = plan_batch(n, q_plan, k, num_cus);
+    const size_t np = 1ull << P.b1;
+    return batch_clean_bytes() + 2 * al256((size_t)q * 4) + al256(np * 4) + al256(np * P.tcap * 8) +
+           al256(np * kTieSlots * 64 * 8) + al256(np * kF3Cap * 8) + al256((size_t)kFbBlocks * kFbGroup * k * 24);
+}
+
+hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus,
+                            uint32_t* stats4, hipStream_t s) {
+    const BatchPlan P = plan_batch(n, q_plan, k, num_cus);
+    const size_t np = 1ull << P.b1;
+    const uint8_t* w = static_cast<const uint8_t*>(ws);
+    std::vector<uint32_t> ps(np);
+    hipError_t e = hipMemcpyAsync(stats4, w + 65536, 16, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(ps.data(), w + batch_clean_bytes() + 2 * al256((size_t)q * 4), np * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    uint64_t tot = 0;
+    for (uint32_t v : ps) tot += v;
+    stats4[1] = (uint32_t)tot;   // survivors = sum over partitions
+    return e;
+}
+
+__global__ void k_shift_w0(const uint32_t* __restrict__ planes, uint64_t stride, uint32_t shift,
+                           uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < stride) out[i] = (planes[i] << shift) | (planes[stride + i] >> (32 - shift));
+}
+
+hipError_t launch_shift_w0(const uint32_t* planes, uint64_t stride, uint32_t shift, uint32_t* out, hipStream_t s) {
+    if (shift == 0 || shift >= 32) return hipErrorInvalidValue;
+    k_shift_w0<<<dim3((uint32_t)((stride + 255) / 256)), dim3(256), 0, s>>>(planes, stride, shift, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
+    if (dirty) *dirty = false;
+    if (c.skip && !c.w0s) return hipErrorInvalidValue;
+    if (!c.q) return hipSuccess;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDevices) std::call_once(g_attr_once[dev], set_lds_attributes);
+    const uint64_t n = c.n;
+    const uint32_t q = c.q, k = c.k;
+    const BatchPlan P = plan_batch(n, c.q_plan, k, c.num_cus);
+    const uint32_t np = 1u << P.b1;
+    const uint32_t dbg = c.dbg;
+    hipEvent_t* ev = c.ev;
+    uint8_t* w = static_cast<uint8_t*>(c.ws);
+    auto take = [&](size_t bytes) {
+        uint8_t* r = w;
+        w += al256(bytes);
+        return r;
+    };
+    uint32_t* bitmap = reinterpret_cast<uint32_t*>(take(65536));
+    uint32_t* ctr = reinterpret_cast<uint32_t*>(take(256));
+    uint32_t* pcount = reinterpret_cast<uint32_t*>(take((size_t)kMaxParts * 4));
+    uint32_t* tcount = reinterpret_cast<uint32_t*>(take((size_t)kMaxParts * kCtrStride * 4));
+    uint4* tie_hdr = reinterpret_cast<uint4*>(take((size_t)kMaxParts * kTieSlots * 16));
+    uint32_t* fb_done = reinterpret_cast<uint32_t*>(take((size_t)kFbBlocks * 4));
+    uint32_t* fb_list = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
+    uint32_t* tspill = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
+    uint32_t* pstat = reinterpret_cast<uint32_t*>(take((size_t)np * 4));
+    uint2* tbuf = reinterpret_cast<uint2*>(take((size_t)np * P.tcap * 8));
+    uint2* tie_cand = reinterpret_cast<uint2*>(take((size_t)np * kTieSlots * 64 * 8));
+    uint2* pbuf = reinterpret_cast<uint2*>(take((size_t)np * kF3Cap * 8));
+    uint32_t* fb_rec = reinterpret_cast<uint32_t*>(take((size_t)kFbBlocks * kFbGroup * k * 24));
+    // ev (diagnostics): 8 events, a start/stop pair per kernel recorded by the kernel's own
+    // dispatch (hipExtLaunchKernel), so the pairs time the kernels themselves
+    auto go = [&](int i, auto kern, dim3 g, dim3 b, size_t lds, auto... args) {
+        if (ev) hipExtLaunchKernelGGL(kern, g, b, (uint32_t)lds, s, ev[2 * i], ev[2 * i + 1], 0, args...);
+        else kern<<<g, b, lds, s>>>(args...);
+    };
+    unsigned long long* stamps = (dbg & 256) ? c.stamps : nullptr;   // F3 [8192][16] then F2 [8192][16]
+    if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)2 * 8192 * 16 * 8, s);
+    go(0, k_f1_targets, dim3((q + kF1Threads - 1) / kF1Threads), dim3(kF1Threads), 0, c.tp, c.tp + c.ts, q, P.Lm, P.b1,
+       c.skip, c.sel_shift, c.sel_bits, c.sel_val, bitmap, tcount, tbuf, P.tcap, ctr, tspill);
+    const uint32_t* planes = c.planes;
+    const uint64_t stride = c.stride;
+    if (n) {
+        // F2 streams word 0, or the shifted word-0 plane of a prefix shard (stride words)
+        const uint64_t lim = (c.w0s ? stride : 5 * stride) - 4;
+        F2Args a2{c.w0s ? c.w0s : planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, kF3Cap, ctr, P.stage, dbg,
+                  (uint32_t)(lim < 0xFFFFFFF0ull ? lim : 0xFFFFFFF0ull), P.sparse,
+                  stamps ? stamps + 8192 * 16 : nullptr};
+        const dim3 g2(P.nblk2), b2(kF2Threads);
+        const size_t l2 = f2_lds(P);
+        if (dbg & 64) go(1, k_f2_filter<kF2Stream>, g2, b2, l2, a2);
+        else if (P.sparse) go(1, k_f2_filter<kF2Sparse>, g2, b2, l2, a2);
+        else go(1, k_f2_filter<kF2Dense>, g2, b2, l2, a2);
+    } else if (ev) {
+        (void)hipEventRecord(ev[2], s);
+        (void)hipEventRecord(ev[3], s);
+    }
+    if (dbg & ~(48u | 256u | 512u | 1024u | 2048u | 4096u | 8192u)) {   // experiments: F1 + F2 only
+        for (int i = 4; ev && i < 8; ++i) (void)hipEventRecord(ev[i], s);
+        if (dirty) *dirty = true;   // F3 (which resets the counters and the bitmap) did not run
+        return hipGetLastError();
+    }
+    if (dirty && (dbg & 48u)) *dirty = true;   // F3 ablation exits leave counters behind
+    F3Args a{pbuf, pcount, kF3Cap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, planes, stride, n,
+             c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, pstat, tie_hdr, tie_cand, dbg, stamps};
+    size_t l3 = f3_lds(P);
+    if (dbg & 4096) l3 = l3 > 81920 ? l3 : 81920;   // experiment: 2 F3 blocks per CU
+    if (dbg & 8192) l3 = l3 > 54000 ? l3 : 54000;   // experiment: 3 F3 blocks per CU
+    const dim3 g3(np), b3(kF3Threads);
+    const bool ex = n >= k && (k == 8 || k == 16 || k == 32);
+#define F3_GO(KK, DD)                                                         \
+    do {                                                                      \
+        if (ex) go(2, k_f3_answer<KK, DD, true>, g3, b3, l3, a);            \
+        else go(2, k_f3_answer<KK, DD, false>, g3, b3, l3, a);              \
+    } while (0)
+    if (dbg) {
+        if (k <= 8) F3_GO(8, true);
+        else if (k <= 16) F3_GO(16, true);
+        else F3_GO(32, true);
+    } else {
+        if (k <= 8) F3_GO(8, false);
+        else if (k <= 16) F3_GO(16, false);
+        else F3_GO(32, false);
+    }
+#undef F3_GO
+    if (dbg & 256) print_phase_profile(P, np, stamps, s);
+    const FbArgs fa{fb_rec, fb_done, kFbBlocks};
+    const dim3 g4(kFbBlocks + np), b4(kF4Threads);
+    if (k <= 8) go(3, k_f4<8>, g4, b4, 0, a, fa);
+    else if (k <= 16) go(3, k_f4<16>, g4, b4, 0, a, fa);
+    else go(3, k_f4<32>, g4, b4, 0, a, fa);
+    return hipGetLastError();
+}
+
+
+// ---- target routing for prefix sub-partitions -------------------------------------------
+// list[*cnt++] = i for every target whose bits [sel_shift, sel_shift + sel_bits) hold a value
+// v with bit v set in mask (order within the list does not matter: results are written to
+// the targets' own rows)
+__global__ __launch_bounds__(256) void k_select_targets(const uint32_t* __restrict__ tw0, uint32_t q, uint32_t sel_shift,
+                                                        uint32_t sel_bits, const uint32_t* __restrict__ mask,
+                                                        uint32_t* __restrict__ list, uint32_t* __restrict__ cnt) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t v = i < q ? (tw0[i] << sel_shift) >> (32 - sel_bits) : 0u;
+    const bool take = i < q && ((mask[v >> 5] >> (v & 31)) & 1u);
+    const uint64_t b = __ballot(take);
+    if (!b) return;
+    const uint32_t lane = lane_id(), first = (uint32_t)__ffsll((long long)b) - 1;
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(cnt, (uint32_t)__popcll(b));
+    base = (uint32_t)__shfl((int)base, (int)first);
+    if (take) list[base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = i;
+}
+
+hipError_t launch_select_targets(const uint32_t* tw0, uint32_t q, uint32_t sel_shift, uint32_t sel_bits,
+                                 const uint32_t* d_mask, uint32_t* list, uint32_t* d_cnt, hipStream_t s) {
+    if (sel_bits == 0 || sel_bits > 16 || sel_shift + sel_bits > 32) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(d_cnt, 0, 4, s);
+    if (e != hipSuccess || !q) return e;
+    k_select_targets<<<(q + 255) / 256, 256, 0, s>>>(tw0, q, sel_shift, sel_bits, d_mask, list, d_cnt);
+    return hipGetLastError();
+}
+
+size_t list_scan_bytes(uint32_t k) { return al256((size_t)kFbBlocks * 4) + al256((size_t)kFbBlocks * kFbGroup * k * 24); }
+
+hipError_t launch_list_scan(const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp, uint64_t ts,
+                            uint32_t k, const uint32_t* list, const uint32_t* d_cnt, const uint32_t* gidx, uint32_t base,
+                            uint32_t* out_idx, uint32_t* out_cnt, void* scratch, hipStream_t s) {
+    uint8_t* w = static_cast<uint8_t*>(scratch);
+    F3Args a{};
+    a.planes = planes;
+    a.stride = stride;
+    a.n = n;
+    a.tp = tp;
+    a.ts = ts;
+    a.k = k;
+    a.gidx = gidx;
+    a.base = base;
+    a.out_idx = out_idx;
+    a.out_cnt = out_cnt;
+    a.ctr = const_cast<uint32_t*>(d_cnt);          // F4 reads the list length from ctr[0]
+    a.fb_list = const_cast<uint32_t*>(list);
+    const FbArgs fa{reinterpret_cast<uint32_t*>(w + al256((size_t)kFbBlocks * 4)), reinterpret_cast<uint32_t*>(w),
+                    kFbBlocks};
+    if (k <= 8) k_f4<8><<<kFbBlocks, kF4Threads, 0, s>>>(a, fa);
+    else if (k <= 16) k_f4<16><<<kFbBlocks, kF4Threads, 0, s>>>(a, fa);
+    else k_f4<32><<<kFbBlocks, kF4Threads, 0, s>>>(a, fa);
     return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@ namespace dhtgpu {
 constexpr uint32_t kTile = 4096;
 constexpr uint32_t kScanWaves = 8;       // waves per scan workgroup
 constexpr uint32_t kScanTargets = 16;    // targets held (wave-uniform) per wave
+constexpr uint32_t kLdsBytes = 160 * 1024;   // LDS per CU (gfx950)
 
 inline uint64_t pad_ids(uint64_t n) { return ((n + kTile - 1) / kTile) * kTile; }
 
@@ -41,11 +42,14 @@ struct ScanPlan {
     uint32_t splits;     // id-range splits
     uint64_t split_len;  // ids per split (multiple of kTile)
 };
-ScanPlan plan_scan(uint64_t n, uint32_t q, int num_cus);
+// splits are capped so that K3 can stage splits * k records (24 B) of a target in LDS
+ScanPlan plan_scan(uint64_t n, uint32_t q, uint32_t k, int num_cus);
+// final form: out_idx/out_cnt mapped through gidx (nullable) or offset by idx_base;
+// record form (out_rec != nullptr): rec[((split * q) + qi) * k + r] * 6, idx offset by idx_base
 hipError_t launch_scan(const uint32_t* ids, uint64_t is, uint64_t n, const ScanPlan& p,
                        const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k,
                        uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec,
-                       uint32_t idx_base, hipStream_t s);
+                       const uint32_t* gidx, uint32_t idx_base, hipStream_t s);
 hipError_t launch_merge(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_t kin,
                         const uint32_t* tp, uint64_t ts, uint32_t k, uint32_t* out_idx,
                         uint32_t* out_cnt, hipStream_t s);
@@ -67,7 +71,8 @@ hipError_t launch_find_closest(uint32_t nb, const uint32_t* fp, const uint32_t* 
 hipError_t launch_classify(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t nb,
                            const uint32_t* fp, const uint32_t* myid, uint8_t* out_bucket,
                            unsigned long long* hist, hipStream_t s);
-hipError_t launch_cached(const uint32_t* planes, uint64_t stride, uint64_t n,
+// perm (nullable): sorted position -> caller index (accept and the output use caller indices)
+hipError_t launch_cached(const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* perm,
                          const uint8_t* accept, const uint32_t* tp, uint64_t ts, uint32_t q,
                          uint32_t count, uint32_t* out_idx, uint32_t* out_cnt, hipStream_t s);
 
@@ -82,22 +87,54 @@ hipError_t launch_index_query(const void* ws, uint64_t n, uint32_t B, const uint
                               uint32_t* out_cnt, hipStream_t s);
 
 // batch.hip: K6 per-batch target-prefix filter + exact top-k (no persistent index).
-// out_idx/out_cnt indices are mapped through gidx (nullable) or offset by base.
-// ev (nullable): 5 events recorded around F1, F2, F3, F4.
-bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus);
-size_t batch_bytes(uint64_t n, uint32_t q, uint32_t k, int num_cus);
+// q_plan: targets the call is planned for (= q, or the expected share of a sub-partition call
+// whose F1 keeps only the targets of its prefix).
+bool batch_supported(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus);
+size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus);
 // leading workspace bytes that must be zero before the first call (they are left zero)
 size_t batch_clean_bytes();
-// device address of {fallback targets, survivors} of the last call on workspace ws
-// stats4 = {fallback targets, survivors, wave-path targets, 0} of the last call (synchronises s)
-hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t* stats4,
-                            hipStream_t s);
+// stats4 = {fallback targets, survivors, wave-path targets, 0} of the last call on workspace ws
+// (synchronises s)
+hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus,
+                            uint32_t* stats4, hipStream_t s);
 // prefix shards: out[i] = planes word 0 << shift | word 1 >> (32 - shift), i < stride
 hipError_t launch_shift_w0(const uint32_t* planes, uint64_t stride, uint32_t shift, uint32_t* out, hipStream_t s);
-hipError_t launch_batch_topk(void* ws, const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp,
-                             uint64_t ts, uint32_t q, uint32_t k, const uint32_t* gidx, uint32_t base,
-                             uint32_t* out_idx, uint32_t* out_cnt, int num_cus, uint32_t skip,
-                             const uint32_t* w0s, hipStream_t s, hipEvent_t* ev = nullptr);
+struct BatchCall {
+    void* ws;                              // workspace (batch_bytes), head zero (batch_clean_bytes)
+    const uint32_t* planes; uint64_t stride; uint64_t n;   // the id set (unshifted word planes)
+    const uint32_t* tp; uint64_t ts;       // target planes
+    uint32_t q;                            // targets F1 reads (the whole batch)
+    uint32_t q_plan;                       // targets the plan is sized for
+    uint32_t k;
+    uint32_t sel_shift, sel_bits, sel_val; // F1 keeps targets whose bits [sel_shift, +sel_bits) == sel_val
+    uint32_t skip; const uint32_t* w0s;    // w0s = 32 id bits from bit `skip` (every id shares its top skip bits)
+    const uint32_t* gidx; uint32_t base;   // result index map (nullable) or offset
+    uint32_t* out_idx; uint32_t* out_cnt;  // rows of the ORIGINAL target indices
+    int num_cus;
+    uint32_t dbg;                          // DHTGPU_DBG experiment switches (0 in production)
+    unsigned long long* stamps;            // dbg & 256: phase stamps [2 * 8192 * 16]
+    hipEvent_t* ev;                        // nullable: 8 events around F1..F4
+};
+// *dirty (nullable) = an experiment exit skipped the kernels that re-zero the workspace head
+hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty);
+// list[] = the targets whose bits [sel_shift, +sel_bits) (sel_bits <= 16) hold a value whose bit
+// is set in d_mask; *d_cnt = their number (zeroed first)
+hipError_t launch_select_targets(const uint32_t* tw0, uint32_t q, uint32_t sel_shift, uint32_t sel_bits,
+                                 const uint32_t* d_mask, uint32_t* list, uint32_t* d_cnt, hipStream_t s);
+// exact top-k of the listed targets (count *d_cnt, on the device) by the K1 scan over the id
+// set, results in the targets' own rows (K6's F4 fallback pass run on its own); scratch:
+// list_scan_bytes(k), its first kFbBlocks words zero before the first call (left zero)
+size_t list_scan_bytes(uint32_t k);
+hipError_t launch_list_scan(const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp, uint64_t ts,
+                            uint32_t k, const uint32_t* list, const uint32_t* d_cnt, const uint32_t* gidx, uint32_t base,
+                            uint32_t* out_idx, uint32_t* out_cnt, void* scratch, hipStream_t s);
+
+// sort.hip: lexicographic sort of an id set (stable LSD radix over the 160-bit keys).
+// out_planes (out_stride >= n) = the ids in ascending InfoHash order, perm[j] = the input index
+// of sorted id j; *unique = 0 when two ids are equal.  Synchronises s.
+size_t sort_scratch_bytes(uint64_t n);
+hipError_t launch_sort_ids(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t* out_planes, uint64_t out_stride,
+                           uint32_t* perm, void* scratch, int* unique, hipStream_t s);
 
 // wire.hip: NetworkEngine::bufferNodes / deserializeNodes (compact node records)
 hipError_t launch_wire_encode(const uint32_t* planes, uint64_t stride, const uint8_t* tail, uint32_t alen,

@@ -171,10 +171,13 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
 // ---------------------------------------------------------------------------------
 // a8.  One thread per target: lower_bound over the lexicographically sorted planes,
 // then the reference's two-pointer walk (take the XOR-closer of prev/next; accept
-// iff the accept bit is set), emitting accepted nodes in walk order.
+// iff the accept bit is set), emitting accepted nodes in walk order.  perm (nullable)
+// maps a sorted position to the caller's index (an unsorted upload sorted on the
+// device, sort.hip); accept and the output are in the caller's index space.
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_cached(const uint32_t* __restrict__ planes,
                                                 uint64_t stride, uint64_t n,
+                                                const uint32_t* __restrict__ perm,
                                                 const uint8_t* __restrict__ accept,
                                                 const uint32_t* __restrict__ tp, uint64_t ts,
                                                 uint32_t q, uint32_t count,
@@ -215,7 +218,8 @@ __global__ __launch_bounds__(256) void k_cached(const uint32_t* __restrict__ pla
                 it = it_n++;
             }
         }
-        if (!accept || accept[it]) out_idx[(uint64_t)qi * count + c++] = (uint32_t)it;
+        const uint32_t id = perm ? perm[it] : (uint32_t)it;
+        if (!accept || accept[id]) out_idx[(uint64_t)qi * count + c++] = id;
     }
     out_cnt[qi] = c;
     for (uint32_t r = c; r < count; ++r) out_idx[(uint64_t)qi * count + r] = DHT_NONE;
@@ -251,11 +255,11 @@ hipError_t launch_classify(const uint32_t* planes, uint64_t stride, uint64_t n, 
     return hipGetLastError();
 }
 
-hipError_t launch_cached(const uint32_t* planes, uint64_t stride, uint64_t n,
+hipError_t launch_cached(const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* perm,
                          const uint8_t* accept, const uint32_t* tp, uint64_t ts, uint32_t q,
                          uint32_t count, uint32_t* out_idx, uint32_t* out_cnt, hipStream_t s) {
     if (!q) return hipSuccess;
-    k_cached<<<(q + 255) / 256, 256, 0, s>>>(planes, stride, n, accept, tp, ts, q, count, out_idx, out_cnt);
+    k_cached<<<(q + 255) / 256, 256, 0, s>>>(planes, stride, n, perm, accept, tp, ts, q, count, out_idx, out_cnt);
     return hipGetLastError();
 }
 

@@ -105,6 +105,35 @@ int main(int argc, char** argv) {
         for (uint32_t r = 0; r < c; ++r)
             if (std::memcmp(got[r]->id.data(), &sorted[20 * want[r]], 20)) ++bad;
     }
+    // the versioned form (upload skipped while the map is unchanged) gives the same nodes
+    for (int i = 0; i < 50; ++i) {
+        auto a = dhtgpu::getCachedNodes(ctx, cache, targets[i], 14, 7);
+        auto b = dhtgpu::getCachedNodes(ctx, cache, targets[i], 14, 7);
+        auto c0 = dhtgpu::getCachedNodes(ctx, cache, targets[i], 14);
+        if (a != b || a != c0) ++bad;
+    }
+    // a ClosestIndex keeps answering over ITS id set across getCachedNodes / bufferNodesBatch
+    // calls on the same Context (they use the context's NodeCache mirror / their own nodes)
+    {
+        const size_t nid = 30000, q = 200;
+        std::vector<uint8_t> kb(20 * nid);
+        orc_gen_ids(555, 0, nid, kb.data());
+        std::vector<mock::InfoHash> kid(nid);
+        for (size_t i = 0; i < nid; ++i) std::memcpy(kid[i].d.data(), &kb[20 * i], 20);
+        dhtgpu::ClosestIndex index(ctx);
+        index.assign(kid.data(), nid);
+        std::vector<uint32_t> want(q * 8), wcnt(q);
+        orc_topk(kb.data(), nid, tb.data(), q, 8, want.data(), wcnt.data(), 4);
+        auto before = index.query(targets.data(), q, 8);
+        auto unused = dhtgpu::getCachedNodes(ctx, cache, targets[0], 14);
+        (void)unused;
+        auto after = index.query(targets.data(), q, 8);
+        for (size_t i = 0; i < q; ++i) {
+            if (before[i] != after[i] || after[i].size() != wcnt[i]) { ++bad; continue; }
+            for (uint32_t r = 0; r < wcnt[i]; ++r)
+                if (after[i][r] != want[i * 8 + r]) ++bad;
+        }
+    }
     std::printf("adapter_check: %d mismatches\n", bad);
     return bad ? 1 : 0;
 }

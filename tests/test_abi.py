@@ -36,7 +36,7 @@ def test_ctypes_load_and_strerror():
     for s in header_symbols():
         assert hasattr(L, s)
     assert L.dhtgpu_strerror(0) == b"ok"
-    assert L.dhtgpu_strerror(-5).startswith(b"id set is not")
+    assert L.dhtgpu_strerror(-5).startswith(b"id set holds duplicate")
 
 
 def test_cpp_adapter_header_compiles(tmp_path):

@@ -183,11 +183,55 @@ def test_cached_nodes_vs_oracle(ctx):
             assert list(got[qi, : cnt[qi]]) == list(want)
 
 
-def test_cached_nodes_requires_sorted(ctx):
+def test_cached_nodes_unsorted_upload(ctx):
+    """f2: an id set uploaded in arbitrary order is sorted on the device (LSD radix over the
+    160-bit keys) and walked like NodeCache's std::map; indices refer to the caller's order.
+    Duplicates are refused (a map has unique keys)."""
     import opendht_amd
-    ctx.set_ids(O.gen_ids(23, 100))
-    with pytest.raises(opendht_amd.DhtGpuError):
+    ids = O.gen_ids(24, 30000)
+    ids[:3000, :8] = ids[0, :8]           # equal (w0, w1): the full 160-bit sort path
+    rng = np.random.default_rng(4)
+    perm = rng.permutation(ids.shape[0])
+    shuffled = ids[perm]
+    order = np.lexsort(shuffled.T[::-1])
+    srt = shuffled[order]
+    acc = (rng.random(ids.shape[0]) < 0.8).astype(np.uint8)   # caller order
+    ctx.set_ids(shuffled)
+    tg = np.concatenate([O.gen_ids(25, 300), shuffled[:20], ids[:10]])
+    got, cnt = ctx.cached_nodes(tg, 14, acc)
+    for qi in range(tg.shape[0]):
+        want = O.cached_nodes(srt, acc[order], tg[qi], 14)
+        assert list(got[qi, : cnt[qi]]) == list(order[want]), qi
+    ctx.set_ids(np.concatenate([ids[:100], ids[50:51]]))
+    with pytest.raises(opendht_amd.DhtGpuError) as ei:
         ctx.cached_nodes(O.gen_ids(1, 2), 8)
+    assert ei.value.code == -5
+
+
+def test_cache_mirror_1e6(ctx):
+    """The NodeCache mirror at 10^6 entries uploaded unsorted: its device sort equals the host
+    lexicographic order, getCachedNodes equals the oracle walk, the k-NN id set of the same
+    context is untouched, and a repeated version skips the upload."""
+    n = 1_000_000
+    keys = O.gen_ids(31337, n)
+    rng = np.random.default_rng(9)
+    keys = keys[rng.permutation(n)]
+    ctx.set_ids(O.gen_ids(4, 5000))
+    before, _ = ctx.topk(O.gen_ids(5, 50), 8)
+    ctx.cache_set(keys, version=3)
+    order = np.lexsort(keys.T[::-1])
+    assert np.array_equal(ctx.cache_sorted(), order.astype(np.uint32))
+    acc = (rng.random(n) < 0.75).astype(np.uint8)
+    tg = np.concatenate([O.gen_ids(31338, 500), keys[:12]])
+    got, cnt = ctx.cache_nodes(tg, 14, acc)
+    srt = keys[order]
+    for qi in range(tg.shape[0]):
+        want = O.cached_nodes(srt, acc[order], tg[qi], 14)
+        assert list(got[qi, : cnt[qi]]) == list(order[want]), qi
+    ctx.cache_set(keys[:10], version=3)   # same version, different n: uploaded
+    assert ctx.cache_sorted().size == 10
+    after, _ = ctx.topk(O.gen_ids(5, 50), 8)
+    assert np.array_equal(before, after)
 
 
 def test_sharded_records_merge(ctx):
@@ -299,20 +343,15 @@ def test_prefix_shard_weak_shape(ctx, pbits, pval):
     assert np.array_equal(gl[loc], got) and np.array_equal(sl, loc)
 
 
-def test_batch_refuses_unsafe_plan(ctx):
-    """n = 2^27 with 131,072 targets: the level-19 subtrees hold 256 ids, so a partition's
-    survivors would overflow the F3 stage on uniform ids; K6 refuses the plan (ERANGE)
-    instead of sending thousands of targets to the brute force.  Split into prefix
-    sub-shards (bench --sub-shards, cfg 3) each part is planned normally."""
-    import opendht_amd
-    ctx.gen_ids(777, 1 << 27)
-    tg = O.gen_ids(778, 131072)
-    with pytest.raises(opendht_amd.DhtGpuError) as ei:
-        ctx.batch_topk(tg, 8)
-    assert ei.value.code == -6
-    idx, cnt = ctx.batch_topk(tg[:16], 8)   # a small batch plans fine (few marked subtrees)
-    want, wcnt = O.topk(O.gen_ids(777, 1 << 27), tg[:16], 8)
-    assert np.array_equal(cnt, wcnt) and np.array_equal(idx, want)
+def test_topk_k32_many_splits(ctx):
+    """K1 with a small batch over 2^20 ids at k = 32: the id-range splits are capped so that
+    K3 can stage every split's 32 records in LDS (was: 256 splits, LDS overflow)."""
+    ids = O.gen_ids(3232, 1 << 20)
+    tg = O.gen_ids(3233, 16)
+    ctx.set_ids(ids)
+    want, wcnt = O.topk(ids, tg, 32)
+    got, cnt = ctx.topk(tg, 32)
+    assert np.array_equal(cnt, wcnt) and np.array_equal(got, want)
 
 
 def test_select_prefix_dev(ctx):
@@ -425,6 +464,32 @@ def test_buffer_nodes_vs_oracle(ctx, af):
         want = O.buffer_nodes(ids, tail, alen, tg[i], cand[i])
         assert ln[i] == want.size, i
         assert np.array_equal(out[i, : ln[i]], want), i
+
+
+def test_buffer_nodes_ids_and_bounds(ctx):
+    """bufferNodes over the caller's own nodes leaves the context's id set alone; a candidate
+    index past the node set is refused (EINVAL) instead of read out of bounds."""
+    import opendht_amd
+    rng = np.random.default_rng(77)
+    nodes = O.gen_ids(980, 700)
+    tail = O.special_addrs(rng, 700, 4)
+    tg = O.gen_ids(981, 50)
+    cand = rng.integers(0, 700, size=(50, 12)).astype(np.uint32)
+    cand[::7, 10:] = 0xFFFFFFFF
+    kset = O.gen_ids(982, 3000)
+    ctx.set_ids(kset)
+    out, ln = ctx.buffer_nodes_ids(nodes, tail, 4, tg, cand)
+    for i in range(50):
+        want = O.buffer_nodes(nodes, tail, 4, tg[i], cand[i])
+        assert ln[i] == want.size and np.array_equal(out[i, : ln[i]], want), i
+    assert np.array_equal(ctx.get_ids(), kset)
+    bad = cand.copy()
+    bad[3, 2] = 700
+    with pytest.raises(opendht_amd.DhtGpuError) as ei:
+        ctx.buffer_nodes_ids(nodes, tail, 4, tg, bad)
+    assert ei.value.code == -1
+    with pytest.raises(opendht_amd.DhtGpuError):
+        ctx.buffer_nodes(O.special_addrs(rng, 3000, 4), 4, tg, np.full((50, 4), 3000, np.uint32))
 
 
 @pytest.mark.parametrize("af", [4, 6])
