@@ -23,16 +23,28 @@ Multi-GPU (one process per GPU, torch.distributed over RCCL; --route):
              minimum shard size with one all-reduce and refuses otherwise.
   broadcast  ids range-sharded, all targets on every rank, per-rank candidate records
              exchanged by one RCCL all-gather, merged by K3 (SURVEY §8(e) north-star scheme).
-Scaling (--scaling): "weak" (default with the prefix route: the path partitions into
-independent prefix shards, so every rank keeps the one-GPU workload -- --n ids and --q
-targets per GPU out of a global problem N times as large; value = all ranks' targets / the
-slowest rank's time) or "strong" (--n and --q are the global totals, split across ranks).
+Scaling (--scaling): "weak" (default with the prefix route: every rank keeps the one-GPU
+workload -- --n ids and --q targets per GPU out of a global problem N times as large; value =
+all ranks' targets / the slowest rank's time) or "strong" (--n and --q are global totals).
 
+Beside the headline (`value`) the line carries, measured in the same run:
+  roofline        F2 (the dominant K6 kernel) timed by events its own dispatches record in
+                  every timed step; roofline_hbm: the same kernel with the Infinity Cache
+                  evicted before each call (the cfg-2 working set otherwise stays in L3)
+  small_batch     Q = 1 / 8 / 32 targets over the same ids (HBM-bound latency mode)
+  find_closest    RoutingTable::findClosestNodes drop-in on a cfg-1-shaped table
+  cfg3_shard      one GPU's shard of BASELINE cfg 3 (2^27 ids, 131,072 targets; the library
+                  splits it into prefix sub-partitions) -- its w0 planes (537 MB) exceed L3
+  cfg4 / cfg5     classification of 10^8 ids; iterative searches over 5*10^7 nodes
+  cfg3 (N > 1)    BASELINE cfg 3 itself over the ranks: 10^9 ids, 2^20 targets, both routes
+  cpu_baseline    the oracle port on the host cores (rank 0, N = 1), 1 core and 16 threads
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import ctypes
 import json
 import os
+import platform
 import sys
 import time
 
@@ -40,7 +52,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # Two batches in flight (--inflight) need their streams on different hardware queues; HIP's
 # default of 4 queues per process is shared round-robin by every stream the process creates
-# (torch's, the context's), so ask for 8 before the runtime starts.
+# (torch's, the contexts'), so ask for 8 before the runtime starts.
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import numpy as np  # noqa: E402
@@ -58,27 +70,24 @@ VALU_PEAK_TOPS = 1024 * 16 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
 # Algorithmic VALU work per (id, target) pair in K1: the XOR distance and the running-min
 # select, done two pairs at a time on packed top-16-bit words (v_xor_b32 + v_pk_min_u16
-# per two pairs) = 1 lane-op per pair.  (SURVEY 8(d)'s contract assumed 3 ops/pair on a
-# 64-bit lane; the packed prefilter is an algorithmic win, so frac here is measured
-# against the op count the kernel actually needs and cannot exceed 1.)
+# per two pairs) = 1 lane-op per pair.  SURVEY 8(d)'s contract counts 3 ops/pair on a
+# 64-bit lane; both fractions are reported (the packed prefilter is an algorithmic win).
 OPS_PER_PAIR = 1.0
+SURVEY_OPS_PER_PAIR = 3.0
+PMC_FILE = "profiles/r02/pmc_traffic.json"
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)   # ~41 ms timed: steady state, not ramp-up
+    ap.add_argument("--steps", type=int, default=1000)   # ~40 ms timed: steady state, not ramp-up
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--n", type=int, default=1 << 24, help="node ids (total over all ranks)")
-    ap.add_argument("--q", type=int, default=65536, help="targets per step (total over all ranks)")
+    ap.add_argument("--n", type=int, default=1 << 24, help="node ids (per GPU with weak scaling)")
+    ap.add_argument("--q", type=int, default=65536, help="targets per step (per GPU with weak scaling)")
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--algo", choices=["batch", "index", "scan"], default="batch")
     ap.add_argument("--route", choices=["auto", "prefix", "broadcast"], default="auto")
-    ap.add_argument("--sub-shards", type=int, default=0,
-                    help="prefix route: split each rank's shard into this many prefix sub-shards (one "
-                         "K6 context each, calls spread over the in-flight streams); 0 = auto, the "
-                         "smallest power of two with <= 2^24 ids per sub-shard")
     ap.add_argument("--shard-index", choices=["local", "global"], default="local",
                     help="prefix shards: results as shard-local node indices (the rank owns its shard's "
                          "node table) or mapped to global stream indices (one gather per result)")
@@ -93,10 +102,11 @@ def parse():
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="prefix route only: run rank --simulate-rank of a world of this size on one GPU")
     ap.add_argument("--simulate-rank", type=int, default=0)
-    ap.add_argument("--cpu-targets", type=int, default=256, help="cpu_baseline sample (targets)")
+    ap.add_argument("--cpu-targets", type=int, default=256, help="cpu_baseline sample (targets, 16 threads)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-scan", action="store_true", help="skip the reference K1 scan measurement (index algo)")
+    ap.add_argument("--no-extra", action="store_true", help="skip the extra legs (small batch, cfg 1/3/4/5)")
+    ap.add_argument("--no-scan", action="store_true", help="skip the reference K1 scan measurement")
     ap.add_argument("--verify", type=int, default=16, help="targets re-checked against the oracle (rank 0)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="batch algo: consecutive steps alternate over this many streams, so one step's "
@@ -104,38 +114,11 @@ def parse():
     return ap.parse_args()
 
 
-PMC_FILE = "profiles/r01_batch/pmc_traffic.json"
-
-
-def pmc_traffic(kernel, n, q, k):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
-    (tools/pmc_traffic.py; gfx950 FETCH correction applied there), when they were taken on this
-    workload (cfg 2 shape); None otherwise."""
-    try:
-        d = json.load(open(os.path.join(ROOT, PMC_FILE)))
-    except (OSError, ValueError):
-        return None
-    if d.get("workload") != [n, q, k]:
-        return None
-    return d["kernels"].get(kernel, {}).get("traffic_bytes")
-
-
 def oracle():
+    """The CPU restatement (test infrastructure): only the verification and cpu_baseline legs."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O
     return O
-
-
-def cpu_baseline(ids, tg, k, threads):
-    """Oracle (std::partial_sort with the restated InfoHash::xorCmp) on the host cores,
-    over a bounded target sample of the same workload."""
-    O = oracle()
-    t0 = time.perf_counter()
-    out, _ = O.topk(ids, tg, k, threads=threads)
-    dt = time.perf_counter() - t0
-    return {"value": tg.shape[0] / dt, "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": f"{tg.shape[0]} targets x {ids.shape[0]} ids, k={k}, std::partial_sort(xorCmp) per target, "
-                      f"{threads} threads, {dt:.2f} s wall"}, out
 
 
 T_START = time.perf_counter()
@@ -145,6 +128,107 @@ def progress(msg):
     """Progress line on stderr (long setups and verifications keep the job visibly alive)."""
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench {time.perf_counter() - T_START:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
+    (tools/pmc_traffic.py, gfx950 FETCH correction applied there) for `workload`; None if absent."""
+    try:
+        d = json.load(open(os.path.join(ROOT, PMC_FILE)))
+    except (OSError, ValueError):
+        return None
+    w = d.get("workloads", {}).get(workload)
+    return None if w is None else w.get(kernel, {}).get("traffic_bytes")
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+class EvSets:
+    """Per-call kernel timing: 8 events (F1..F4 start/stop) armed on a K6 call, recorded by the
+    kernels' own dispatches (no synchronisation inside the timed region)."""
+
+    def __init__(self, count, stream):   # stream: a torch.cuda.Stream
+        self.sets = [[torch.cuda.Event(enable_timing=True) for _ in range(8)] for _ in range(count)]
+        for s in self.sets:   # materialise the HIP events
+            for e in s:
+                e.record(stream)
+        self.used = 0
+
+    def arm(self, ctx):
+        ctx.batch_events(self.sets[self.used])
+        self.used += 1
+
+    def mean_ms(self):
+        """mean duration of F1..F4 over the armed calls (synchronises)."""
+        torch.cuda.synchronize()
+        acc = [0.0] * 4
+        for s in self.sets[: self.used]:
+            for i in range(4):
+                acc[i] += s[2 * i].elapsed_time(s[2 * i + 1])
+        return [a / max(self.used, 1) for a in acc]
+
+
+def ev_time(fn, reps, stream=None):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def gen_targets(L, seed, q, dev, stream):
+    ts = (q + 63) // 64 * 64
+    tp = torch.empty(5 * ts, dtype=torch.int32, device=dev)
+    assert L.dhtgpu_gen_dev(seed, 0, q, tp.data_ptr(), ts, stream) == 0
+    return tp, ts
+
+
+def k6_kernels(ms, n, q, k, surv):
+    """Algorithmic bytes per launch of the four K6 kernels."""
+    return {"k_f1_targets": (ms[0], 12 * q), "k_f2_filter": (ms[1], 4 * n + 8 * surv),
+            "k_f3_answer": (ms[2], 8 * surv + q * (8 + 16 + 4 * k + 4)), "k_f4_fallback": (ms[3], 0)}
+
+
+def synthetic_table(myid, depth, per_bucket, rng):
+    """A RoutingTable-shaped snapshot (src/routing_table.cpp: contiguous lexicographic buckets
+    split along myid's path, each holding per_bucket nodes): the sibling subtree of myid at
+    every level < depth, plus myid's own depth-`depth` subtree, sorted by Bucket::first."""
+    me = int.from_bytes(bytes(myid), "big")
+    ranges = []
+    for lvl in range(depth + 1):
+        if lvl < depth:
+            bit = (me >> (159 - lvl)) & 1
+            prefix = ((me >> (160 - lvl)) << 1 | (1 - bit)) if lvl else (1 - bit)
+            plen = lvl + 1
+        else:
+            prefix, plen = me >> (160 - depth), depth
+        ranges.append((prefix << (160 - plen), plen))
+    ranges.sort()
+    firsts, ids, off = [], [], [0]
+    for first, plen in ranges:
+        firsts.append(first.to_bytes(20, "big"))
+        for _ in range(per_bucket):
+            low = int.from_bytes(rng.bytes(20), "big") & ((1 << (160 - plen)) - 1)
+            ids.append((first | low).to_bytes(20, "big"))
+        off.append(len(ids))
+    as_u8 = lambda v: np.frombuffer(b"".join(v), dtype=np.uint8).reshape(-1, 20).copy()
+    return as_u8(firsts), np.array(off, np.uint32), as_u8(ids)
+
+
+def l3_evict(buf):
+    """Read 512 MiB (twice the Infinity Cache; a read leaves no dirty lines to write back during
+    the next kernel): the next kernel reads the id set from HBM."""
+    return buf.sum()
 
 
 def main():
@@ -186,87 +270,58 @@ def main():
 
     G, R = (a.simulate_world, a.simulate_rank) if a.simulate_world else (world, rank)
     pbits = G.bit_length() - 1 if route == "prefix" else 0
-    ts_all = (a.q_total + 63) // 64 * 64
-    tp_all = torch.empty(5 * ts_all, dtype=torch.int32, device=dev)
-    assert L.dhtgpu_gen_dev(a.seed + 1, 0, a.q_total, tp_all.data_ptr(), ts_all, stream) == 0
-    S, sbits = 1, 0
+    tp_all, ts = gen_targets(L, a.seed + 1, a.q_total, dev, stream)
     if route == "prefix":
-        S = a.sub_shards
-        if S <= 0:   # auto: K6 plans for <= 2^24 ids per context (n >> 2^24 has 256-id subtrees)
-            S = 1
-            while a.n_total // (G * S) > (1 << 24) and a.algo == "batch":
-                S *= 2
-        assert S & (S - 1) == 0, "--sub-shards must be a power of two"
-        sbits = pbits + S.bit_length() - 1
-        shards = []
-        for s_i in range(S):
-            c = ctx if s_i == 0 else opendht_amd.Context(local)
-            if sbits:
-                pv = R * S + s_i
-                c.gen_ids_prefix(a.seed, a.n_total, sbits, pv)       # this (sub-)shard's ids
-                c.set_global_indices(a.shard_index == "global")
-                tps = torch.empty_like(tp_all)
-                tg_s = torch.empty(ts_all, dtype=torch.int32, device=dev)
-                q_s = c.select_prefix_dev(tp_all.data_ptr(), ts_all, a.q_total, sbits, pv, tps.data_ptr(), ts_all,
-                                          tg_s.data_ptr(), stream)
-            else:                                                 # one shard: the whole set
-                c.gen_ids(a.seed, a.n_total)
-                tps, q_s, tg_s = tp_all, a.q_total, None
-            shards.append({"ctx": c, "tp": tps, "q": q_s, "tgidx": tg_s, "n": c.num_ids})
-            progress(f"sub-shard {s_i}: {c.num_ids} ids, {q_s} targets")
-        ts = ts_all
-        shard_min = torch.tensor([min(sh["n"] for sh in shards)], dtype=torch.int64, device=dev)
+        if pbits:
+            ctx.gen_ids_prefix(a.seed, a.n_total, pbits, R)       # this rank's prefix shard
+            ctx.set_global_indices(a.shard_index == "global")
+            tp = torch.empty_like(tp_all)
+            tgidx = torch.empty(ts, dtype=torch.int32, device=dev)
+            q_local = ctx.select_prefix_dev(tp_all.data_ptr(), ts, a.q_total, pbits, R, tp.data_ptr(), ts,
+                                            tgidx.data_ptr(), stream)
+        else:
+            ctx.gen_ids(a.seed, a.n_total)
+            tp, q_local, tgidx = tp_all, a.q_total, None
+        n_local = ctx.num_ids
+        shard_min = torch.tensor([n_local], dtype=torch.int64, device=dev)
         if use_dist:
             dist.all_reduce(shard_min, op=dist.ReduceOp.MIN)
         if int(shard_min.item()) < a.k:
             raise SystemExit("prefix route needs >= k ids per shard; rerun with --route broadcast")
-        tp, q_local, tgidx = shards[0]["tp"], sum(sh["q"] for sh in shards), shards[0]["tgidx"]
-        n_local = sum(sh["n"] for sh in shards)
         lo = 0
     else:
         lo, hi = sharding.shard_range(a.n_total, world, rank)
         ctx.gen_ids(a.seed, hi - lo, start=lo)      # this rank's contiguous slice of the global id stream
-        tp, ts, q_local, tgidx = tp_all, ts_all, a.q_total, None
+        tp, q_local, tgidx = tp_all, a.q_total, None
         n_local = hi - lo
-        shards = [{"ctx": ctx, "tp": tp, "q": q_local, "tgidx": None, "n": n_local}]
-    # the per-kernel diagnostics below time one K6 call on sub-shard 0
-    q0, n0 = shards[0]["q"], shards[0]["n"]
     collective = use_dist and route == "broadcast"
-    qk = max(q0, 1)
-    out_idx = torch.empty((qk, a.k), dtype=torch.int32, device=dev)
-    out_cnt = torch.empty(qk, dtype=torch.int32, device=dev)
+    qk = max(q_local, 1)
     rec = torch.empty((a.q_total, a.k, 6), dtype=torch.int32, device=dev) if collective else None
     gathered = torch.empty((world * a.q_total, a.k, 6), dtype=torch.int32, device=dev) if collective else None
 
-    def local_lookup(out_i, out_c, out_r, base, stream=stream, sh=None):
-        sh = sh or shards[0]
-        c, tps, qs = sh["ctx"], sh["tp"].data_ptr(), sh["q"]
+    def local_lookup(out_i, out_c, out_r, base, s=stream):
         if a.algo == "batch":
-            c.batch_topk_dev(tps, ts, qs, a.k, out_i, out_c, out_r, base, stream)
+            ctx.batch_topk_dev(tp.data_ptr(), ts, q_local, a.k, out_i, out_c, out_r, base, s)
         elif a.algo == "index":
-            c.index_build(stream)          # the index is rebuilt from the raw id planes every step
-            c.index_topk_dev(tps, ts, qs, a.k, out_i, out_c, out_r, base, stream)
+            ctx.index_build(s)          # the index is rebuilt from the raw id planes every step
+            ctx.index_topk_dev(tp.data_ptr(), ts, q_local, a.k, out_i, out_c, out_r, base, s)
         else:
-            c.topk_dev(tps, ts, qs, a.k, out_i, out_c, out_r, base, stream)
+            ctx.topk_dev(tp.data_ptr(), ts, q_local, a.k, out_i, out_c, out_r, base, s)
 
-    # in-flight calls: call j (step i, sub-shard s: j = i * S + s) runs on stream j % D with
-    # its own output buffers
+    # in-flight calls: step i runs on stream i % D with its own output buffers
     D = max(1, a.inflight) if (a.algo == "batch" and not collective) else 1
     streams = [tstream] + [torch.cuda.Stream(dev) for _ in range(D - 1)]
-    outs = [[(out_idx, out_cnt) if (si == 0 and d == 0) else
-             (torch.empty((max(sh["q"], 1), a.k), dtype=torch.int32, device=dev),
-              torch.empty(max(sh["q"], 1), dtype=torch.int32, device=dev)) for d in range(D)]
-            for si, sh in enumerate(shards)]
+    outs = [(torch.empty((qk, a.k), dtype=torch.int32, device=dev), torch.empty(qk, dtype=torch.int32, device=dev))
+            for _ in range(D)]
+    out_idx, out_cnt = outs[0]
     step_no = [0]
 
     def step():
         i = step_no[0]
         step_no[0] += 1
         if not collective:
-            for si, sh in enumerate(shards):
-                j = i * len(shards) + si
-                oi, oc = outs[si][j % D]
-                local_lookup(oi.data_ptr(), oc.data_ptr(), None, 0, streams[j % D].cuda_stream, sh)
+            oi, oc = outs[i % D]
+            local_lookup(oi.data_ptr(), oc.data_ptr(), None, 0, streams[i % D].cuda_stream)
         else:
             local_lookup(None, None, rec.data_ptr(), lo)
             sharding.gather_records(rec, out=gathered)
@@ -280,123 +335,154 @@ def main():
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record()
     for _ in range(a.steps):
         step()
-    ev1.record()
     torch.cuda.synchronize()
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    ev_ms = ev0.elapsed_time(ev1) / a.steps
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
     if use_dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t.item())
     ms_per_step = wall * 1e3 / a.steps
-    # outputs of the last timed step (for the verification below), per sub-shard
-    got = []
-    for si, sh in enumerate(shards):
-        j = (step_no[0] - 1) * len(shards) + si
-        gi = outs[si][j % D][0][:sh["q"]].cpu().numpy().view(np.uint32).copy()
-        gt = sh["tgidx"][:sh["q"]].cpu().numpy().view(np.uint32).copy() if sh["tgidx"] is not None \
-            else np.arange(sh["q"])
-        got.append((gi, gt))
-
-    def ev_time(fn, reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            fn()
-        e1.record()
-        torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / reps
-
+    last = (step_no[0] - 1) % D
+    got_idx = outs[last][0][:q_local].cpu().numpy().view(np.uint32).copy() if not collective \
+        else out_idx.cpu().numpy().view(np.uint32).copy()
+    got_tg = tgidx[:q_local].cpu().numpy().view(np.uint32).copy() if tgidx is not None else np.arange(q_local)
     progress(f"timed {a.steps} steps: {ms_per_step:.4f} ms/step; diagnostics")
     reps = max(3, min(a.steps, 20))
+    res = {}
+    extra = {}
     # single-batch latency: the same step strictly serial on one stream
-    lat_ms = ev_time(lambda: local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0), reps) \
+    lat_ms = ev_time(lambda: local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0), reps, tstream) \
         if not collective else None
-    lat_global_ms = None
-    if route == "prefix" and sbits and a.shard_index == "local":
-        # the same batch with results mapped to global stream indices (for comparison)
+    if route == "prefix" and pbits and a.shard_index == "local":
         ctx.set_global_indices(True)
-        lat_global_ms = ev_time(lambda: local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0), reps)
+        extra["latency_ms_per_batch_global_indices"] = ev_time(
+            lambda: local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0), reps, tstream)
         ctx.set_global_indices(False)
     if a.algo == "batch":
-        # per-kernel device times (HIP events between F1..F4 on the bench stream)
-        runs = [ctx.batch_topk_timed(tp.data_ptr(), ts, q0, a.k, out_idx.data_ptr(), out_cnt.data_ptr(), stream)
-                for _ in range(reps)]
-        ph = [sum(r[0][i] for r in runs) / reps for i in range(4)]
-        n_fb, surv, n_slow = runs[-1][1], runs[-1][2], runs[-1][3]
-        kern = {"k_f1_targets": (ph[0], 12 * q0),
-                "k_f2_filter": (ph[1], 4 * n0 + 8 * surv),
-                "k_f3_answer": (ph[2], 8 * surv + q0 * (8 + 16 + 4 * a.k + 4)),
-                "k_f4_fallback": (ph[3], 0)}
-        dom = max(kern, key=lambda k: kern[k][0])
+        # per-kernel device time: HIP events recorded by the kernels' own dispatches
+        # (hipExtLaunchKernel) on the bench stream, averaged over `reps` serial calls of the timed
+        # step right after the timed window (arming events on every in-flight step perturbs the
+        # step: +8-15 us); the rocprofv3 kernel-trace average of the bench (profiles/r02) agrees
+        kt = EvSets(reps, tstream)
+        for _ in range(reps):
+            kt.arm(ctx)
+            local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), rec.data_ptr() if collective else None, lo)
+        live = kt.mean_ms()
+        tms, n_fb, surv, n_slow = ctx.batch_topk_timed(tp.data_ptr(), ts, q_local, a.k, out_idx.data_ptr(),
+                                                       out_cnt.data_ptr(), stream)
+        kern = k6_kernels(live, n_local, q_local, a.k, surv)
+        dom = "k_f2_filter"
         dom_ms, dom_bytes = kern[dom]
-        step_bytes = sum(v[1] for v in kern.values()) * len(shards)   # sub-shard 0's bytes x S
-        tb = pmc_traffic(dom, n0, q0, a.k)
+        step_bytes = sum(v[1] for v in kern.values())
+        wl = f"cfg2:{n_local}x{q_local}x{a.k}"
+        tb = pmc_traffic(wl, dom)
+        working = 4 * n_local + 16 * surv + q_local * (12 + 8 + 4 * a.k)
         roof = {"bound": "hbm", "achieved": dom_bytes / (dom_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "traffic": tb / (dom_ms * 1e-3) / 1e9 if tb else None,
                 "traffic_bytes_per_launch": tb, "traffic_source": PMC_FILE if tb else None,
                 "kernel": dom, "kernel_ms": dom_ms, "alg_bytes_per_launch": dom_bytes,
+                "kernel_timing": f"mean of {reps} serial calls of the timed step on the bench stream, HIP events "
+                                 f"recorded by the kernels' own dispatches (hipExtLaunchKernel)",
                 "kernels_ms": {k: v[0] for k, v in kern.items()},
                 "step_alg_bytes": step_bytes,
                 "step_hbm_frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "working_set_bytes": working,
+                "served_from": "Infinity Cache: the cfg-2 working set (w0 plane + survivor buckets) stays "
+                               "resident in the 256 MiB L3 across steps; see roofline_hbm for the HBM figure",
                 # SURVEY 8(d) contract bytes (every id read whole, 20 B) and their time at peak
                 "contract_bytes": n_local * 20 + q_local * 20 + q_local * a.k * 4,
                 "contract_floor_ms": (n_local * 20 + q_local * 20 + q_local * a.k * 4) / HBM_PEAK_GBS / 1e6}
-        extra = {"survivors": surv, "survivor_frac": surv / max(n0, 1), "fallback_targets": n_fb,
-                 "wave_path_targets": n_slow}
+        extra.update({"survivors": surv, "survivor_frac": surv / max(n_local, 1), "fallback_targets": n_fb,
+                      "wave_path_targets": n_slow})
+        # the same kernel with the Infinity Cache evicted before every call (HBM-bound figure)
+        ebuf = torch.zeros(128 << 20, dtype=torch.int32, device=dev)
+        cold = EvSets(8, tstream)
+        for _ in range(8):
+            l3_evict(ebuf)
+            cold.arm(ctx)
+            local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0)
+        cms = cold.mean_ms()
+        del ebuf
+        ckern = k6_kernels(cms, n_local, q_local, a.k, surv)
+        res["roofline_hbm"] = {"bound": "hbm", "kernel": dom, "kernel_ms": ckern[dom][0],
+                               "achieved": dom_bytes / (ckern[dom][0] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": dom_bytes / (ckern[dom][0] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                               "kernels_ms": {k: v[0] for k, v in ckern.items()},
+                               "traffic_bytes_per_launch": pmc_traffic(wl + ":cold", dom),
+                               "how": "512 MiB read between calls (2x the Infinity Cache), 8 serial calls, events "
+                                      "of the kernels' dispatches"}
     elif a.algo == "index":
-        # per-kernel device times of the index build (HIP events between its kernels, on
-        # the bench stream) and of the query kernel alone
         phases = [ctx.index_build_timed(stream) for _ in range(reps)]
         ph = [sum(p[i] for p in phases) / reps for i in range(4)]
-        q_ms = ev_time(lambda: ctx.index_topk_dev(tp.data_ptr(), ts, q0, a.k, out_idx.data_ptr(),
-                                                  out_cnt.data_ptr(), None, 0, stream), reps)
-        kern = {"k_p0_hist": (ph[0], 4 * n0), "k_p0_scans": (ph[1], 0),
-                "k_p1_scatter": (ph[2], 12 * n0), "k_p2_buckets": (ph[3], 16 * n0),
-                "k_query": (q_ms, q0 * (20 + a.k * 4))}
+        q_ms = ev_time(lambda: ctx.index_topk_dev(tp.data_ptr(), ts, q_local, a.k, out_idx.data_ptr(),
+                                                  out_cnt.data_ptr(), None, 0, stream), reps, tstream)
+        kern = {"k_p0_hist": (ph[0], 4 * n_local), "k_p0_scans": (ph[1], 0),
+                "k_p1_scatter": (ph[2], 12 * n_local), "k_p2_buckets": (ph[3], 16 * n_local),
+                "k_query": (q_ms, q_local * (20 + a.k * 4))}
         dom = max(kern, key=lambda k: kern[k][0])
         dom_ms, dom_bytes = kern[dom]
-        step_bytes = n0 * (4 + 8) + q0 * (20 + a.k * 4)
         roof = {"bound": "hbm", "achieved": dom_bytes / (dom_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                 "kernel": dom, "kernel_ms": dom_ms, "alg_bytes_per_launch": dom_bytes,
-                "kernels_ms": {k: v[0] for k, v in kern.items()},
-                "step_alg_bytes": step_bytes,
-                "step_hbm_frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS}
-        extra = {"query_only_qps_per_gpu": q0 / (q_ms * 1e-3), "index_build_ms": sum(ph)}
+                "kernels_ms": {k: v[0] for k, v in kern.items()}}
+        extra.update({"query_only_qps_per_gpu": q_local / (q_ms * 1e-3), "index_build_ms": sum(ph)})
     else:
-        kern_ms = ev_ms
-        if collective:
-            kern_ms = ev_time(lambda: local_lookup(None, None, rec.data_ptr(), lo), reps)
-        pairs = q0 * n0
+        kern_ms = ev_time(lambda: local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(),
+                                               rec.data_ptr() if collective else None, lo), reps, tstream)
+        pairs = q_local * n_local
         achieved = OPS_PER_PAIR * pairs / (kern_ms * 1e-3) / 1e12
         roof = {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
                 "frac": achieved / VALU_PEAK_TOPS, "traffic": None,
                 "kernel": "k_scan (K1 xor_topk_scan)", "kernel_ms": kern_ms,
                 "ops_per_pair": OPS_PER_PAIR, "pairs_per_launch": pairs,
-                "hbm_alg_bytes_per_launch": n0 * 20 + q0 * 20 + q0 * a.k * 4}
-        extra = {}
+                "frac_survey_3op": SURVEY_OPS_PER_PAIR * pairs / (kern_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS,
+                "hbm_alg_bytes_per_launch": n_local * 20 + q_local * 20 + q_local * a.k * 4}
+
     if a.algo != "scan" and not a.no_scan and world == 1 and not a.simulate_world:
         # the north-star brute-force scan (K1) on the same inputs, for reference
-        sc_ms = ev_time(lambda: ctx.topk_dev(tp.data_ptr(), ts, q0, a.k, out_idx.data_ptr(),
-                                             out_cnt.data_ptr(), None, 0, stream), 3)
-        ach = OPS_PER_PAIR * q0 * n0 / (sc_ms * 1e-3) / 1e12
-        extra["scan_k1"] = {"qps": q0 / (sc_ms * 1e-3), "kernel_ms": sc_ms, "bound": "valu",
-                            "achieved_TOPs": ach, "peak_TOPs": VALU_PEAK_TOPS, "frac": ach / VALU_PEAK_TOPS}
+        sc_ms = ev_time(lambda: ctx.topk_dev(tp.data_ptr(), ts, q_local, a.k, out_idx.data_ptr(),
+                                             out_cnt.data_ptr(), None, 0, stream), 3, tstream)
+        pairs = q_local * n_local
+        ach = OPS_PER_PAIR * pairs / (sc_ms * 1e-3) / 1e12
+        extra["scan_k1"] = {"qps": q_local / (sc_ms * 1e-3), "kernel_ms": sc_ms, "bound": "valu",
+                            "achieved_TOPs": ach, "peak_TOPs": VALU_PEAK_TOPS, "frac": ach / VALU_PEAK_TOPS,
+                            "ops_per_pair": OPS_PER_PAIR,
+                            "frac_survey_3op": SURVEY_OPS_PER_PAIR * pairs / (sc_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS,
+                            "note": "frac counts the packed kernel's 1 lane-op per pair; frac_survey_3op counts "
+                                    "SURVEY 8(d)'s 3 ops per pair (> 1 means the packed prefilter beats it)"}
+
+    single = world == 1 and not a.simulate_world and not a.no_extra and a.algo == "batch"
+    if single:
+        progress("small-batch and table legs")
+        extra["small_batch"] = small_batch_leg(ctx, tp, ts, n_local, a.k, stream, tstream, dev)
+        extra["find_closest"] = find_closest_leg(ctx, a, dev)
+        ctx.close()   # the cfg-2 set is no longer needed: free HBM for the size legs
+        ctx = None
+        for name, fn in (("cfg3_shard", cfg3_shard_leg), ("cfg4", cfg4_leg), ("cfg5", cfg5_leg)):
+            progress(f"{name} leg")
+            try:
+                extra[name] = fn(a, L, dev, stream, tstream)
+            except Exception as e:  # noqa: BLE001 -- an extra leg must not cost the headline
+                extra[name] = {"error": repr(e)}
+    if world > 1 and not a.no_extra and a.algo == "batch" and not a.rehearse_one_gpu:
+        progress("cfg3 leg over the ranks")
+        try:
+            if ctx is not None:
+                ctx.close()
+                ctx = None
+            extra["cfg3"] = cfg3_multi_leg(a, L, dev, stream, tstream, world, rank)
+        except Exception as e:  # noqa: BLE001
+            extra["cfg3"] = {"error": repr(e)}
 
     if rank == 0:
-        par = {"prefix": f"prefix-routed shards x{G} (top {pbits} id bits"
-                         + (f", {len(shards)} prefix sub-shards per GPU" if len(shards) > 1 else "")
-                         + "; no data-path collective)",
+        par = {"prefix": f"prefix-routed shards x{G} (top {pbits} id bits; no data-path collective)",
                "broadcast": f"id-range shards x{world}" + (" + RCCL all-gather + K3 merge" if collective else "")}[route]
         res = {
             "metric": METRIC,
@@ -411,60 +497,340 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic: splitmix64 ids and targets generated in HBM (SURVEY 8(d) spec)",
-            "config": {"workload": ("cfg2" if (a.n, a.q) == (1 << 24, 65536) else "custom") + f" batched k-NN: {a.q} targets x {a.n} ids (2^{a.n.bit_length()-1}), k={a.k}"
-                                   + (f" per GPU ({a.q_total} x {a.n_total} over {G_eff} GPUs)" if scaling == "weak" and G_eff > 1
-                                      else ""),
+            "config": {"workload": ("cfg2" if (a.n, a.q) == (1 << 24, 65536) else "custom")
+                                   + f" batched k-NN: {a.q} targets x {a.n} ids (2^{a.n.bit_length()-1}), k={a.k}"
+                                   + (f" per GPU ({a.q_total} x {a.n_total} over {G_eff} GPUs)"
+                                      if scaling == "weak" and G_eff > 1 else ""),
                        "n_ids": a.n_total, "n_targets": a.q_total, "k": a.k, "algo": a.algo, "route": route,
                        "ids_per_gpu": n_local, "targets_per_gpu": q_local, "parallelism": par,
-                       "inflight": D, "sub_shards": len(shards),
+                       "inflight": D,
                        "result_indices": ("shard-local" if a.shard_index == "local" else "global")
-                       if route == "prefix" and sbits else "global"},
+                       if route == "prefix" and pbits else "global"},
             "latency_ms_per_batch": lat_ms,
             "roofline": roof,
+            **res,
         }
-        if len(shards) > 1:
-            res["sub_shard_note"] = (f"each rank's shard is split into {len(shards)} prefix sub-shards (one K6 context "
-                                     f"each); kernels_ms / latency time one call on sub-shard 0 "
-                                     f"({n0} ids, {q0} targets)")
-        if lat_global_ms is not None:
-            res["latency_ms_per_batch_global_indices"] = lat_global_ms
         if a.simulate_world:
             res["simulated"] = f"rank {R} of {G} on one GPU; value = this rank's targets / its step time"
         res.update(extra)
-        # spot check of this run's output against the oracle (rank 0), and the cpu_baseline
-        # leg (rank 0, N = 1 only)
         if not a.no_cpu and (a.verify or world == 1):
             progress("verifying against the oracle")
             O = oracle()
             nv = min(q_local, max(a.verify, a.cpu_targets if world == 1 else 0))
             tg_all = O.gen_ids(a.seed + 1, a.q_total)
-            local_ix = route == "prefix" and sbits and a.shard_index == "local"
-            ok, nver = True, 0
-            if not local_ix:
-                ids_all = O.gen_ids(a.seed, a.n_total)
-            for si, sh in enumerate(shards):
-                gi, gt = got[si]
-                ns = min(sh["q"], max(1, nv // len(shards)))
-                tg = tg_all[gt[:ns]]
-                # shard-local results: the oracle over this (sub-)shard's own ids, read back
-                # from the device -- the set the call answers from, same index space
-                ids = sh["ctx"].get_ids() if local_ix else ids_all
-                if si == 0 and world == 1 and not a.simulate_world:
-                    cb, want = cpu_baseline(ids, tg, a.k, a.cpu_threads)
-                    res["cpu_baseline"] = cb
-                else:
-                    want, _ = O.topk(ids, tg, a.k, threads=a.cpu_threads)
-                ok = ok and bool(np.array_equal(gi[:ns], want))
-                nver += ns
-                del ids
-            res["verified_targets"] = int(nver)
-            res["verified_exact"] = ok
+            tg = tg_all[got_tg[:nv]]
+            local_ix = route == "prefix" and pbits and a.shard_index == "local"
+            if local_ix:   # shard-local results: the oracle over this shard's own ids, in shard order
+                top = O.gen_ids(a.seed, a.n_total)
+                top = top[(top[:, 0] >> (8 - pbits)) == R]
+                ids = top
+            else:
+                ids = O.gen_ids(a.seed, a.n_total)
+            if world == 1 and not a.simulate_world:
+                cb, want = cpu_baseline(O, ids, tg, a)
+                res["cpu_baseline"] = cb
+            else:
+                want, _ = O.topk(ids, tg, a.k, threads=a.cpu_threads)
+            res["verified_targets"] = int(nv)
+            res["verified_exact"] = bool(np.array_equal(got_idx[:nv], want))
             progress("verified")
         print(json.dumps(res), flush=True)
-    ctx.close()
+    if ctx is not None:
+        ctx.close()
     if use_dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def small_batch_leg(ctx, tp, ts, n, k, stream, tstream, dev):
+    """Q = 1 / 8 / 32 targets over the same id set: latency per call and the bytes the call has
+    to stream (K6 and K1 read the w0 plane, 4 B/id; SURVEY's contract counts 20 B/id)."""
+    out = {}
+    oi = torch.empty((32, k), dtype=torch.int32, device=dev)
+    oc = torch.empty(32, dtype=torch.int32, device=dev)
+    for q in (1, 8, 32):
+        row = {}
+        for name, fn in (("k6", ctx.batch_topk_dev), ("k1", ctx.topk_dev)):
+            call = lambda: fn(tp.data_ptr(), ts, q, k, oi.data_ptr(), oc.data_ptr(), None, 0, stream)
+            call()
+            ms = ev_time(call, 20, tstream)
+            row[name] = {"latency_ms": ms, "qps": q / (ms * 1e-3),
+                         "w0_GBps": 4 * n / (ms * 1e-3) / 1e9, "w0_frac": 4 * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "contract_GBps": (20 * n + 24 * q + 4 * k * q) / (ms * 1e-3) / 1e9}
+        kms = None
+        ev = EvSets(1, tstream)
+        ev.arm(ctx)
+        ctx.batch_topk_dev(tp.data_ptr(), ts, q, k, oi.data_ptr(), oc.data_ptr(), None, 0, stream)
+        kms = ev.mean_ms()
+        row["k6_kernels_ms"] = dict(zip(["k_f1_targets", "k_f2_filter", "k_f3_answer", "k_f4_fallback"], kms))
+        row["k6_f2_frac"] = 4 * n / (kms[1] * 1e-3) / 1e9 / HBM_PEAK_GBS
+        out[f"q{q}"] = row
+    out["note"] = ("id set L3-resident (the cfg-2 set); w0_frac = the 4 B/id w0 stream over the whole call's "
+                   "time; k6_f2_frac = the same bytes over the F2 kernel alone")
+    return out
+
+
+def find_closest_leg(ctx, a, dev):
+    """RoutingTable::findClosestNodes (dhtgpu_find_closest, K1r) on a cfg-1-shaped table: one
+    target per call (the reference's call pattern; host pointers, PCIe included) and one
+    65,536-target batch."""
+    rng = np.random.default_rng(a.seed)
+    myid = np.frombuffer(rng.bytes(20), dtype=np.uint8).copy()
+    firsts, off, nodes = synthetic_table(myid, 11, 8, rng)
+    good = np.ones(nodes.shape[0], np.uint8)
+    tg = np.frombuffer(rng.bytes(20 * 65536), dtype=np.uint8).reshape(-1, 20).copy()
+    ctx.find_closest(firsts, off, nodes, good, tg[:1], 8)
+    t0 = time.perf_counter()
+    for i in range(200):
+        ctx.find_closest(firsts, off, nodes, good, tg[i:i + 1], 8)
+    single = (time.perf_counter() - t0) / 200
+    ctx.find_closest(firsts, off, nodes, good, tg, 8)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        ctx.find_closest(firsts, off, nodes, good, tg, 8)
+    batch = (time.perf_counter() - t0) / 5
+    return {"table": f"{firsts.shape[0]} buckets, {nodes.shape[0]} nodes (synthetic, RoutingTable shape)",
+            "single_target_us": single * 1e6, "batch_65536_ms": batch * 1e3, "batch_qps": 65536 / batch,
+            "note": "host API per call: snapshot + targets uploaded, results downloaded (PCIe included)"}
+
+
+def cfg3_shard_leg(a, L, dev, stream, tstream):
+    """One GPU's shard of cfg 3: 2^27 ids (~10^9 / 8), 131,072 targets.  The library splits the
+    set once into 8 prefix sub-partitions of 2^24 (setup, not timed) and runs one K6 pass per
+    sub-partition; its 8 w0 planes (537 MB) exceed the Infinity Cache, so F2 streams HBM."""
+    n, q, k = 1 << 27, 131072, a.k
+    c = opendht_amd.Context(dev.index)
+    try:
+        c.gen_ids(a.seed + 3, n)
+        tp, ts = gen_targets(L, a.seed + 4, q, dev, stream)
+        outs = [(torch.empty((q, k), dtype=torch.int32, device=dev), torch.empty(q, dtype=torch.int32, device=dev))
+                for _ in range(2)]
+        sts = [tstream, torch.cuda.Stream(dev)]
+        t0 = time.perf_counter()
+        c.batch_topk_dev(tp.data_ptr(), ts, q, k, outs[0][0].data_ptr(), outs[0][1].data_ptr(), None, 0, stream)
+        torch.cuda.synchronize()
+        first_s = time.perf_counter() - t0
+        for i in range(4):
+            c.batch_topk_dev(tp.data_ptr(), ts, q, k, outs[i % 2][0].data_ptr(), outs[i % 2][1].data_ptr(), None, 0,
+                             sts[i % 2].cuda_stream)
+        steps = 20
+        ev = EvSets(steps, tstream)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            ev.arm(c)
+            c.batch_topk_dev(tp.data_ptr(), ts, q, k, outs[i % 2][0].data_ptr(), outs[i % 2][1].data_ptr(), None, 0,
+                             sts[i % 2].cuda_stream)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3 / steps
+        kms = ev.mean_ms()
+        iso, fb, surv, slow = c.batch_topk_timed(tp.data_ptr(), ts, q, k, outs[0][0].data_ptr(), outs[0][1].data_ptr(),
+                                                stream)
+        n_sub = n // 8
+        q_sub = q // 8
+        kern = k6_kernels(kms, n_sub, q_sub, k, surv)
+        f2ms, f2b = kern["k_f2_filter"]
+        res = {"workload": f"{q} targets x {n} ids (2^27), k={k}: 8 prefix sub-partitions of ~2^24",
+               "ms_per_step": ms, "qps": q / (ms * 1e-3), "setup_first_call_s": first_s,
+               "sub_partition_kernels_ms": {kk: v[0] for kk, v in kern.items()},
+               "sub_partition_kernels_ms_isolated": dict(zip(["k_f1_targets", "k_f2_filter", "k_f3_answer",
+                                                              "k_f4_fallback"], list(iso))),
+               "roofline_f2_isolated_frac": f2b / (iso[1] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+               "roofline_f2": {"bound": "hbm", "achieved": f2b / (f2ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": f2b / (f2ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                               "alg_bytes_per_launch": f2b, "kernel_ms": f2ms,
+                               "traffic_bytes_per_launch": pmc_traffic(f"cfg3shard:{n}x{q}x{k}", "k_f2_filter"),
+                               "served_from": "HBM: 8 sub-partition w0 planes = 537 MB per step > 256 MiB L3"},
+               "sub0_survivors": surv, "sub0_fallback": fb, "sub0_wave_path": slow}
+        if not a.no_cpu:
+            O = oracle()
+            rows = np.arange(0, q, q // 16)
+            got = outs[(steps - 1) % 2][0].cpu().numpy().view(np.uint32)[rows]
+            want, _ = O.topk(O.gen_ids(a.seed + 3, n), O.gen_ids(a.seed + 4, q)[rows], k, threads=a.cpu_threads)
+            res["verified_targets"] = int(rows.size)
+            res["verified_exact"] = bool(np.array_equal(got, want))
+        return res
+    finally:
+        c.close()
+        torch.cuda.synchronize()
+
+
+def cfg4_leg(a, L, dev, stream, tstream):
+    """BASELINE cfg 4: findBucket + commonBits classification of 10^8 ids vs a local id (K2),
+    bucket firsts of a table grown from ~10^5 ids; 21 B/id algorithmic (20 in + 1 out)."""
+    n = 100_000_000
+    rng = np.random.default_rng(a.seed + 5)
+    myid = np.frombuffer(rng.bytes(20), dtype=np.uint8).copy()
+    firsts, _, _ = synthetic_table(myid, 14, 1, rng)
+    c = opendht_amd.Context(dev.index)
+    try:
+        c.gen_ids(a.seed + 6, n)
+        planes, stride = c.ids_dev()
+        fp = torch.from_numpy(firsts.view(">u4").reshape(-1, 5).astype(np.uint32).T.copy().reshape(-1).view(np.int32)).to(dev)
+        my = np.frombuffer(myid.tobytes(), dtype=">u4").astype(np.uint32)
+        my_c = (ctypes.c_uint32 * 5)(*[int(x) for x in my])
+        bucket = torch.empty(n, dtype=torch.uint8, device=dev)
+        hist = torch.zeros(161, dtype=torch.int64, device=dev)
+        nb = firsts.shape[0]
+
+        def call():
+            hist.zero_()
+            assert L.dhtgpu_classify_dev(planes, stride, n, nb, fp.data_ptr(), my_c, bucket.data_ptr(), hist.data_ptr(),
+                                         stream) == 0
+        call()
+        ms = ev_time(call, 10, tstream)
+        b = 21 * n
+        return {"workload": f"{n} ids vs one local id, {nb} routing buckets", "ms": ms, "ids_per_s": n / (ms * 1e-3),
+                "roofline": {"bound": "hbm", "achieved": b / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "alg_bytes": b},
+                "hist_total": int(hist.sum().item())}
+    finally:
+        c.close()
+        torch.cuda.synchronize()
+
+
+def cfg5_leg(a, L, dev, stream, tstream):
+    """BASELINE cfg 5: iterative searches (Search::insertNode rounds, 4 requests per round) over a
+    5*10^7-node synthetic network with 10 % dead nodes (crawl model, crawl.hip)."""
+    n, q = 50_000_000, 65536
+    c = opendht_amd.Context(dev.index)
+    try:
+        c.gen_ids(a.seed + 7, n)
+        dead = (np.random.default_rng(a.seed + 7).random(n) < 0.1).astype(np.uint8)
+        t0 = time.perf_counter()
+        c.net_prepare(dead, table_seed=a.seed + 7)
+        prep = time.perf_counter() - t0
+        tp, ts = gen_targets(L, a.seed + 8, q, dev, stream)
+        sr = torch.from_numpy(((np.arange(q, dtype=np.uint64) * 2654435761) % n).astype(np.uint32).view(np.int32)).to(dev)
+        o_idx = torch.empty((q, 64), dtype=torch.int32, device=dev)
+        o_fl = torch.empty((q, 64), dtype=torch.uint8, device=dev)
+        o_len, o_rd, o_qs = (torch.empty(q, dtype=torch.int32, device=dev) for _ in range(3))
+        args = (tp.data_ptr(), ts, q, sr.data_ptr(), 64, o_idx.data_ptr(), o_fl.data_ptr(), o_len.data_ptr(),
+                o_rd.data_ptr(), o_qs.data_ptr(), stream)
+        call = lambda: L.dhtgpu_search_batch_dev(c._h, *args)
+        call()
+        ms = ev_time(call, 3, tstream)
+        return {"workload": f"{q} searches over {n} nodes (10% dead)", "ms_per_batch": ms,
+                "searches_per_s": q / (ms * 1e-3), "rounds_mean": float(o_rd.float().mean().item()),
+                "requests_mean": float(o_qs.float().mean().item()), "net_prepare_s": prep}
+    finally:
+        c.close()
+        torch.cuda.synchronize()
+
+
+def cfg3_multi_leg(a, L, dev, stream, tstream, world, rank):
+    """BASELINE cfg 3 over the ranks: 10^9 ids, 2^20 targets, k = 8, each route timed:
+    broadcast (SURVEY 8(e) north star: id-range shards, every target on every rank, K6 record
+    mode, one RCCL all-gather of q*k*24 B, K3 merge) and prefix (ids and targets routed by
+    their top log2(N) bits, no collective on the data path)."""
+    n, q, k = 1_000_000_000, 1 << 20, a.k
+    out = {"workload": f"{q} targets x {n} ids over {world} GPUs, k={k}"}
+    steps = 5
+    tp_all, ts = gen_targets(L, a.seed + 11, q, dev, stream)
+    # broadcast route
+    lo, hi = sharding.shard_range(n, world, rank)
+    c = opendht_amd.Context(dev.index)
+    try:
+        c.gen_ids(a.seed + 10, hi - lo, start=lo)
+        rec = torch.empty((q, k, 6), dtype=torch.int32, device=dev)
+        gathered = torch.empty((world * q, k, 6), dtype=torch.int32, device=dev)
+        oi = torch.empty((q, k), dtype=torch.int32, device=dev)
+        oc = torch.empty(q, dtype=torch.int32, device=dev)
+
+        def bstep():
+            c.batch_topk_dev(tp_all.data_ptr(), ts, q, k, None, None, rec.data_ptr(), lo, stream)
+            sharding.gather_records(rec, out=gathered)
+            assert L.dhtgpu_merge_dev(gathered.data_ptr(), world, q, k, tp_all.data_ptr(), ts, k, oi.data_ptr(),
+                                      oc.data_ptr(), stream) == 0
+        bstep()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            bstep()
+        torch.cuda.synchronize()
+        dist.barrier()
+        tm = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        ms = float(tm.item()) * 1e3 / steps
+        out["broadcast"] = {"ms_per_step": ms, "qps": q / (ms * 1e-3), "ids_per_gpu": hi - lo,
+                            "allgather_bytes_per_gpu": q * k * 24, "scaling": "strong (one global batch)"}
+    finally:
+        c.close()
+        torch.cuda.synchronize()
+    # prefix route
+    pbits = world.bit_length() - 1
+    c = opendht_amd.Context(dev.index)
+    try:
+        c.gen_ids_prefix(a.seed + 10, n, pbits, rank)
+        c.set_global_indices(False)
+        tp = torch.empty_like(tp_all)
+        ql = c.select_prefix_dev(tp_all.data_ptr(), ts, q, pbits, rank, tp.data_ptr(), ts, None, stream)
+        oi = torch.empty((max(ql, 1), k), dtype=torch.int32, device=dev)
+        oc = torch.empty(max(ql, 1), dtype=torch.int32, device=dev)
+        pstep = lambda: c.batch_topk_dev(tp.data_ptr(), ts, ql, k, oi.data_ptr(), oc.data_ptr(), None, 0, stream)
+        pstep()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            pstep()
+        torch.cuda.synchronize()
+        dist.barrier()
+        tm = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        ms = float(tm.item()) * 1e3 / steps
+        out["prefix"] = {"ms_per_step": ms, "qps": q / (ms * 1e-3), "ids_per_gpu_rank0": c.num_ids,
+                         "targets_rank0": ql, "scaling": "strong (one global batch, routed by prefix)"}
+    finally:
+        c.close()
+        torch.cuda.synchronize()
+    return out
+
+
+def cpu_baseline(O, ids, tg, a):
+    """Oracle port on the host cores (rank 0, N = 1): std::partial_sort(xorCmp) over the cfg-2
+    set on a bounded target sample at 16 threads and on 1 core, plus the reference's own
+    RoutingTable::findClosestNodes call pattern (cfg 1) and NodeCache::getCachedNodes."""
+    t0 = time.perf_counter()
+    want, _ = O.topk(ids, tg, a.k, threads=a.cpu_threads)
+    dt = time.perf_counter() - t0
+    m1 = min(24, tg.shape[0])
+    t0 = time.perf_counter()
+    O.topk(ids, tg[:m1], a.k, threads=1)
+    dt1 = time.perf_counter() - t0
+    cb = {"value": tg.shape[0] / dt, "unit": "queries/s", "cores": a.cpu_threads, "kind": "port",
+          "sample": f"{tg.shape[0]} targets x {ids.shape[0]} ids, k={a.k}, std::partial_sort(xorCmp) per target, "
+                    f"{a.cpu_threads} threads, {dt:.2f} s wall",
+          "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "compiler": "g++ -O2 (the reference's Release)",
+          "one_core": {"value": m1 / dt1, "unit": "queries/s", "sample": f"{m1} targets, {dt1:.2f} s"}}
+    # cfg 1: findClosestNodes per target over a RoutingTable-shaped snapshot
+    rng = np.random.default_rng(a.seed)
+    myid = np.frombuffer(rng.bytes(20), dtype=np.uint8).copy()
+    firsts, off, nodes = synthetic_table(myid, 11, 8, rng)
+    good = np.ones(nodes.shape[0], np.uint8)
+    tq = np.frombuffer(rng.bytes(20 * 1_000_000), dtype=np.uint8).reshape(-1, 20).copy()
+    fc = {}
+    for th in (1, a.cpu_threads):
+        O.find_closest_batch(firsts, off, nodes, good, tq[:1000], 8, threads=th)
+        t0 = time.perf_counter()
+        O.find_closest_batch(firsts, off, nodes, good, tq, 8, threads=th)
+        d = time.perf_counter() - t0
+        fc[f"threads_{th}"] = {"queries_per_s": tq.shape[0] / d, "us_per_query_per_core": d * th / tq.shape[0] * 1e6}
+    cb["cfg1_find_closest"] = {"table": f"{firsts.shape[0]} buckets, {nodes.shape[0]} nodes", "targets": tq.shape[0],
+                               **fc, "kind": "port (RoutingTable::findClosestNodes restated over a flat snapshot)"}
+    # NodeCache::getCachedNodes over a 10^6-node cache
+    cache = O.gen_ids(a.seed + 9, 1_000_000)
+    cache = cache[np.lexsort(cache.T[::-1])]
+    acc = np.ones(cache.shape[0], np.uint8)
+    gc = {}
+    for th in (1, a.cpu_threads):
+        t0 = time.perf_counter()
+        O.cached_nodes_batch(cache, acc, tq[:200_000], 14, threads=th)
+        d = time.perf_counter() - t0
+        gc[f"threads_{th}"] = {"queries_per_s": 200_000 / d}
+    cb["get_cached_nodes"] = {"cache": "10^6 nodes, count 14", **gc, "kind": "port"}
+    return cb, want
 
 
 if __name__ == "__main__":

@@ -173,6 +173,11 @@ int dhtgpu_batch_topk_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_
 int dhtgpu_batch_topk_timed(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
                             uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, void* stream, float* ms4,
                             uint32_t* stats4);
+/* Arm per-kernel timing of the NEXT K6 call on this context without synchronising it:
+ * its kernels' own dispatches record start/stop into ev8[0..7] (hipEvent_t as void*, created
+ * by the caller with timing enabled) = {F1 start, F1 stop, F2 start, F2 stop, F3 .., F4 ..}
+ * (sub-partitioned calls: sub-partition 0's kernels).  For timing kernels inside a timed loop. */
+int dhtgpu_batch_events(dhtgpu_ctx* ctx, void** ev8);
 /* Host form (synchronous). */
 int dhtgpu_batch_topk(dhtgpu_ctx* ctx, const uint8_t* targets20_be, uint32_t q, uint32_t k,
                       uint32_t* out_idx, uint32_t* out_cnt);

@@ -83,6 +83,7 @@ def lib():
         "dhtgpu_cached_nodes": ([_vp, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p],
                                 ctypes.c_int),
         "dhtgpu_cache_set": ([_vp, _u8p, ctypes.c_uint64, ctypes.c_uint64], ctypes.c_int),
+        "dhtgpu_batch_events": ([_vp, ctypes.POINTER(_vp)], ctypes.c_int),
         "dhtgpu_cache_nodes": ([_vp, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p], ctypes.c_int),
         "dhtgpu_cache_sorted": ([_vp, _u32p], ctypes.c_int),
         "dhtgpu_buffer_nodes_ids": ([_vp, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_uint32, _u32p,
@@ -133,7 +134,7 @@ def exported_symbols():
             "dhtgpu_batch_topk_dev", "dhtgpu_batch_topk_timed", "dhtgpu_batch_topk", "dhtgpu_table_depth",
             "dhtgpu_buffer_nodes_dev", "dhtgpu_buffer_nodes", "dhtgpu_deserialize_nodes", "dhtgpu_net_prepare",
             "dhtgpu_search_batch", "dhtgpu_search_batch_dev", "dhtgpu_set_global_indices", "dhtgpu_cache_set",
-            "dhtgpu_cache_nodes", "dhtgpu_cache_sorted", "dhtgpu_buffer_nodes_ids"]
+            "dhtgpu_cache_nodes", "dhtgpu_cache_sorted", "dhtgpu_buffer_nodes_ids", "dhtgpu_batch_events"]
 
 
 def _ids(a, name="ids"):
@@ -281,6 +282,12 @@ class Context:
         _check(lib().dhtgpu_batch_topk_timed(self._h, t_planes_ptr, t_stride, q, k, out_idx_ptr, out_cnt_ptr,
                                              stream, ms, st), "batch_topk_timed")
         return tuple(ms), int(st[0]), int(st[1]), int(st[2])
+
+    def batch_events(self, events):
+        """Arm per-kernel timing of the next K6 call: `events` = 8 torch.cuda.Event(enable_timing=True)
+        (F1..F4 start/stop, recorded by the kernels' own dispatches; no synchronisation)."""
+        arr = (_vp * 8)(*[e.cuda_event for e in events])
+        _check(lib().dhtgpu_batch_events(self._h, arr), "batch_events")
 
     def topk_dev(self, t_planes_ptr, t_stride, q, k, out_idx_ptr=None, out_cnt_ptr=None, out_rec_ptr=None,
                  idx_base=0, stream=None):

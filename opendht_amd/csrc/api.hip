@@ -107,6 +107,7 @@ struct dhtgpu_ctx {
     DevBuf sub_mask, sub_list, sub_scratch;   // deficient / unplannable sub-partitions: routed to the scan
     bool sub_scratch_clean = false;
     hipStream_t side[2] = {nullptr, nullptr};  // internal streams for sub-calls
+
     hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
     uint32_t shard_pval = 0;
     // lexicographically sorted views (sort.hip): of the main set when it was uploaded unsorted
@@ -121,6 +122,8 @@ struct dhtgpu_ctx {
     DevBuf cache_in, sort_scratch, cache_acc;
     // diagnostics (DHTGPU_DBG, read once at creation; phase stamps per context)
     uint32_t dbg = 0;
+    hipEvent_t next_ev[8] = {};   // dhtgpu_batch_events: the next K6 call records its kernels here
+    bool has_next_ev = false;
     DevBuf stamps;
 
     hipError_t bind() { return hipSetDevice(device); }
@@ -725,6 +728,12 @@ static bool needs_subs(const dhtgpu_ctx* c, uint32_t q, uint32_t k) {
 
 static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k, uint32_t* out_idx,
                      uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base, hipStream_t s, hipEvent_t* ev) {
+    hipEvent_t evs[8];
+    if (!ev && c->has_next_ev) {   // armed by dhtgpu_batch_events: this call only
+        for (int i = 0; i < 8; ++i) evs[i] = c->next_ev[i];
+        c->has_next_ev = false;
+        ev = evs;
+    }
     if (needs_subs(c, q, k)) return batch_run_subs(c, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s, ev);
     if (!batch_supported(c->n, q, k, c->num_cus)) return DHTGPU_ERANGE;
     const int si = c->bnext;
@@ -775,6 +784,16 @@ int dhtgpu_batch_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     DHT_TRY(c->bind());
     return batch_run(c, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base,
                      stream ? (hipStream_t)stream : c->stream, nullptr);
+}
+
+int dhtgpu_batch_events(dhtgpu_ctx* c, void** ev8) {
+    if (!c || !ev8) return DHTGPU_EINVAL;
+    for (int i = 0; i < 8; ++i) {
+        if (!ev8[i]) return DHTGPU_EINVAL;
+        c->next_ev[i] = (hipEvent_t)ev8[i];
+    }
+    c->has_next_ev = true;
+    return DHTGPU_OK;
 }
 
 int dhtgpu_batch_topk_timed(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k,

@@ -140,34 +140,41 @@ constexpr uint32_t kSpill = 8;   // ctr word: spilled targets (all-zero between 
 // Sub-partition calls (dhtgpu_ctx's prefix sub-partitions of a large id set) keep only the
 // targets whose bits [sel_shift, sel_shift + sel_bits) equal sel_val; the others belong to
 // another sub-partition's call.
-__global__ __launch_bounds__(kF1Threads) void k_f1_targets(const uint32_t* __restrict__ tw0,
-                                                          const uint32_t* __restrict__ tw1, uint32_t q, uint32_t Lm,
-                                                          uint32_t b1, uint32_t shift, uint32_t sel_shift,
-                                                          uint32_t sel_bits, uint32_t sel_val,
-                                                          uint32_t* __restrict__ bitmap, uint32_t* __restrict__ tcount,
-                                                          uint2* __restrict__ tbuf, uint32_t tcap,
-                                                          uint32_t* __restrict__ ctr, uint32_t* __restrict__ tspill) {
-    if (blockIdx.x == 0 && threadIdx.x < 4) ctr[threadIdx.x] = 0;   // fallback, survivors, wave path, -
+
+struct F1Args {
+    const uint32_t* tw0; const uint32_t* tw1;
+    uint32_t q, Lm, b1, shift, sel_shift, sel_bits, sel_val;
+    uint32_t* bitmap;
+    uint32_t* tcount; uint2* tbuf; uint32_t tcap;
+    uint32_t* ctr; uint32_t* tspill;
+};
+
+__device__ __forceinline__ bool f1_keep(const F1Args& a, uint32_t w) {
+    return !a.sel_bits || ((w << a.sel_shift) >> (32 - a.sel_bits)) == a.sel_val;
+}
+
+__global__ __launch_bounds__(kF1Threads) void k_f1_targets(F1Args a) {
+    if (blockIdx.x == 0 && threadIdx.x < 4) a.ctr[threadIdx.x] = 0;   // fallback, survivors, wave path, -
     const uint32_t i = blockIdx.x * kF1Threads + threadIdx.x;
-    if (i >= q) return;
-    const uint32_t w = tw0[i];
-    if (sel_bits && ((w << sel_shift) >> (32 - sel_bits)) != sel_val) return;
-    const uint32_t v = shift ? (w << shift) | (tw1[i] >> (32 - shift)) : w;
-    const uint32_t pre = top_bits(v, Lm);
-    atomicOr(bitmap + (pre >> 5), 1u << (pre & 31));
-    const uint32_t p = top_bits(v, b1);
-    const uint32_t slot = atomicAdd(tcount + p * kCtrStride, 1u);
-    if (slot < tcap) {
-        tbuf[(uint64_t)p * tcap + slot] = make_uint2(v, i);
+    if (i >= a.q) return;
+    const uint32_t w = a.tw0[i];
+    if (!f1_keep(a, w)) return;
+    const uint32_t v = a.shift ? (w << a.shift) | (a.tw1[i] >> (32 - a.shift)) : w;
+    const uint32_t pre = top_bits(v, a.Lm);
+    atomicOr(a.bitmap + (pre >> 5), 1u << (pre & 31));
+    const uint32_t p = top_bits(v, a.b1);
+    const uint32_t slot = atomicAdd(a.tcount + p * kCtrStride, 1u);
+    if (slot < a.tcap) {
+        a.tbuf[(uint64_t)p * a.tcap + slot] = make_uint2(v, i);
         return;
     }
     // spill: one atomic per wave (a single counter would serialise every lane's add)
     const uint64_t sp = __ballot(1);   // the lanes still here (the others returned)
     const uint32_t lane = lane_id();
     uint32_t base = 0;
-    if (lane == (uint32_t)__ffsll((long long)sp) - 1) base = atomicAdd(ctr + kSpill, (uint32_t)__popcll(sp));
+    if (lane == (uint32_t)__ffsll((long long)sp) - 1) base = atomicAdd(a.ctr + kSpill, (uint32_t)__popcll(sp));
     base = __shfl((int)base, __ffsll((long long)sp) - 1);
-    tspill[base + (uint32_t)__popcll(sp & ((1ull << lane) - 1ull))] = i;
+    a.tspill[base + (uint32_t)__popcll(sp & ((1ull << lane) - 1ull))] = i;
 }
 
 // ---- F2: stream w0, keep ids in marked subtrees, partition them ----------------------
@@ -303,8 +310,10 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     const uint32_t lm5 = a.Lm > 5 ? a.Lm - 5 : 0u;   // word index width
     const uint32_t tid4 = 4 * threadIdx.x;
     // the prefix bitmap first (ahead of the ring, its loads land first: measured 1 µs better
-    // per block than ring-first); indices past the end are clamped, so a clamped lane
-    // rewrites a word with its own value
+    // per block than ring-first; per-XCD copies stored by F1 -- L2-resident on paper -- did not
+    // shorten this phase either: it is the fabric, not the source); indices past the end are
+    // clamped, so a clamped lane rewrites a word with its own value
+    const uint32_t* bsrc = a.bitmap;
     if ((a.nwords & 3) == 0) {
         for (uint32_t i0 = 0; i0 < a.nwords; i0 += kF2Threads * 16) {
             uint4 t[4];
@@ -314,13 +323,13 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                 uint32_t i = i0 + (r * kF2Threads + threadIdx.x) * 4;
                 if (a.dbg & 512) i = (i + (blockIdx.x & 31) * 512) & (a.nwords - 1);   // experiment: rotated start
                 ic[r] = i < a.nwords ? i : a.nwords - 4;
-                t[r] = *reinterpret_cast<const uint4*>(a.bitmap + ic[r]);
+                t[r] = *reinterpret_cast<const uint4*>(bsrc + ic[r]);
             }
 #pragma unroll
             for (uint32_t r = 0; r < 4; ++r) *reinterpret_cast<uint4*>(bm + ic[r]) = t[r];
         }
     } else {
-        for (uint32_t i = threadIdx.x; i < a.nwords; i += kF2Threads) bm[i] = a.bitmap[i];
+        for (uint32_t i = threadIdx.x; i < a.nwords; i += kF2Threads) bm[i] = bsrc[i];
     }
     // ring of kRing sub-steps (one 16-B load per lane each) in flight: 128 KB per CU.
     // Loads past the block's range are clamped to its last 16 B (cache hits, masked).
@@ -488,8 +497,9 @@ struct F3Args {
     uint32_t* out_idx; uint32_t* out_cnt;
     uint32_t* ctr; uint32_t* fb_list;   // ctr[0] = fallback targets
     uint32_t* pstat;                     // [np] survivors per partition (statistics; plain stores)
-    uint4* tie_hdr;                      // [np][kTieSlots] deferred ties {qi, t0, count, 0} (count 0 = free)
+    uint4* tie_hdr;                      // [np][kTieSlots] deferred ties {qi, t0, count, 0}
     uint2* tie_cand;                     // [np][kTieSlots][64] their candidates {w0, idx}
+    uint32_t* tie_cnt;                   // [np] deferred-tie slots in use per partition (all-zero between calls)
     uint32_t dbg;
     unsigned long long* stamps;          // dbg & 256: per-block phase timestamps [np][16]
 };
@@ -865,29 +875,31 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     // address serialises at the memory side: 1,000 of them held this kernel ~10 µs)
     sync_lds();
     if (threadIdx.x == 0 && ntie[1]) atomicAdd(a.ctr + 2, ntie[1]);
+    // this partition's deferred ties for F4 (a plain store: no shared counter to serialise on)
+    if (threadIdx.x == 0 && ntie[0]) a.tie_cnt[p] = ntie[0] < kTieSlots ? ntie[0] : kTieSlots;
     F3_STAMP(7);
 }
 
 // ---- F4: the fallback targets (K1 scan, run-time roles) and the deferred ties -------------
-// Blocks [0, nfb): the fallback list (count ctr[0], known only on the device) is answered by
+// Every block first answers the ties F3 deferred in its share of the partitions (one wave per
+// slot: wave_rank_answer on the copied candidates), then the fallback list (count ctr[0],
+// known only on the device) is answered by
 // the K1 streaming scan over all ids: target groups of 128 (8 waves x 16) x id-range splits,
 // S = min(nfb / groups, 256 / k) so that the chip fills however short the list is; with
 // S > 1 every split writes its sorted candidate records and the last split of a group to
 // finish (agent-scope counter, sc1 records: MI355X_MICROARCH inter-workgroup hand-off)
 // merges the group's S lists per target (a k-way merge over the list heads, one wave per
-// target).  Blocks [nfb, nfb + np): the ties F3 partition blockIdx - nfb deferred, one wave
-// per slot (wave_rank_answer on the copied candidates); a slot is freed (count 0) once
-// answered, so the headers are all-zero between calls.
+// target).
 constexpr uint32_t kF4Threads = scan::WAVES * 64;                 // 512
 constexpr uint32_t kFbGroup = scan::WAVES * kScanTargets;          // targets per scan role
 constexpr uint32_t kFbBlocks = 256;                                // fallback-scan workgroups
 constexpr uint32_t kFbCands = 256;                                 // merge: splits * k <= 256
-static_assert(kTieSlots == kF4Threads / 64, "one F4 tie block per partition, a wave per slot");
 
 struct FbArgs {
-    uint32_t* rec;    // [kFbBlocks * kFbGroup * k * 6] split lists (S > 1 only)
-    uint32_t* done;   // [kFbBlocks] per-group split completion counters (all-zero between calls)
-    uint32_t nfb;     // fallback-scan blocks at the front of the grid
+    uint32_t* rec;      // [kFbBlocks * kFbGroup * k * 6] split lists (S > 1 only)
+    uint32_t* done;     // [kFbBlocks] per-group split completion counters (all-zero between calls)
+    uint32_t nfb;       // fallback-scan workgroups (the grid)
+    uint32_t np_ties;   // partitions whose deferred ties F4 answers (0: a list scan)
 };
 
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
@@ -961,16 +973,35 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[scan::lds_words<kScanTargets>()];
     __shared__ uint32_t last;
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-    if (blockIdx.x >= f.nfb) {   // deferred ties: one slot per wave, header and candidates in one round trip
+    // deferred ties of the block's partitions p = blockIdx + j * gridDim (j < ppb <= 64): lane j
+    // loads partition j's count, a wave scan numbers the block's ties, and the waves take them
+    // round-robin -- every tie in flight at once (one round trip for the counts)
+    if (f.np_ties) {
         const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
-        const uint32_t g = (blockIdx.x - f.nfb) * kTieSlots + wv;
-        const uint4 h = a.tie_hdr[g];
-        const uint2 c = a.tie_cand[(uint64_t)g * 64 + lane];
-        const uint32_t mm = __builtin_amdgcn_readfirstlane(h.z);
-        if (mm == 0) return;
-        wave_rank_answer(a, c, mm, __builtin_amdgcn_readfirstlane(h.x), __builtin_amdgcn_readfirstlane(h.y), want, lane);
-        if (lane == 0) a.tie_hdr[g].z = 0;
-        return;
+        const uint32_t ppb = (f.np_ties + gridDim.x - 1) / gridDim.x;
+        const uint32_t pj = blockIdx.x + lane * gridDim.x;
+        const bool mine = lane < ppb && pj < f.np_ties;
+        const uint32_t myc = mine ? a.tie_cnt[pj] : 0u;
+        uint32_t inc = myc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+            if (lane >= (uint32_t)o) inc += y;
+        }
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        for (uint32_t t = wv; t < total; t += scan::WAVES) {
+            const uint32_t j = (uint32_t)__popcll(__ballot(inc <= t));   // partition j holds tie t
+            const uint32_t before = j ? (uint32_t)__builtin_amdgcn_readlane((int)inc, (int)j - 1) : 0u;
+            const uint32_t g = (blockIdx.x + j * gridDim.x) * kTieSlots + (t - before);
+            const uint4 h = a.tie_hdr[g];
+            const uint2 c = a.tie_cand[(uint64_t)g * 64 + lane];
+            wave_rank_answer(a, c, __builtin_amdgcn_readfirstlane(h.z), __builtin_amdgcn_readfirstlane(h.x),
+                             __builtin_amdgcn_readfirstlane(h.y), want, lane);
+        }
+        if (total) {   // block-uniform: every wave has read the counts before they are cleared
+            __syncthreads();
+            if (threadIdx.x < 64 && mine && myc) a.tie_cnt[pj] = 0;   // all-zero again for the next call
+        }
     }
     const uint32_t cnt = a.ctr[0];
     if (cnt == 0) return;
@@ -1219,7 +1250,8 @@ void set_lds_attributes() {
 }
 
 // workspace: bitmap (64 KB) | ctr[64] | pcount[kMaxParts] | tcount[kMaxParts * kCtrStride] |
-// tie_hdr[kMaxParts * kTieSlots] | fb done[kFbBlocks] -- all-zero between calls -- | fb_list[q] |
+// tie_hdr[kMaxParts * kTieSlots] | fb done[kFbBlocks] | tie_cnt[kMaxParts] -- all-zero between calls -- |
+// fb_list[q] |
 // tspill[q] | pstat[np] | tbuf[np * tcap] | tie_cand[np * kTieSlots * 64] | pbuf[np * kF3Cap] |
 // fb rec[kFbBlocks * kFbGroup * k * 6]
 constexpr uint32_t kMaxParts = 1u << 13;
@@ -1238,7 +1270,7 @@ bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
 
 size_t batch_clean_bytes() {
     return 65536 + 256 + (size_t)kMaxParts * 4 + (size_t)kMaxParts * kCtrStride * 4 + (size_t)kMaxParts * kTieSlots * 16 +
-           al256((size_t)kFbBlocks * 4);
+           al256((size_t)kFbBlocks * 4) + (size_t)kMaxParts * 4;
 }
 
 size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus) {
@@ -1300,6 +1332,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     uint32_t* tcount = reinterpret_cast<uint32_t*>(take((size_t)kMaxParts * kCtrStride * 4));
     uint4* tie_hdr = reinterpret_cast<uint4*>(take((size_t)kMaxParts * kTieSlots * 16));
     uint32_t* fb_done = reinterpret_cast<uint32_t*>(take((size_t)kFbBlocks * 4));
+    uint32_t* tie_cnt = reinterpret_cast<uint32_t*>(take((size_t)kMaxParts * 4));
     uint32_t* fb_list = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
     uint32_t* tspill = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
     uint32_t* pstat = reinterpret_cast<uint32_t*>(take((size_t)np * 4));
@@ -1315,8 +1348,9 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     };
     unsigned long long* stamps = (dbg & 256) ? c.stamps : nullptr;   // F3 [8192][16] then F2 [8192][16]
     if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)2 * 8192 * 16 * 8, s);
-    go(0, k_f1_targets, dim3((q + kF1Threads - 1) / kF1Threads), dim3(kF1Threads), 0, c.tp, c.tp + c.ts, q, P.Lm, P.b1,
-       c.skip, c.sel_shift, c.sel_bits, c.sel_val, bitmap, tcount, tbuf, P.tcap, ctr, tspill);
+    const F1Args a1{c.tp, c.tp + c.ts, q, P.Lm, P.b1, c.skip, c.sel_shift, c.sel_bits, c.sel_val, bitmap, tcount, tbuf,
+                    P.tcap, ctr, tspill};
+    go(0, k_f1_targets, dim3((q + kF1Threads - 1) / kF1Threads), dim3(kF1Threads), 0, a1);
     const uint32_t* planes = c.planes;
     const uint64_t stride = c.stride;
     if (n) {
@@ -1341,7 +1375,8 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     }
     if (dirty && (dbg & 48u)) *dirty = true;   // F3 ablation exits leave counters behind
     F3Args a{pbuf, pcount, kF3Cap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, planes, stride, n,
-             c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, pstat, tie_hdr, tie_cand, dbg, stamps};
+             c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, pstat, tie_hdr, tie_cand, tie_cnt, dbg,
+             stamps};
     size_t l3 = f3_lds(P);
     if (dbg & 4096) l3 = l3 > 81920 ? l3 : 81920;   // experiment: 2 F3 blocks per CU
     if (dbg & 8192) l3 = l3 > 54000 ? l3 : 54000;   // experiment: 3 F3 blocks per CU
@@ -1363,8 +1398,8 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     }
 #undef F3_GO
     if (dbg & 256) print_phase_profile(P, np, stamps, s);
-    const FbArgs fa{fb_rec, fb_done, kFbBlocks};
-    const dim3 g4(kFbBlocks + np), b4(kF4Threads);
+    const FbArgs fa{fb_rec, fb_done, kFbBlocks, np};
+    const dim3 g4(kFbBlocks), b4(kF4Threads);
     if (k <= 8) go(3, k_f4<8>, g4, b4, 0, a, fa);
     else if (k <= 16) go(3, k_f4<16>, g4, b4, 0, a, fa);
     else go(3, k_f4<32>, g4, b4, 0, a, fa);
@@ -1420,7 +1455,7 @@ hipError_t launch_list_scan(const uint32_t* planes, uint64_t stride, uint64_t n,
     a.ctr = const_cast<uint32_t*>(d_cnt);          // F4 reads the list length from ctr[0]
     a.fb_list = const_cast<uint32_t*>(list);
     const FbArgs fa{reinterpret_cast<uint32_t*>(w + al256((size_t)kFbBlocks * 4)), reinterpret_cast<uint32_t*>(w),
-                    kFbBlocks};
+                    kFbBlocks, 0u};
     if (k <= 8) k_f4<8><<<kFbBlocks, kF4Threads, 0, s>>>(a, fa);
     else if (k <= 16) k_f4<16><<<kFbBlocks, kF4Threads, 0, s>>>(a, fa);
     else k_f4<32><<<kFbBlocks, kF4Threads, 0, s>>>(a, fa);

@@ -279,6 +279,16 @@ uint32_t orc_find_closest(uint32_t nb, const uint8_t* firsts20, const uint32_t* 
     return (uint32_t)nodes.size();
 }
 
+/* One findClosestNodes per target (the responder loop of Dht::onFindNode, src/dht.cpp:2128-2138,
+ * over many requests); out_idx[q * count], out_cnt[q].  Threads split the targets. */
+void orc_find_closest_batch(uint32_t nb, const uint8_t* firsts20, const uint32_t* off, const uint8_t* ids20,
+                            const uint8_t* good, const uint8_t* targets20, uint32_t q, uint32_t count,
+                            uint32_t* out_idx, uint32_t* out_cnt, int threads) {
+    parallel_for(q, threads, [&](uint64_t i) {
+        out_cnt[i] = orc_find_closest(nb, firsts20, off, ids20, good, targets20 + 20 * i, count, out_idx + i * count);
+    });
+}
+
 void orc_classify(uint32_t nb, const uint8_t* firsts20, const uint8_t* myid20,
                   const uint8_t* ids20, uint64_t n, uint8_t* out_bucket, uint64_t* hist161) {
     for (unsigned i = 0; i <= 8 * HASH_LEN; i++) hist161[i] = 0;
@@ -316,6 +326,14 @@ uint32_t orc_cached_nodes(const uint8_t* sorted_ids20, uint64_t n, const uint8_t
         if (accept[it]) out_idx[cnt++] = (uint32_t)it;
     }
     return cnt;
+}
+
+/* One getCachedNodes per target (Dht::refill, src/dht.cpp:656-677, over many searches). */
+void orc_cached_nodes_batch(const uint8_t* sorted_ids20, uint64_t n, const uint8_t* accept, const uint8_t* targets20,
+                            uint32_t q, uint32_t count, uint32_t* out_idx, uint32_t* out_cnt, int threads) {
+    parallel_for(q, threads, [&](uint64_t i) {
+        out_cnt[i] = orc_cached_nodes(sorted_ids20, n, accept, targets20 + 20 * i, count, out_idx + i * count);
+    });
 }
 
 /* ---- compact node wire format (src/network_engine.cpp) ------------------------------ */

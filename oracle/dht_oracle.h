@@ -65,6 +65,10 @@ unsigned orc_depth(uint32_t nb, const uint8_t* firsts20, uint32_t b);
 uint32_t orc_find_closest(uint32_t nb, const uint8_t* firsts20, const uint32_t* off,
                           const uint8_t* ids20, const uint8_t* good, const uint8_t* target20,
                           uint32_t count, uint32_t* out_idx);
+/* orc_find_closest for q targets (out_idx[q*count], out_cnt[q]) on `threads` threads. */
+void orc_find_closest_batch(uint32_t nb, const uint8_t* firsts20, const uint32_t* off, const uint8_t* ids20,
+                            const uint8_t* good, const uint8_t* targets20, uint32_t q, uint32_t count,
+                            uint32_t* out_idx, uint32_t* out_cnt, int threads);
 /* findBucket + commonBits classification (cfg 4). */
 void orc_classify(uint32_t nb, const uint8_t* firsts20, const uint8_t* myid20,
                   const uint8_t* ids20, uint64_t n, uint8_t* out_bucket, uint64_t* hist161);
@@ -74,6 +78,9 @@ void orc_classify(uint32_t nb, const uint8_t* firsts20, const uint8_t* myid20,
 uint32_t orc_cached_nodes(const uint8_t* sorted_ids20, uint64_t n, const uint8_t* accept,
                           const uint8_t* target20, uint32_t count, uint32_t* out_idx);
 
+/* orc_cached_nodes for q targets (out_idx[q*count], out_cnt[q]) on `threads` threads. */
+void orc_cached_nodes_batch(const uint8_t* sorted_ids20, uint64_t n, const uint8_t* accept, const uint8_t* targets20,
+                            uint32_t q, uint32_t count, uint32_t* out_idx, uint32_t* out_cnt, int threads);
 /* NetworkEngine::bufferNodes (src/network_engine.cpp:1003-1032): sort candidates by xorCmp
  * to the target, keep 8, pack 26 (IPv4, alen 4) / 38 (IPv6, alen 16) byte records.
  * tail[i] = node i's address || port bytes.  Returns the blob length. */

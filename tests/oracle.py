@@ -54,6 +54,10 @@ def lib():
         L.orc_find_closest.argtypes = [ctypes.c_uint32, u8p, u32p, u8p, u8p, u8p, ctypes.c_uint32, u32p]
         L.orc_find_closest.restype = ctypes.c_uint32
         L.orc_classify.argtypes = [ctypes.c_uint32, u8p, u8p, u8p, ctypes.c_uint64, u8p, u64p]
+        L.orc_find_closest_batch.argtypes = [ctypes.c_uint32, u8p, u32p, u8p, u8p, u8p, ctypes.c_uint32,
+                                             ctypes.c_uint32, u32p, u32p, ctypes.c_int]
+        L.orc_cached_nodes_batch.argtypes = [u8p, ctypes.c_uint64, u8p, u8p, ctypes.c_uint32, ctypes.c_uint32,
+                                             u32p, u32p, ctypes.c_int]
         L.orc_cached_nodes.argtypes = [u8p, ctypes.c_uint64, u8p, u8p, ctypes.c_uint32, u32p]
         L.orc_cached_nodes.restype = ctypes.c_uint32
         L.orc_buffer_nodes.argtypes = [u8p, u8p, ctypes.c_uint32, u8p, u32p, ctypes.c_uint32, u8p]
@@ -158,6 +162,33 @@ def find_closest(firsts, off, ids, good, target, count):
     c = lib().orc_find_closest(firsts.shape[0], _p(firsts, u8p), _p(off, u32p), _p(ids, u8p),
                                _p(good, u8p), _p(target, u8p), count, _p(out, u32p))
     return out[:c].copy()
+
+
+def find_closest_batch(firsts, off, ids, good, targets, count, threads=1):
+    """findClosestNodes for every target: ((q, count) indices, UINT32_MAX padded; (q,) counts)."""
+    firsts = np.ascontiguousarray(firsts, dtype=np.uint8)
+    ids = np.ascontiguousarray(ids, dtype=np.uint8)
+    good = np.ascontiguousarray(good, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint32)
+    targets = np.ascontiguousarray(targets, dtype=np.uint8)
+    q = targets.shape[0]
+    out = np.full((q, count), 0xFFFFFFFF, dtype=np.uint32)
+    cnt = np.zeros(q, dtype=np.uint32)
+    lib().orc_find_closest_batch(firsts.shape[0], _p(firsts, u8p), _p(off, u32p), _p(ids, u8p), _p(good, u8p),
+                                 _p(targets, u8p), q, count, _p(out, u32p), _p(cnt, u32p), threads)
+    return out, cnt
+
+
+def cached_nodes_batch(sorted_ids, accept, targets, count, threads=1):
+    sorted_ids = np.ascontiguousarray(sorted_ids, dtype=np.uint8)
+    accept = np.ascontiguousarray(accept, dtype=np.uint8)
+    targets = np.ascontiguousarray(targets, dtype=np.uint8)
+    q = targets.shape[0]
+    out = np.full((q, count), 0xFFFFFFFF, dtype=np.uint32)
+    cnt = np.zeros(q, dtype=np.uint32)
+    lib().orc_cached_nodes_batch(_p(sorted_ids, u8p), sorted_ids.shape[0], _p(accept, u8p), _p(targets, u8p), q,
+                                 count, _p(out, u32p), _p(cnt, u32p), threads)
+    return out, cnt
 
 
 def classify(firsts, myid, ids):

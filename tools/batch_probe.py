@@ -16,6 +16,7 @@ ap.add_argument("--k", type=int, default=8)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--algo", default="batch")
 ap.add_argument("--prefix", type=int, default=0, help="prefix shard: keep ids with top PREFIX bits == 0 of 2^PREFIX x n")
+ap.add_argument("--evict", action="store_true", help="write 512 MiB before every call (Infinity Cache evicted)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
@@ -36,7 +37,12 @@ oi = torch.empty((a.q, a.k), dtype=torch.int32, device=dev)
 oc = torch.empty(a.q, dtype=torch.int32, device=dev)
 
 
+ebuf = torch.zeros(128 << 20, dtype=torch.int32, device=dev) if a.evict else None
+
+
 def call():
+    if ebuf is not None:
+        ebuf.sum()
     if a.algo == "batch":
         ctx.batch_topk_dev(tp.data_ptr(), ts, a.q, a.k, oi.data_ptr(), oc.data_ptr(), None, 0, s)
     else:

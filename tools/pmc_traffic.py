@@ -1,9 +1,11 @@
 """HBM traffic per launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE), per kernel.
 
-usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json
+usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json WORKLOAD
 FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reports half the bytes of wide
 (16 B/lane) streaming reads (MI355X_MICROARCH.md, HBM section): it is doubled here.
-WRITE_SIZE is taken as is.  Infinity-Cache hits are counted by these counters."""
+WRITE_SIZE is taken as is.  Infinity-Cache hits are counted by these counters, so only a
+workload that does not fit the 256 MiB L3 (or evicts it between calls) reads as HBM traffic.
+Results are merged into OUT.json under workloads[WORKLOAD] (the key bench.py looks up)."""
 import collections
 import csv
 import json
@@ -32,8 +34,12 @@ for k in sorted(set(fetch) | set(write)):
     f = 2.0 * fetch.get(k, 0.0)
     w = write.get(k, 0.0)
     res[k] = {"fetch_bytes": f, "write_bytes": w, "traffic_bytes": f + w}
-json.dump({"note": "per-launch HBM bytes: 2 x FETCH_SIZE (gfx950 wide-read correction) + WRITE_SIZE; "
-                   "collected with separate rocprofv3 --pmc passes on tools/batch_probe.py (cfg 2)",
-           "workload": [1 << 24, 65536, 8],
-           "kernels": res}, open(sys.argv[3], "w"), indent=1)
-print(json.dumps(res, indent=1))
+try:
+    doc = json.load(open(sys.argv[3]))
+except (OSError, ValueError):
+    doc = {}
+doc["note"] = ("per-launch HBM-side bytes: 2 x FETCH_SIZE (gfx950 wide-read correction) + WRITE_SIZE, averaged over "
+               "the launches of each kernel; separate rocprofv3 --pmc passes on tools/batch_probe.py")
+doc.setdefault("workloads", {})[sys.argv[4]] = res
+json.dump(doc, open(sys.argv[3], "w"), indent=1)
+print(sys.argv[4], json.dumps(res, indent=1))
