@@ -53,7 +53,7 @@ sys.path.insert(0, ROOT)
 # Two batches in flight (--inflight) need their streams on different hardware queues; HIP's
 # default of 4 queues per process is shared round-robin by every stream the process creates
 # (torch's, the contexts'), so ask for 8 before the runtime starts.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("DHT_BENCH_HW_QUEUES", "8")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -23,6 +23,9 @@
  *   dhtgpu_deserialize_nodes  NetworkEngine::deserializeNodes (src/network_engine.cpp:849-887)
  *   dhtgpu_search_batch    Dht::Search node refresh: Search::insertNode (src/search.h:636-722)
  *                          driven by find_node rounds (crawl replay, tools/dhtscanner.cpp)
+ *   dhtgpu_search_insert   Search::insertNode (src/search.h:636-722) itself, batched over searches
+ *   dhtgpu_table_stats     InfoHash::lowbit + RoutingTable::depth of every bucket, on the device
+ *   dhtgpu_cache_set/_nodes  NodeCache's map (node_cache.h:43) sorted on the device + getCachedNodes
  *
  * Threading (mirrors the reference, src/dhtrunner.cpp:115-150): one context per
  * thread, or external locking; every host-pointer call is synchronous.
@@ -263,6 +266,26 @@ int dhtgpu_deserialize_nodes(dhtgpu_ctx* ctx, uint32_t af, const uint8_t* myid20
                              const uint64_t* msg_off, uint32_t m, const uint8_t* from_af, const uint8_t* from_addr,
                              uint8_t* out_ids20, uint8_t* out_tail, uint8_t* out_status, uint8_t* msg_status,
                              uint32_t* out_nrec);
+
+/* ---- a10: Dht::Search::insertNode (src/search.h:636-722), batched ------------------------ */
+/* q searches (targets20[q]): search s holds list_len[s] <= cap SearchNodes list_node[s*cap ..]
+ * (indices into node_ids20[nn * 20], closest first) with list_flags (bit0 candidate, bit1
+ * replied) and search_expired[s] (Search::expired).  Its insertions ins_node[ins_off[s] ..
+ * ins_off[s+1]) (ins_token != 0: the node replied with a token) are applied in order with the
+ * reference's ordering, trimming to SEARCH_NODES = 14 non-bad nodes (isBad = isExpired() ||
+ * candidate, :352-354) and removeExpiredNode (:541-551); ins_added = insertNode's result.
+ * node_state[nn]: bit0 Node::isExpired(), bit1 Node::isRemovable(now) (node.h:87-89), a
+ * snapshot like the good mask of dhtgpu_find_closest.  Lists are updated in place;
+ * DHTGPU_ERANGE if a list would outgrow cap (that insertion is dropped). */
+int dhtgpu_search_insert(dhtgpu_ctx* ctx, const uint8_t* node_ids20, const uint8_t* node_state, uint32_t nn,
+                         const uint8_t* targets20, uint32_t q, uint32_t cap, uint32_t* list_node, uint8_t* list_flags,
+                         uint32_t* list_len, uint8_t* search_expired, const uint64_t* ins_off, const uint32_t* ins_node,
+                         const uint8_t* ins_token, uint8_t* ins_added);
+
+/* ---- a4 / a6: InfoHash::lowbit (infohash.h:132-143) + RoutingTable::depth per bucket ------ */
+/* out_lowbit[b] = lowbit(first[b]) (-1 for the zero id), out_depth[b] = depth of bucket b
+ * (src/routing_table.cpp:100-107) for every bucket of a table snapshot, on the device. */
+int dhtgpu_table_stats(dhtgpu_ctx* ctx, uint32_t nb, const uint8_t* firsts20, int32_t* out_lowbit, uint32_t* out_depth);
 
 /* ---- f3: crawl replay (BASELINE configs[4]) -------------------------------------------- */
 /* The context's id set becomes a synthetic network (model: opendht_amd/csrc/crawl.hip and

@@ -23,6 +23,8 @@ __all__ = ["Context", "DhtGpuError", "NONE", "MAX_K", "lib", "LIB_PATH", "id_wor
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdhtgpu.so")
 NONE = 0xFFFFFFFF
 MAX_K = 32
+# status codes (include/dhtgpu.h)
+EINVAL, ENOMEM, EDEVICE, ENOIDS, EUNSORTED, ERANGE = -1, -2, -3, -4, -5, -6
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -84,6 +86,9 @@ def lib():
                                 ctypes.c_int),
         "dhtgpu_cache_set": ([_vp, _u8p, ctypes.c_uint64, ctypes.c_uint64], ctypes.c_int),
         "dhtgpu_batch_events": ([_vp, ctypes.POINTER(_vp)], ctypes.c_int),
+        "dhtgpu_search_insert": ([_vp, _u8p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u8p,
+                                  _u32p, _u8p, _u64p, _u32p, _u8p, _u8p], ctypes.c_int),
+        "dhtgpu_table_stats": ([_vp, ctypes.c_uint32, _u8p, ctypes.POINTER(ctypes.c_int32), _u32p], ctypes.c_int),
         "dhtgpu_cache_nodes": ([_vp, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p], ctypes.c_int),
         "dhtgpu_cache_sorted": ([_vp, _u32p], ctypes.c_int),
         "dhtgpu_buffer_nodes_ids": ([_vp, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_uint32, _u32p,
@@ -134,7 +139,8 @@ def exported_symbols():
             "dhtgpu_batch_topk_dev", "dhtgpu_batch_topk_timed", "dhtgpu_batch_topk", "dhtgpu_table_depth",
             "dhtgpu_buffer_nodes_dev", "dhtgpu_buffer_nodes", "dhtgpu_deserialize_nodes", "dhtgpu_net_prepare",
             "dhtgpu_search_batch", "dhtgpu_search_batch_dev", "dhtgpu_set_global_indices", "dhtgpu_cache_set",
-            "dhtgpu_cache_nodes", "dhtgpu_cache_sorted", "dhtgpu_buffer_nodes_ids", "dhtgpu_batch_events"]
+            "dhtgpu_cache_nodes", "dhtgpu_cache_sorted", "dhtgpu_buffer_nodes_ids", "dhtgpu_batch_events",
+            "dhtgpu_search_insert", "dhtgpu_table_stats"]
 
 
 def _ids(a, name="ids"):
@@ -440,6 +446,41 @@ class Context:
                                              _p(t, _u8p), q, _p(cand, _u32p), cand.shape[1], _p(out, _u8p),
                                              _p(ln, _u32p)), "buffer_nodes_ids")
         return out, ln
+
+
+    # ---- a10: Search::insertNode, batched -----------------------------------------------------
+    def search_insert(self, node_ids, node_state, targets, lists, flags, lens, expired, ins_off, ins_node,
+                      ins_token):
+        """Apply insertions (CSR ins_off over searches) to the search lists in place-copies:
+        returns (lists, flags, lens, expired, added)."""
+        nodes = _ids(node_ids, "node_ids")
+        st = np.ascontiguousarray(node_state, dtype=np.uint8)
+        t = _ids(targets, "targets")
+        q = t.shape[0]
+        lists = np.ascontiguousarray(lists, dtype=np.uint32).copy()
+        cap = lists.shape[1]
+        flags = np.ascontiguousarray(flags, dtype=np.uint8).copy()
+        lens = np.ascontiguousarray(lens, dtype=np.uint32).copy()
+        expired = np.ascontiguousarray(expired, dtype=np.uint8).copy()
+        off = np.ascontiguousarray(ins_off, dtype=np.uint64)
+        node = np.ascontiguousarray(ins_node, dtype=np.uint32)
+        tok = np.ascontiguousarray(ins_token, dtype=np.uint8)
+        added = np.zeros(max(node.size, 1), np.uint8)
+        _check(lib().dhtgpu_search_insert(self._h, _p(nodes, _u8p), _p(st, _u8p), nodes.shape[0], _p(t, _u8p), q, cap,
+                                          _p(lists, _u32p), _p(flags, _u8p), _p(lens, _u32p), _p(expired, _u8p),
+                                          _p(off, _u64p), _p(node, _u32p) if node.size else None,
+                                          _p(tok, _u8p) if tok.size else None, _p(added, _u8p)), "search_insert")
+        return lists, flags, lens, expired, added[: node.size]
+
+    def table_stats(self, firsts):
+        """(lowbit, depth) of every bucket of a table snapshot, computed on the device."""
+        f = _ids(firsts, "firsts")
+        nb = f.shape[0]
+        lb = np.zeros(max(nb, 1), np.int32)
+        dp = np.zeros(max(nb, 1), np.uint32)
+        _check(lib().dhtgpu_table_stats(self._h, nb, _p(f, _u8p), lb.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                        _p(dp, _u32p)), "table_stats")
+        return lb[:nb], dp[:nb]
 
 
 def table_depth(firsts, b):

@@ -49,6 +49,7 @@ int map_err(hipError_t e) {
     } while (0)
 
 uint32_t pad_q(uint32_t q) { return (q + 63) & ~63u; }
+inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
 }  // namespace
 
@@ -120,6 +121,7 @@ struct dhtgpu_ctx {
     SortedSet sview, cache;
     uint64_t cache_version = 0;
     DevBuf cache_in, sort_scratch, cache_acc;
+    DevBuf srch;            // search_insert / table_stats staging
     // diagnostics (DHTGPU_DBG, read once at creation; phase stamps per context)
     uint32_t dbg = 0;
     hipEvent_t next_ev[8] = {};   // dhtgpu_batch_events: the next K6 call records its kernels here
@@ -181,9 +183,6 @@ int dhtgpu_ctx_create(int device, dhtgpu_ctx** out) {
     c->device = device;
     hipError_t e = c->bind();
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
-    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming);
     if (const char* d = getenv("DHTGPU_DBG")) c->dbg = (uint32_t)atoi(d);
     if (e == hipSuccess) {
         hipDeviceProp_t prop;
@@ -215,7 +214,7 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
         for (DevBuf* d : {&b.ws, &b.out_idx, &b.out_cnt}) d->release();
     c->invalidate_subs();
     for (DevBuf* b : {&c->sub_mask, &c->sub_list, &c->sub_scratch, &c->stamps, &c->w0s, &c->sview.planes, &c->sview.perm,
-                      &c->cache.planes, &c->cache.perm, &c->cache_in, &c->sort_scratch, &c->cache_acc})
+                      &c->cache.planes, &c->cache.perm, &c->cache_in, &c->sort_scratch, &c->cache_acc, &c->srch})
         b->release();
     for (hipStream_t x : c->side)
         if (x) (void)hipStreamDestroy(x);
@@ -645,6 +644,11 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
         li = b0.out_idx.as<uint32_t>();
         lc = b0.out_cnt.as<uint32_t>();
     }
+    if (!c->side[0]) {   // created on first use: streams claim hardware queues round-robin
+        for (int i = 0; i < 2; ++i) DHT_TRY(hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking));
+        DHT_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
+        for (int i = 0; i < 2; ++i) DHT_TRY(hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming));
+    }
     DHT_TRY(hipEventRecord(c->fork, s));
     for (hipStream_t x : c->side) DHT_TRY(hipStreamWaitEvent(x, c->fork, 0));
     const uint32_t q_plan = std::max<uint32_t>(1u, (uint32_t)(((uint64_t)q + S - 1) >> sb));
@@ -1052,7 +1056,6 @@ int dhtgpu_cache_sorted(dhtgpu_ctx* c, uint32_t* perm) {
 }
 
 // ---- a11 / f4: compact node wire format ------------------------------------------------
-static inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
 int dhtgpu_buffer_nodes_dev(dhtgpu_ctx* c, const uint8_t* node_tail, uint32_t af, const uint32_t* tp, uint64_t ts,
                             uint32_t q, const uint32_t* cand, uint32_t nc, uint8_t* out, uint32_t* out_len,
@@ -1197,6 +1200,94 @@ int dhtgpu_table_depth(uint32_t nb, const uint8_t* firsts20, uint32_t b, uint32_
     const int bit1 = lowbit(firsts20 + 20 * (size_t)b);
     const int bit2 = b + 1 < nb ? lowbit(firsts20 + 20 * (size_t)(b + 1)) : -1;
     *out_depth = (uint32_t)(std::max(bit1, bit2) + 1);
+    return DHTGPU_OK;
+}
+
+// ---- a10: Search::insertNode, batched ---------------------------------------------------------
+int dhtgpu_search_insert(dhtgpu_ctx* c, const uint8_t* node_ids20, const uint8_t* node_state, uint32_t nn,
+                         const uint8_t* t20, uint32_t q, uint32_t cap, uint32_t* list_node, uint8_t* list_flags,
+                         uint32_t* list_len, uint8_t* search_expired, const uint64_t* ins_off, const uint32_t* ins_node,
+                         const uint8_t* ins_token, uint8_t* ins_added) {
+    if (!c || cap == 0 || cap > 4096) return DHTGPU_EINVAL;
+    if (q && (!t20 || !list_node || !list_flags || !list_len || !search_expired || !ins_off)) return DHTGPU_EINVAL;
+    if (!q) return DHTGPU_OK;
+    const uint64_t m = ins_off[q];
+    if (m && (!ins_node || !ins_token || !ins_added)) return DHTGPU_EINVAL;
+    if (nn && (!node_ids20 || !node_state)) return DHTGPU_EINVAL;
+    for (uint32_t i = 0; i < q; ++i) {   // every index the kernel follows must name a node
+        if (ins_off[i + 1] < ins_off[i] || list_len[i] > cap) return DHTGPU_EINVAL;
+        for (uint32_t j = 0; j < list_len[i]; ++j)
+            if (list_node[(size_t)i * cap + j] >= nn) return DHTGPU_EINVAL;
+    }
+    for (uint64_t i = 0; i < m; ++i)
+        if (ins_node[i] >= nn) return DHTGPU_EINVAL;
+    DHT_TRY(c->bind());
+    const uint64_t ns = pad_q(nn ? nn : 1);
+    const size_t sz[] = {(size_t)ns * 20, (size_t)nn, (size_t)q * cap * 4, (size_t)q * cap, (size_t)q * 4, (size_t)q,
+                         ((size_t)q + 1) * 8, (size_t)m * 4, (size_t)m, (size_t)m, 16};
+    size_t tot = 0;
+    for (size_t x : sz) tot += al256(x);
+    DHT_TRY(c->srch.ensure(tot));
+    uint8_t* p[11];
+    uint8_t* w = c->srch.as<uint8_t>();
+    for (int i = 0; i < 11; ++i) {
+        p[i] = w;
+        w += al256(sz[i]);
+    }
+    if (nn) {
+        DHT_TRY(c->staging.ensure((size_t)nn * 20));
+        DHT_TRY(hipMemcpyAsync(c->staging.p, node_ids20, (size_t)nn * 20, hipMemcpyHostToDevice, c->stream));
+        DHT_TRY(launch_pack(c->staging.as<uint8_t>(), nn, reinterpret_cast<uint32_t*>(p[0]), ns, c->stream));
+        DHT_TRY(hipMemcpyAsync(p[1], node_state, nn, hipMemcpyHostToDevice, c->stream));
+        DHT_TRY(hipStreamSynchronize(c->stream));   // staging is reused for the targets
+    }
+    DHT_TRY(hipMemcpyAsync(p[2], list_node, sz[2], hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(hipMemcpyAsync(p[3], list_flags, sz[3], hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(hipMemcpyAsync(p[4], list_len, sz[4], hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(hipMemcpyAsync(p[5], search_expired, sz[5], hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(hipMemcpyAsync(p[6], ins_off, sz[6], hipMemcpyHostToDevice, c->stream));
+    if (m) {
+        DHT_TRY(hipMemcpyAsync(p[7], ins_node, sz[7], hipMemcpyHostToDevice, c->stream));
+        DHT_TRY(hipMemcpyAsync(p[8], ins_token, sz[8], hipMemcpyHostToDevice, c->stream));
+    }
+    DHT_TRY(hipMemsetAsync(p[10], 0, 4, c->stream));
+    uint64_t ts = 0;
+    DHT_TRY(c->upload_targets(t20, q, &ts));
+    DHT_TRY(launch_search_insert(reinterpret_cast<uint32_t*>(p[0]), ns, p[1], c->targets.as<uint32_t>(), ts, q, cap,
+                                 reinterpret_cast<uint32_t*>(p[2]), p[3], reinterpret_cast<uint32_t*>(p[4]), p[5],
+                                 reinterpret_cast<const uint64_t*>(p[6]), reinterpret_cast<const uint32_t*>(p[7]), p[8],
+                                 p[9], reinterpret_cast<uint32_t*>(p[10]), c->stream));
+    uint32_t overflow = 0;
+    DHT_TRY(hipMemcpyAsync(&overflow, p[10], 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(list_node, p[2], sz[2], hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(list_flags, p[3], sz[3], hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(list_len, p[4], sz[4], hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(search_expired, p[5], sz[5], hipMemcpyDeviceToHost, c->stream));
+    if (m) DHT_TRY(hipMemcpyAsync(ins_added, p[9], sz[9], hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
+    return overflow ? DHTGPU_ERANGE : DHTGPU_OK;
+}
+
+// ---- a4 / a6: InfoHash::lowbit and RoutingTable::depth of every bucket ---------------------------
+int dhtgpu_table_stats(dhtgpu_ctx* c, uint32_t nb, const uint8_t* firsts20, int32_t* out_lowbit, uint32_t* out_depth) {
+    if (!c || (nb && (!firsts20 || !out_lowbit || !out_depth))) return DHTGPU_EINVAL;
+    if (!nb) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    std::vector<uint32_t> fp((size_t)5 * nb);
+    for (uint32_t b = 0; b < nb; ++b)
+        for (int w = 0; w < 5; ++w) {
+            const uint8_t* q4 = firsts20 + 20 * (size_t)b + 4 * w;
+            fp[(size_t)w * nb + b] = ((uint32_t)q4[0] << 24) | ((uint32_t)q4[1] << 16) | ((uint32_t)q4[2] << 8) | q4[3];
+        }
+    const size_t a = al256(fp.size() * 4), bsz = al256((size_t)nb * 4);
+    DHT_TRY(c->srch.ensure(a + 2 * bsz));
+    uint8_t* base = c->srch.as<uint8_t>();
+    DHT_TRY(hipMemcpyAsync(base, fp.data(), fp.size() * 4, hipMemcpyHostToDevice, c->stream));
+    DHT_TRY(launch_table_stats(reinterpret_cast<uint32_t*>(base), nb, reinterpret_cast<int32_t*>(base + a),
+                               reinterpret_cast<uint32_t*>(base + a + bsz), c->stream));
+    DHT_TRY(hipMemcpyAsync(out_lowbit, base + a, (size_t)nb * 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipMemcpyAsync(out_depth, base + a + bsz, (size_t)nb * 4, hipMemcpyDeviceToHost, c->stream));
+    DHT_TRY(hipStreamSynchronize(c->stream));
     return DHTGPU_OK;
 }
 

@@ -136,6 +136,13 @@ size_t sort_scratch_bytes(uint64_t n);
 hipError_t launch_sort_ids(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t* out_planes, uint64_t out_stride,
                            uint32_t* perm, void* scratch, int* unique, hipStream_t s);
 
+// search.hip: batched Dht::Search::insertNode; RoutingTable::depth + InfoHash::lowbit per bucket
+hipError_t launch_search_insert(const uint32_t* planes, uint64_t stride, const uint8_t* st, const uint32_t* tp,
+                                uint64_t ts, uint32_t q, uint32_t cap, uint32_t* list_node, uint8_t* list_flags,
+                                uint32_t* list_len, uint8_t* expired, const uint64_t* ins_off, const uint32_t* ins_node,
+                                const uint8_t* ins_token, uint8_t* ins_added, uint32_t* overflow, hipStream_t s);
+hipError_t launch_table_stats(const uint32_t* fp, uint32_t nb, int32_t* out_lowbit, uint32_t* out_depth, hipStream_t s);
+
 // wire.hip: NetworkEngine::bufferNodes / deserializeNodes (compact node records)
 hipError_t launch_wire_encode(const uint32_t* planes, uint64_t stride, const uint8_t* tail, uint32_t alen,
                               const uint32_t* tp, uint64_t ts, uint32_t q, const uint32_t* cand, uint32_t c,

@@ -21,6 +21,7 @@ namespace {
 
 constexpr unsigned HASH_LEN = 20;          /* include/opendht/infohash.h:267 */
 constexpr unsigned TARGET_NODES = 8;       /* include/opendht/routing_table.h:26 */
+constexpr size_t SEARCH_NODES = 14;        /* src/dht.h:308 */
 using Id = std::array<uint8_t, HASH_LEN>;
 
 inline Id load(const uint8_t* p) { Id r; std::memcpy(r.data(), p, HASH_LEN); return r; }
@@ -333,6 +334,114 @@ void orc_cached_nodes_batch(const uint8_t* sorted_ids20, uint64_t n, const uint8
                             uint32_t q, uint32_t count, uint32_t* out_idx, uint32_t* out_cnt, int threads) {
     parallel_for(q, threads, [&](uint64_t i) {
         out_cnt[i] = orc_cached_nodes(sorted_ids20, n, accept, targets20 + 20 * i, count, out_idx + i * count);
+    });
+}
+
+/* ---- Dht::Search::insertNode, src/search.h:636-722 ------------------------------------------ */
+/* One search's node list: entry = (node, candidate, replied); SearchNode::isBad (:352-354) =
+ * node->isExpired() || candidate.  Node state comes from node_state[node]: bit0 isExpired(),
+ * bit1 isRemovable(now) (include/opendht/node.h:87-89).  `expired` is Search::expired. */
+struct OrcSearch {
+    const uint8_t* ids;          /* node ids, 20 B each */
+    const uint8_t* state;        /* per node: bit0 expired, bit1 removable */
+    const uint8_t* target;
+    std::vector<uint32_t> node;
+    std::vector<uint8_t> fl;     /* bit0 candidate, bit1 replied */
+    bool expired;
+    bool is_bad(size_t i) const { return (state[node[i]] & 1) || (fl[i] & 1); }
+    size_t bad_count() const {   /* Search::getNumberOfBadNodes */
+        size_t b = 0;
+        for (size_t i = 0; i < node.size(); i++) b += is_bad(i);
+        return b;
+    }
+    /* Search::removeExpiredNode, src/search.h:541-551: erase the last removable node */
+    void remove_expired_node() {
+        for (size_t e = node.size(); e != 0;) {
+            --e;
+            if (state[node[e]] & 2) {
+                node.erase(node.begin() + e);
+                fl.erase(fl.begin() + e);
+                return;
+            }
+        }
+    }
+    bool insert(uint32_t x, bool token) {
+        const uint8_t* nid = ids + 20ull * x;
+        bool found = false;
+        size_t n = node.size();                  /* auto n = nodes.end() */
+        while (n != 0) {
+            --n;
+            if (node[n] == x) { found = true; break; }
+            if (xor_cmp(target, nid, ids + 20ull * node[n]) > 0) { ++n; break; }   /* insert after it */
+        }
+        bool new_search_node = false;
+        if (!found) {
+            size_t t = node.size();              /* auto t = nodes.cend() */
+            size_t bad = 0;
+            bool full = false;
+            if (expired) {
+                if (node.size() >= SEARCH_NODES) { full = true; t = SEARCH_NODES; }
+            } else {
+                bad = bad_count();
+                full = node.size() - bad >= SEARCH_NODES;
+                while (t - bad > SEARCH_NODES) {
+                    --t;
+                    if (is_bad(t)) bad--;
+                }
+            }
+            if (full) {
+                if (t != node.size()) { node.resize(t); fl.resize(t); }
+                if (n >= t) return false;
+            }
+            node.insert(node.begin() + n, x);
+            fl.insert(fl.begin() + n, (uint8_t)0);
+            new_search_node = true;
+            if (state[x] & 1) {
+                if (!expired) bad++;
+            } else if (expired) {
+                bad = node.size() - 1;
+                expired = false;
+            }
+            while (node.size() - bad > SEARCH_NODES) {
+                if (!expired && is_bad(node.size() - 1)) bad--;
+                node.pop_back();
+                fl.pop_back();
+            }
+        }
+        /* the token is recorded on the inserted node; when the trimming above popped it (it
+         * was appended last) the reference's iterator would be dangling: skipped here */
+        if (token && n < node.size() && node[n] == x) {
+            fl[n] &= (uint8_t)~1u;   /* candidate = false */
+            fl[n] |= 2;              /* last_get_reply = now */
+            expired = false;
+        }
+        if (new_search_node) remove_expired_node();
+        return new_search_node;
+    }
+};
+
+/* Batched: search s applies insertions [ins_off[s], ins_off[s+1]) in order. */
+void orc_search_insert(const uint8_t* ids20, const uint8_t* node_state, const uint8_t* targets20, uint32_t q,
+                       uint32_t cap, uint32_t* list_node, uint8_t* list_flags, uint32_t* list_len,
+                       uint8_t* search_expired, const uint64_t* ins_off, const uint32_t* ins_node,
+                       const uint8_t* ins_token, uint8_t* ins_added, int threads) {
+    parallel_for(q, threads, [&](uint64_t s) {
+        OrcSearch sr;
+        sr.ids = ids20;
+        sr.state = node_state;
+        sr.target = targets20 + 20 * s;
+        sr.node.assign(list_node + s * cap, list_node + s * cap + list_len[s]);
+        sr.fl.assign(list_flags + s * cap, list_flags + s * cap + list_len[s]);
+        sr.expired = search_expired[s] != 0;
+        for (uint64_t i = ins_off[s]; i < ins_off[s + 1]; i++)
+            ins_added[i] = sr.insert(ins_node[i], ins_token[i] != 0) ? 1 : 0;
+        const size_t len = sr.node.size() < cap ? sr.node.size() : cap;
+        for (size_t i = 0; i < cap; i++) {
+            list_node[s * cap + i] = i < len ? sr.node[i] : UINT32_MAX;
+            list_flags[s * cap + i] = i < len ? sr.fl[i] : 0;
+        }
+        list_len[s] = (uint32_t)sr.node.size();
+        search_expired[s] = sr.expired ? 1 : 0;
     });
 }
 

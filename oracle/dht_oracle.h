@@ -81,6 +81,16 @@ uint32_t orc_cached_nodes(const uint8_t* sorted_ids20, uint64_t n, const uint8_t
 /* orc_cached_nodes for q targets (out_idx[q*count], out_cnt[q]) on `threads` threads. */
 void orc_cached_nodes_batch(const uint8_t* sorted_ids20, uint64_t n, const uint8_t* accept, const uint8_t* targets20,
                             uint32_t q, uint32_t count, uint32_t* out_idx, uint32_t* out_cnt, int threads);
+/* Dht::Search::insertNode (src/search.h:636-722, + removeExpiredNode :541-551) batched over q
+ * searches: search s holds list_len[s] entries list_node/list_flags[s*cap ..] (flags bit0
+ * candidate, bit1 replied) and search_expired[s]; its insertions ins_node[ins_off[s] ..
+ * ins_off[s+1]) (ins_token != 0: a reply with a token) are applied in order; ins_added =
+ * insertNode's return value.  node_state[node]: bit0 isExpired(), bit1 isRemovable(now).
+ * list_len may exceed cap (entries past cap are not stored). */
+void orc_search_insert(const uint8_t* ids20, const uint8_t* node_state, const uint8_t* targets20, uint32_t q,
+                       uint32_t cap, uint32_t* list_node, uint8_t* list_flags, uint32_t* list_len,
+                       uint8_t* search_expired, const uint64_t* ins_off, const uint32_t* ins_node,
+                       const uint8_t* ins_token, uint8_t* ins_added, int threads);
 /* NetworkEngine::bufferNodes (src/network_engine.cpp:1003-1032): sort candidates by xorCmp
  * to the target, keep 8, pack 26 (IPv4, alen 4) / 38 (IPv6, alen 16) byte records.
  * tail[i] = node i's address || port bytes.  Returns the blob length. */

@@ -54,6 +54,8 @@ def lib():
         L.orc_find_closest.argtypes = [ctypes.c_uint32, u8p, u32p, u8p, u8p, u8p, ctypes.c_uint32, u32p]
         L.orc_find_closest.restype = ctypes.c_uint32
         L.orc_classify.argtypes = [ctypes.c_uint32, u8p, u8p, u8p, ctypes.c_uint64, u8p, u64p]
+        L.orc_search_insert.argtypes = [u8p, u8p, u8p, ctypes.c_uint32, ctypes.c_uint32, u32p, u8p, u32p, u8p, u64p,
+                                        u32p, u8p, u8p, ctypes.c_int]
         L.orc_find_closest_batch.argtypes = [ctypes.c_uint32, u8p, u32p, u8p, u8p, u8p, ctypes.c_uint32,
                                              ctypes.c_uint32, u32p, u32p, ctypes.c_int]
         L.orc_cached_nodes_batch.argtypes = [u8p, ctypes.c_uint64, u8p, u8p, ctypes.c_uint32, ctypes.c_uint32,
@@ -189,6 +191,25 @@ def cached_nodes_batch(sorted_ids, accept, targets, count, threads=1):
     lib().orc_cached_nodes_batch(_p(sorted_ids, u8p), sorted_ids.shape[0], _p(accept, u8p), _p(targets, u8p), q,
                                  count, _p(out, u32p), _p(cnt, u32p), threads)
     return out, cnt
+
+
+def search_insert(node_ids, node_state, targets, lists, flags, lens, expired, ins_off, ins_node, ins_token):
+    """Search::insertNode restatement, batched (same contract as libdhtgpu's search_insert)."""
+    node_ids = np.ascontiguousarray(node_ids, dtype=np.uint8)
+    st = np.ascontiguousarray(node_state, dtype=np.uint8)
+    targets = np.ascontiguousarray(targets, dtype=np.uint8)
+    lists = np.ascontiguousarray(lists, dtype=np.uint32).copy()
+    flags = np.ascontiguousarray(flags, dtype=np.uint8).copy()
+    lens = np.ascontiguousarray(lens, dtype=np.uint32).copy()
+    expired = np.ascontiguousarray(expired, dtype=np.uint8).copy()
+    off = np.ascontiguousarray(ins_off, dtype=np.uint64)
+    node = np.ascontiguousarray(ins_node, dtype=np.uint32)
+    tok = np.ascontiguousarray(ins_token, dtype=np.uint8)
+    added = np.zeros(max(node.size, 1), np.uint8)
+    lib().orc_search_insert(_p(node_ids, u8p), _p(st, u8p), _p(targets, u8p), targets.shape[0], lists.shape[1],
+                            _p(lists, u32p), _p(flags, u8p), _p(lens, u32p), _p(expired, u8p), _p(off, u64p),
+                            _p(node, u32p), _p(tok, u8p), _p(added, u8p), 4)
+    return lists, flags, lens, expired, added[: node.size]
 
 
 def classify(firsts, myid, ids):

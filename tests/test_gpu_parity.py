@@ -564,3 +564,69 @@ def test_crawl_gpu_vs_oracle(ctx):
     o = crawl.crawl(lambda t, s, r: O.search_batch(ids, dead, 31, t, s, r), lambda ix: ids[ix], 4321)
     assert g["steps"] == o["steps"] and g["queries"] == o["queries"] and g["rounds"] == o["rounds"]
     assert np.array_equal(g["found"], o["found"])
+
+
+def _search_case(seed, nn, q, cap, maxins, pre_len=0):
+    rng = np.random.default_rng(seed)
+    ids = O.gen_ids(seed, nn)
+    ids[: nn // 8, :4] = ids[0, :4]                     # a cluster: long common prefixes
+    state = rng.choice([0, 0, 0, 0, 1, 2, 3], size=nn).astype(np.uint8)
+    tg = O.gen_ids(seed + 1, q)
+    tg[: q // 4, :4] = ids[0, :4]
+    lists = np.full((q, cap), 0xFFFFFFFF, np.uint32)
+    flags = np.zeros((q, cap), np.uint8)
+    lens = np.zeros(q, np.uint32)
+    expired = (rng.random(q) < 0.2).astype(np.uint8)
+    if pre_len:   # searches that already hold lists (built by the oracle itself)
+        off0 = (np.arange(q + 1, dtype=np.uint64) * pre_len)
+        n0 = rng.integers(0, nn, size=q * pre_len).astype(np.uint32)
+        t0 = (rng.random(n0.size) < 0.5).astype(np.uint8)
+        lists, flags, lens, expired, _ = O.search_insert(ids, state, tg, lists, flags, lens, expired, off0, n0, t0)
+    counts = rng.integers(0, maxins, size=q)
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    node = rng.integers(0, nn, size=int(off[-1])).astype(np.uint32)
+    node[::7] = node[::7] % 64                          # repeats of the same nodes
+    tok = (rng.random(node.size) < 0.3).astype(np.uint8)
+    return ids, state, tg, lists, flags, lens, expired, off, node, tok
+
+
+@pytest.mark.parametrize("seed,nn,q,maxins,pre", [(31, 500, 3000, 40, 0), (32, 20000, 10000, 60, 20),
+                                                  (33, 64, 700, 200, 5)])
+def test_search_insert_matches_oracle(ctx, seed, nn, q, maxins, pre):
+    """a10: batched Search::insertNode (search.h:636-722 + removeExpiredNode :541-551) over
+    random insertion sequences -- expired and removable nodes, candidates, token replies,
+    expired searches, repeated nodes, clustered ids -- equals the oracle list for list."""
+    case = _search_case(seed, nn, q, 64, maxins, pre)
+    got = ctx.search_insert(*case)
+    want = O.search_insert(*case)
+    for g, w, nm in zip(got, want, ["lists", "flags", "lens", "expired", "added"]):
+        bad = np.nonzero((g != w).reshape(g.shape[0], -1).any(axis=1))[0] if g.ndim > 1 else np.nonzero(g != w)[0]
+        assert bad.size == 0, f"{nm}: {bad.size} rows differ, first {bad[:5]}"
+
+
+def test_search_insert_overflow_and_bounds(ctx):
+    """A row too small for the list is reported (ERANGE), and node indices outside the node
+    table are refused before any launch (EINVAL)."""
+    import opendht_amd
+    ids, state, tg, lists, flags, lens, expired, off, node, tok = _search_case(40, 300, 50, 4, 40)
+    state[:] = 1                                        # every node bad: lists grow past 14
+    with pytest.raises(opendht_amd.DhtGpuError) as e:
+        ctx.search_insert(ids, state, tg, lists, flags, lens, expired, off, node, tok)
+    assert e.value.code == opendht_amd.ERANGE
+    node2 = node.copy()
+    node2[0] = 300
+    with pytest.raises(opendht_amd.DhtGpuError) as e:
+        ctx.search_insert(ids, np.zeros(300, np.uint8), tg, np.full((50, 64), 0xFFFFFFFF, np.uint32),
+                          np.zeros((50, 64), np.uint8), lens * 0, expired, off, node2, tok)
+    assert e.value.code == opendht_amd.EINVAL
+
+
+def test_table_stats_lowbit_depth(ctx):
+    """a4/a6: InfoHash::lowbit of every bucket's first id and RoutingTable::depth of every
+    bucket computed on the device equal the oracle on grown tables (and on a one-bucket table)."""
+    for seed, n in [(71, 50_000), (72, 3), (73, 400_000)]:
+        myid = O.gen_ids(seed, 1)[0]
+        firsts, _, _ = O.Table(myid).grow(O.gen_ids(seed + 1, n)).export()
+        lb, dp = ctx.table_stats(firsts)
+        assert list(lb) == [O.lowbit(f) for f in firsts]
+        assert list(dp) == [O.depth(firsts, b) for b in range(firsts.shape[0])]

@@ -289,3 +289,89 @@ def test_search_model_converges_to_exact_topk():
     exact = sum(list(idx[i, :8]) == list(want[i]) for i in range(200))
     assert exact >= 190, exact
     assert np.all(ln >= 8) and np.all(rd <= 64)
+
+
+def py_insert_node(ids, state, target, lst, fl, expired, x, token):
+    """Search::insertNode (src/search.h:636-722) restated in Python on big integers, independent
+    of the C oracle: lst/fl are Python lists (modified), returns (added, expired)."""
+    dist = lambda i: int.from_bytes(bytes(ids[i]), "big") ^ int.from_bytes(bytes(target), "big")
+    bad = lambda j: bool(state[lst[j]] & 1) or bool(fl[j] & 1)
+    n = len(lst)
+    found = False
+    while n:
+        n -= 1
+        if lst[n] == x:
+            found = True
+            break
+        if dist(x) > dist(lst[n]):
+            n += 1
+            break
+    added = False
+    if not found:
+        t, nb, full = len(lst), 0, False
+        if expired:
+            if len(lst) >= 14:
+                full, t = True, 14
+        else:
+            nb = sum(bad(j) for j in range(len(lst)))
+            full = len(lst) - nb >= 14
+            while t - nb > 14:
+                t -= 1
+                nb -= bad(t)
+        if full:
+            del lst[t:]
+            del fl[t:]
+            if n >= t:
+                return False, expired
+        lst.insert(n, x)
+        fl.insert(n, 0)
+        added = True
+        if state[x] & 1:
+            if not expired:
+                nb += 1
+        elif expired:
+            nb, expired = len(lst) - 1, False
+        while len(lst) - nb > 14:
+            if not expired and bad(len(lst) - 1):
+                nb -= 1
+            lst.pop()
+            fl.pop()
+    if token and n < len(lst) and lst[n] == x:
+        fl[n] = (fl[n] & ~1) | 2
+        expired = False
+    if added:
+        for e in range(len(lst) - 1, -1, -1):
+            if state[lst[e]] & 2:
+                del lst[e]
+                del fl[e]
+                break
+    return added, expired
+
+
+def test_search_insert_oracle_vs_python():
+    """The C restatement of Search::insertNode equals an independent Python restatement over
+    random insertion sequences (expired / removable nodes, candidates, tokens, expired searches)."""
+    rng = np.random.default_rng(11)
+    nn, q, cap = 400, 60, 64
+    ids = O.gen_ids(9, nn)
+    ids[:40, :4] = ids[0, :4]
+    state = rng.choice([0, 0, 0, 1, 3], size=nn).astype(np.uint8)
+    tg = O.gen_ids(10, q)
+    lists = np.full((q, cap), 0xFFFFFFFF, np.uint32)
+    flags = np.zeros((q, cap), np.uint8)
+    lens = np.zeros(q, np.uint32)
+    expired = (rng.random(q) < 0.2).astype(np.uint8)
+    counts = rng.integers(0, 40, size=q)
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    node = rng.integers(0, nn, size=int(off[-1])).astype(np.uint32)
+    tok = (rng.random(node.size) < 0.3).astype(np.uint8)
+    got = O.search_insert(ids, state, tg, lists, flags, lens, expired, off, node, tok)
+    for s in range(q):
+        lst, fl, ex = [], [], bool(expired[s])
+        adds = []
+        for i in range(int(off[s]), int(off[s + 1])):
+            a, ex = py_insert_node(ids, state, tg[s], lst, fl, ex, int(node[i]), bool(tok[i]))
+            adds.append(int(a))
+        assert got[2][s] == len(lst), s
+        assert list(got[0][s, : len(lst)]) == lst and list(got[1][s, : len(lst)]) == fl, s
+        assert bool(got[3][s]) == ex and list(got[4][int(off[s]):int(off[s + 1])]) == adds, s
