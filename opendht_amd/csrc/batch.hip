@@ -60,6 +60,12 @@ constexpr uint32_t kTieSlots = 8;                    // deferred-tie slots per F
 // at the memory side, one request per lane (random partitions), and counters packed into one
 // 4 KB run would all queue on the same channel.  F2's pcount stays packed: its flush reserves
 // consecutive partitions from consecutive lanes, which coalesce into one request per line.
+// F2's survivor buckets come in kSets sets, one per XCD (block b uses set b % 8: blocks b and
+// b + 8 share an XCD): a counter then takes 32 blocks' reservations instead of 256 (one
+// address completes about 88 returning atomics per µs), and a bucket's partial-line runs are
+// all written through one XCD's L2, which merges them into whole lines.  F3 gathers a
+// partition from its kSets contiguous buckets.
+constexpr uint32_t kSets = 8;
 constexpr uint32_t kCtrStride = 64;
 constexpr uint32_t kLdsMax = 160 * 1024;
 
@@ -195,8 +201,8 @@ struct F2Args {
     const uint32_t* w0; uint64_t n; uint64_t per_blk;
     uint32_t Lm, b1;
     const uint32_t* bitmap; uint32_t nwords;
-    uint32_t* pcount;             // [np] survivors per partition (all-zero between calls)
-    uint2* pbuf;                  // [np][pcap] survivors, partition-major
+    uint32_t* pcount;             // [kSets][np] survivors per set and partition (all-zero between calls)
+    uint2* pbuf;                  // [np][kSets][pcap] survivors, partition- and set-major
     uint32_t pcap;
     uint32_t* ctr;                // shared counters (F2 writes none; the survivor total is sum(pcount))
     uint32_t stage;               // LDS stage capacity (entries, <= kStage)
@@ -232,11 +238,12 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
     sync_lds();
     // reserve the partitions' slots (before the scan overwrites the counts)
     uint32_t res[8];
+    const uint32_t set = blockIdx.x % kSets, set_off = set * np;   // this block's bucket set
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) {
         const uint32_t p = i * kF2Threads + threadIdx.x;
         const uint32_t c = p < np ? hist[p] : 0u;
-        res[i] = c && !(a.dbg & 8) ? atomicAdd(a.pcount + p, c) : 0u;
+        res[i] = c && !(a.dbg & 8) ? atomicAdd(a.pcount + set_off + p, c) : 0u;
     }
     F2_STAMP(3);
     scan_lds<kF2Threads>(hist, np, wsum);   // hist = partition starts inside the stage
@@ -267,7 +274,7 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
             const uint2 x = stage[j];
             const uint32_t p = top_bits(x.x, a.b1);
             const uint32_t pos = hist[p] + j;
-            if (pos < a.pcap) a.pbuf[(uint64_t)p * a.pcap + pos] = x;
+            if (pos < a.pcap) a.pbuf[(uint64_t)(p * kSets + set) * a.pcap + pos] = x;
         }
     }
     sync_lds();
@@ -333,6 +340,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     }
     // ring of kRing sub-steps (one 16-B load per lane each) in flight: 128 KB per CU.
     // Loads past the block's range are clamped to its last 16 B (cache hits, masked).
+    // (the ring's first loads take most of this phase's ~4 µs: all CUs start their streams at
+    // once; the 64 KB bitmap copy alone is ~1 µs)
     const uint32_t lim = min(a.lim, ((hi + 3u) & ~3u) - 4u);
     uint4 ring[kRing];
 #pragma unroll
@@ -437,7 +446,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
             while (m) {
                 const uint32_t b = (uint32_t)__ffs(m) - 1;
                 m &= m - 1;
-                atomicAdd(a.pcount + 32 * i + b, a.pcap + 1u);
+                atomicAdd(a.pcount + (blockIdx.x % kSets) * np + 32 * i + b, a.pcap + 1u);
             }
         }
     }
@@ -636,10 +645,26 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     for (uint32_t i = p + np * threadIdx.x; i < a.nwords; i += np * kF3Threads) a.bitmap[i] = 0;
     for (uint32_t i = threadIdx.x; i <= nsub; i += kF3Threads) sofs[i] = 0;
     if (threadIdx.x == 0) ntie[0] = ntie[1] = 0;
-    const uint32_t m = a.pcount[p];           // survivors of this partition (F2)
+    // survivors of this partition in each of the kSets bucket sets (F2), its targets (F1), and
+    // -- speculatively, in the same round trip -- the first kSpec slots of every set (entry
+    // u * kF3Threads + tid = slot (u & 1) * kF3Threads + tid of set u >> 1) and the first
+    // chunk of targets; slots past a set's count are dropped below
+    constexpr uint32_t kSpec = kF3Cap / kSets;
+    static_assert(kSpec == 2 * kF3Threads && kF3Per == 2 * kSets, "speculative gather layout");
+    uint32_t ms[kSets];
+#pragma unroll
+    for (uint32_t x = 0; x < kSets; ++x) ms[x] = a.pcount[x * np + p];
     const uint32_t mt0 = a.tcount[p * kCtrStride];   // targets of this partition (F1)
-    const uint32_t mt = mt0 < a.tcap ? mt0 : a.tcap;
     const uint2* tsrc = a.tbuf + (uint64_t)p * a.tcap;
+    const uint2 tfirst = tsrc[threadIdx.x < a.tcap ? threadIdx.x : 0u];
+    uint2 e[kF3Per];
+    const uint2* pb = a.pbuf + (uint64_t)p * kSets * a.pcap;
+#pragma unroll
+    for (uint32_t u = 0; u < kF3Per; ++u) {
+        const uint32_t pos = (u & 1) * kF3Threads + threadIdx.x;
+        e[u] = pb[(u >> 1) * a.pcap + (pos < a.pcap ? pos : 0u)];
+    }
+    const uint32_t mt = mt0 < a.tcap ? mt0 : a.tcap;
     if (p == 0) {   // spilled targets (foreign, or a full bucket) join the fallback list
         const uint32_t nsp = a.ctr[kSpill];
         if (nsp) {   // one reservation for the block
@@ -649,9 +674,21 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         }
     }
     sync_lds();   // every thread has read the counts
-    if (threadIdx.x == 0) {   // all-zero again for the next call
+    // set offsets inside the partition (soff[x] = entries of sets < x); over = a set overflowed;
+    // spec = every set fits its speculative slots
+    uint32_t soff[kSets + 1];
+    bool over = false, spec = true;
+    soff[0] = 0;
+#pragma unroll
+    for (uint32_t x = 0; x < kSets; ++x) {
+        over = over || ms[x] > a.pcap;
+        spec = spec && ms[x] <= kSpec;
+        soff[x + 1] = soff[x] + (ms[x] < a.pcap ? ms[x] : a.pcap);
+    }
+    const uint32_t m = soff[kSets];
+    if (threadIdx.x < kSets) a.pcount[threadIdx.x * np + p] = 0;   // all-zero again for the next call
+    if (threadIdx.x == 0) {
         a.pstat[p] = m;
-        a.pcount[p] = 0;
         a.tcount[p * kCtrStride] = 0;
         if (p == 0) a.ctr[kSpill] = 0;
     }
@@ -660,35 +697,42 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     constexpr uint32_t NWV = kF3Threads / 64;
     if (Diag && (a.dbg & 32)) return;
-    if (m > kF3Cap || m > a.pcap) {
+    if (m > kF3Cap || over) {
         // strongly clustered ids: this partition's targets take the exact brute-force path
         if (threadIdx.x == 0) ntie[2] = atomicAdd(a.ctr, mt);   // one reservation for the block
         sync_lds();
         for (uint32_t j = threadIdx.x; j < mt; j += kF3Threads) a.fb_list[ntie[2] + j] = tsrc[j].y;
         return;
     }
-    // first chunk of targets and the partition's survivors: both loads in flight together
-    const uint2 tfirst = tsrc[threadIdx.x < mt ? threadIdx.x : 0];
     const uint32_t smask = nsub - 1u;
-    const uint2* src = a.pbuf + (uint64_t)p * a.pcap;
-    uint2 e[kF3Per];
     uint32_t rk[kF3Per];
-    const uint32_t nper = (m + kF3Threads - 1) / kF3Threads;   // rounds actually needed (uniform)
     const uint32_t sq_sh = 32 - a.Lq;                            // sub-prefix = bfe(w, 32 - Lq, Lq - b1)
-    // unconditional loads (a load under a branch gets its own wait): rounds past nper
-    // re-read entry 0 from the cache
+    // valid[u]: slot u holds one of the partition's entries
+    uint32_t valid = 0;
+    if (spec) {
 #pragma unroll
-    for (uint32_t u = 0; u < kF3Per; ++u) {
-        const uint32_t j = u * kF3Threads + threadIdx.x;
-        e[u] = src[j < m ? j : 0];
+        for (uint32_t u = 0; u < kF3Per; ++u)
+            valid |= (uint32_t)((u & 1) * kF3Threads + threadIdx.x < ms[u >> 1]) << u;
+    } else {
+        // a set past its speculative slots (not on uniform ids): gather the partition
+        // exactly, entry j from set x (soff[x] <= j < soff[x + 1]) at slot j - soff[x]
+#pragma unroll
+        for (uint32_t u = 0; u < kF3Per; ++u) {
+            const uint32_t j = u * kF3Threads + threadIdx.x;
+            uint32_t x = 0, base = 0;
+#pragma unroll
+            for (uint32_t y = 1; y < kSets; ++y)
+                if (j >= soff[y]) { x = y; base = soff[y]; }
+            e[u] = pb[x * a.pcap + (j < m ? j - base : 0u)];
+            valid |= (uint32_t)(j < m) << u;
+        }
     }
     // counting sort by sub-prefix: LDS histogram (ranks from the atomics), scan, placement
     // rk[u] = NONE marks an empty slot (the scatter tests the value: no exec masks kept live)
 #pragma unroll
     for (uint32_t u = 0; u < kF3Per; ++u) {
         rk[u] = DHT_NONE;
-        if (u < nper && u * kF3Threads + threadIdx.x < m)
-            rk[u] = atomicAdd(sofs + __builtin_amdgcn_ubfe(e[u].x, sq_sh, a.Lq - a.b1), 1u);
+        if ((valid >> u) & 1u) rk[u] = atomicAdd(sofs + __builtin_amdgcn_ubfe(e[u].x, sq_sh, a.Lq - a.b1), 1u);
     }
     sync_lds();
     F3_STAMP(2);
@@ -1037,6 +1081,7 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
 
 struct BatchPlan {
     uint32_t Lm, b1, Lq, nwords, nblk1, nblk2, stage, sparse, tcap;
+    uint32_t scap;   // survivors per (bucket set, partition)
     bool fits;   // partitions' survivors fit the F3 stage on uniform ids
     uint64_t per_blk;
 };
@@ -1090,6 +1135,13 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
         if (b1 >= 13 || b1 >= P.Lm) break;
     }
     P.b1 = b1;
+    {   // a set holds each id with probability 1 / kSets (ids are spread over the blocks by
+        // index, independently of their prefix): mean + 8 sigma + 64 of one set's share
+        const double sub = (double)(1ull << (P.Lm - b1)), mu = (double)n / (double)(1ull << P.Lm) / kSets;
+        const double mean = sub * f * mu, var = sub * f * (1.0 - f) * mu * mu + sub * f * mu;
+        const double cap = mean + 8.0 * std::sqrt(var) + 64.0;
+        P.scap = cap >= (double)kF3Cap ? kF3Cap : ((uint32_t)cap + 63u) & ~63u;
+    }
     // F3 sorts by up to 1 bit below the mark level (finer candidate ranges), <= 4096 bins
     P.Lq = P.Lm + 1 < 32 ? P.Lm + 1 : 32;
     while (P.Lq > P.Lm && P.Lq - P.b1 > 12) --P.Lq;
@@ -1249,10 +1301,10 @@ void set_lds_attributes() {
     for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
 }
 
-// workspace: bitmap (64 KB) | ctr[64] | pcount[kMaxParts] | tcount[kMaxParts * kCtrStride] |
+// workspace: bitmap (64 KB) | ctr[64] | pcount[kSets * kMaxParts] | tcount[kMaxParts * kCtrStride] |
 // tie_hdr[kMaxParts * kTieSlots] | fb done[kFbBlocks] | tie_cnt[kMaxParts] -- all-zero between calls -- |
 // fb_list[q] |
-// tspill[q] | pstat[np] | tbuf[np * tcap] | tie_cand[np * kTieSlots * 64] | pbuf[np * kF3Cap] |
+// tspill[q] | pstat[np] | tbuf[np * tcap] | tie_cand[np * kTieSlots * 64] | pbuf[np * kSets * scap] |
 // fb rec[kFbBlocks * kFbGroup * k * 6]
 constexpr uint32_t kMaxParts = 1u << 13;
 inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
@@ -1269,7 +1321,7 @@ bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
 }
 
 size_t batch_clean_bytes() {
-    return 65536 + 256 + (size_t)kMaxParts * 4 + (size_t)kMaxParts * kCtrStride * 4 + (size_t)kMaxParts * kTieSlots * 16 +
+    return 65536 + 256 + (size_t)kSets * kMaxParts * 4 + (size_t)kMaxParts * kCtrStride * 4 + (size_t)kMaxParts * kTieSlots * 16 +
            al256((size_t)kFbBlocks * 4) + (size_t)kMaxParts * 4;
 }
 
@@ -1277,7 +1329,7 @@ size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_
     const BatchPlan P = plan_batch(n, q_plan, k, num_cus);
     const size_t np = 1ull << P.b1;
     return batch_clean_bytes() + 2 * al256((size_t)q * 4) + al256(np * 4) + al256(np * P.tcap * 8) +
-           al256(np * kTieSlots * 64 * 8) + al256(np * kF3Cap * 8) + al256((size_t)kFbBlocks * kFbGroup * k * 24);
+           al256(np * kTieSlots * 64 * 8) + al256(kSets * np * P.scap * 8) + al256((size_t)kFbBlocks * kFbGroup * k * 24);
 }
 
 hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus,
@@ -1328,7 +1380,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     };
     uint32_t* bitmap = reinterpret_cast<uint32_t*>(take(65536));
     uint32_t* ctr = reinterpret_cast<uint32_t*>(take(256));
-    uint32_t* pcount = reinterpret_cast<uint32_t*>(take((size_t)kMaxParts * 4));
+    uint32_t* pcount = reinterpret_cast<uint32_t*>(take((size_t)kSets * kMaxParts * 4));
     uint32_t* tcount = reinterpret_cast<uint32_t*>(take((size_t)kMaxParts * kCtrStride * 4));
     uint4* tie_hdr = reinterpret_cast<uint4*>(take((size_t)kMaxParts * kTieSlots * 16));
     uint32_t* fb_done = reinterpret_cast<uint32_t*>(take((size_t)kFbBlocks * 4));
@@ -1338,7 +1390,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     uint32_t* pstat = reinterpret_cast<uint32_t*>(take((size_t)np * 4));
     uint2* tbuf = reinterpret_cast<uint2*>(take((size_t)np * P.tcap * 8));
     uint2* tie_cand = reinterpret_cast<uint2*>(take((size_t)np * kTieSlots * 64 * 8));
-    uint2* pbuf = reinterpret_cast<uint2*>(take((size_t)np * kF3Cap * 8));
+    uint2* pbuf = reinterpret_cast<uint2*>(take((size_t)kSets * np * P.scap * 8));
     uint32_t* fb_rec = reinterpret_cast<uint32_t*>(take((size_t)kFbBlocks * kFbGroup * k * 24));
     // ev (diagnostics): 8 events, a start/stop pair per kernel recorded by the kernel's own
     // dispatch (hipExtLaunchKernel), so the pairs time the kernels themselves
@@ -1356,7 +1408,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     if (n) {
         // F2 streams word 0, or the shifted word-0 plane of a prefix shard (stride words)
         const uint64_t lim = (c.w0s ? stride : 5 * stride) - 4;
-        F2Args a2{c.w0s ? c.w0s : planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, kF3Cap, ctr, P.stage, dbg,
+        F2Args a2{c.w0s ? c.w0s : planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, P.scap, ctr, P.stage, dbg,
                   (uint32_t)(lim < 0xFFFFFFF0ull ? lim : 0xFFFFFFF0ull), P.sparse,
                   stamps ? stamps + 8192 * 16 : nullptr};
         const dim3 g2(P.nblk2), b2(kF2Threads);
@@ -1374,7 +1426,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         return hipGetLastError();
     }
     if (dirty && (dbg & 48u)) *dirty = true;   // F3 ablation exits leave counters behind
-    F3Args a{pbuf, pcount, kF3Cap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, planes, stride, n,
+    F3Args a{pbuf, pcount, P.scap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, planes, stride, n,
              c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, pstat, tie_hdr, tie_cand, tie_cnt, dbg,
              stamps};
     size_t l3 = f3_lds(P);
