@@ -31,7 +31,7 @@ Beside the headline (`value`) the line carries, measured in the same run:
   roofline        F2 (the dominant K6 kernel) timed by events its own dispatches record in
                   every timed step; roofline_hbm: the same kernel with the Infinity Cache
                   evicted before each call (the cfg-2 working set otherwise stays in L3)
-  small_batch     Q = 1 / 8 / 32 targets over the same ids (HBM-bound latency mode)
+  small_batch     Q = 1 / 8 / 32 / 64 targets over the same ids (HBM-bound latency mode, KS path)
   find_closest    RoutingTable::findClosestNodes drop-in on a cfg-1-shaped table
   cfg3_shard      one GPU's shard of BASELINE cfg 3 (2^27 ids, 131,072 targets; the library
                   splits it into prefix sub-partitions) -- its w0 planes (537 MB) exceed L3
@@ -543,30 +543,32 @@ def main():
 
 
 def small_batch_leg(ctx, tp, ts, n, k, stream, tstream, dev):
-    """Q = 1 / 8 / 32 targets over the same id set: latency per call and the bytes the call has
-    to stream (K6 and K1 read the w0 plane, 4 B/id; SURVEY's contract counts 20 B/id)."""
+    """Q = 1 / 8 / 32 / 64 targets over the same id set: latency per call and the bytes the call
+    has to stream (4 B/id of the w0 plane; SURVEY's contract counts 20 B/id).  The library's
+    batch entry point takes the small-batch path (KS: S1 one pass over w0, S2 one workgroup per
+    target prefix, F4 the K1 scan for short subtrees -- an empty list here) for q <= 64; K1 is
+    the plain scan beside it."""
     out = {}
-    oi = torch.empty((32, k), dtype=torch.int32, device=dev)
-    oc = torch.empty(32, dtype=torch.int32, device=dev)
-    for q in (1, 8, 32):
+    oi = torch.empty((64, k), dtype=torch.int32, device=dev)
+    oc = torch.empty(64, dtype=torch.int32, device=dev)
+    for q in (1, 8, 32, 64):
         row = {}
-        for name, fn in (("k6", ctx.batch_topk_dev), ("k1", ctx.topk_dev)):
+        for name, fn in (("batch", ctx.batch_topk_dev), ("k1", ctx.topk_dev)):
             call = lambda: fn(tp.data_ptr(), ts, q, k, oi.data_ptr(), oc.data_ptr(), None, 0, stream)
             call()
             ms = ev_time(call, 20, tstream)
             row[name] = {"latency_ms": ms, "qps": q / (ms * 1e-3),
                          "w0_GBps": 4 * n / (ms * 1e-3) / 1e9, "w0_frac": 4 * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "contract_GBps": (20 * n + 24 * q + 4 * k * q) / (ms * 1e-3) / 1e9}
-        kms = None
         ev = EvSets(1, tstream)
         ev.arm(ctx)
         ctx.batch_topk_dev(tp.data_ptr(), ts, q, k, oi.data_ptr(), oc.data_ptr(), None, 0, stream)
         kms = ev.mean_ms()
-        row["k6_kernels_ms"] = dict(zip(["k_f1_targets", "k_f2_filter", "k_f3_answer", "k_f4_fallback"], kms))
-        row["k6_f2_frac"] = 4 * n / (kms[1] * 1e-3) / 1e9 / HBM_PEAK_GBS
+        row["kernels_ms"] = {"k_s1_filter": kms[1], "k_s2_answer": kms[2], "k_f4 (fallback scan, empty)": kms[3]}
+        row["s1_frac"] = 4 * n / (kms[1] * 1e-3) / 1e9 / HBM_PEAK_GBS
         out[f"q{q}"] = row
     out["note"] = ("id set L3-resident (the cfg-2 set); w0_frac = the 4 B/id w0 stream over the whole call's "
-                   "time; k6_f2_frac = the same bytes over the F2 kernel alone")
+                   "time; s1_frac = the same bytes over the S1 kernel alone")
     return out
 
 

@@ -87,13 +87,15 @@ struct dhtgpu_ctx {
     struct BatchSlot {
         DevBuf ws;              // workspace; its zero-between-calls head (bitmap, counters) stays clean
         DevBuf out_idx, out_cnt;   // record mode: local results before the record conversion
-        bool clean = false;
+        DevBuf sws;             // small-batch path workspace (zero between calls once cleaned)
+        bool clean = false, sclean = false;
         hipEvent_t done = nullptr;
         hipStream_t last = nullptr;
     };
     static constexpr int kBatchDepth = 4;
     BatchSlot bslot[kBatchDepth];
     int bnext = 0, blast = 0;
+    bool last_small = false;   // the last K6-API call took the small-batch path
     // Prefix sub-partitions of a large id set (built on the first K6 call K6 cannot plan in
     // one piece, e.g. the 2^27-id cfg-3 shard): the ids whose next sub_bits bits (after the
     // shard's own prefix) equal i, compacted in order, with their shifted word-0 plane; each
@@ -726,6 +728,55 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     return DHTGPU_OK;
 }
 
+// Batches of at most 64 targets: one pass over word 0 + one workgroup per target prefix (KS).
+static int small_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k, uint32_t* out_idx,
+                     uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base, hipStream_t s, hipEvent_t* ev) {
+    const int si = c->bnext;
+    c->bnext = (c->bnext + 1) % dhtgpu_ctx::kBatchDepth;
+    dhtgpu_ctx::BatchSlot& b = c->bslot[si];
+    if (b.last && b.last != s) {   // the slot's previous user on another stream
+        if (!b.done) DHT_TRY(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+        DHT_TRY(hipEventRecord(b.done, b.last));
+        DHT_TRY(hipStreamWaitEvent(s, b.done, 0));
+    }
+    if (b.sws.cap < small_bytes()) b.sclean = false;
+    DHT_TRY(b.sws.ensure(small_bytes()));
+    if (!b.sclean) DHT_TRY(hipMemsetAsync(b.sws.p, 0, small_bytes(), s));
+    b.sclean = true;   // the kernels leave it zero
+    const uint32_t* gidx = c->out_map();
+    uint32_t* li = out_idx;
+    uint32_t* lc = out_cnt;
+    if (out_rec) {
+        DHT_TRY(b.out_idx.ensure((size_t)q * k * 4));
+        DHT_TRY(b.out_cnt.ensure((size_t)q * 4));
+        li = b.out_idx.as<uint32_t>();
+        lc = b.out_cnt.as<uint32_t>();
+    }
+    BatchCall bc{};
+    bc.planes = c->planes.as<uint32_t>();
+    bc.stride = c->stride;
+    bc.n = c->n;
+    bc.tp = tp;
+    bc.ts = ts;
+    bc.q = q;
+    bc.q_plan = q;
+    bc.k = k;
+    bc.skip = c->shard_pbits;
+    bc.w0s = c->shard_pbits ? c->w0s.as<uint32_t>() : nullptr;
+    bc.gidx = out_rec ? nullptr : gidx;
+    bc.base = out_rec ? 0u : idx_base;
+    bc.out_idx = li;
+    bc.out_cnt = lc;
+    bc.num_cus = c->num_cus;
+    bc.ev = ev;
+    DHT_TRY(launch_small_topk(bc, b.sws.p, s));
+    b.last = s;
+    c->last_small = true;
+    if (out_rec)
+        DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx, out_rec, s));
+    return DHTGPU_OK;
+}
+
 static bool needs_subs(const dhtgpu_ctx* c, uint32_t q, uint32_t k) {
     return c->n > (1ull << 24) && !batch_supported(c->n, q, k, c->num_cus) && q <= (1u << 22);
 }
@@ -738,6 +789,10 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
         c->has_next_ev = false;
         ev = evs;
     }
+    // DHTGPU_DBG bit 2^23: K6 for small batches too (comparison runs)
+    if (small_supported(c->n, q, k) && !(c->dbg & (1u << 23)))
+        return small_run(c, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s, ev);
+    c->last_small = false;
     if (needs_subs(c, q, k)) return batch_run_subs(c, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s, ev);
     if (!batch_supported(c->n, q, k, c->num_cus)) return DHTGPU_ERANGE;
     const int si = c->bnext;
@@ -816,7 +871,9 @@ int dhtgpu_batch_topk_timed(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint
     for (int i = 0; i < 8; ++i) (void)hipEventDestroy(ev[i]);
     if (r) return r;
     DHT_TRY(e);
-    if (stats4) {
+    if (stats4 && c->last_small) {   // the small-batch path keeps no statistics
+        for (int i = 0; i < 4; ++i) stats4[i] = 0;
+    } else if (stats4) {
         if (subs) {   // sub-partition 0's call (slot 0)
             const auto& sp = c->subs[0];
             const uint32_t qp = std::max<uint32_t>(1u, (uint32_t)(((uint64_t)q + (1u << c->sub_bits) - 1) >> c->sub_bits));

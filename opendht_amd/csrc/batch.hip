@@ -1420,7 +1420,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         (void)hipEventRecord(ev[2], s);
         (void)hipEventRecord(ev[3], s);
     }
-    if (dbg & ~(48u | 256u | 512u | 1024u | 2048u | 4096u | 8192u)) {   // experiments: F1 + F2 only
+    if (dbg & ~(48u | 256u | 512u | 1024u | 2048u | 4096u | 8192u | (1u << 23))) {   // experiments: F1 + F2 only
         for (int i = 4; ev && i < 8; ++i) (void)hipEventRecord(ev[i], s);
         if (dirty) *dirty = true;   // F3 (which resets the counters and the bitmap) did not run
         return hipGetLastError();
@@ -1458,6 +1458,238 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     return hipGetLastError();
 }
 
+
+// ---- KS: small batches (q <= kSmallQ) --------------------------------------------------------
+// K6's four kernels cost ~30 µs whatever q is; a handful of targets needs one pass over w0 and
+// little else.  S1 streams w0 once on every CU: each id's top hb = min(16, Ls) bits are tested
+// against an LDS bitmap of the targets' (at most 64 set bits of 2^16), and the rare hits are
+// matched exactly against the sorted distinct level-Ls prefixes of the targets; a match is
+// appended to that prefix's candidate bucket (one returning atomic on its counter).  S2: one
+// workgroup per distinct prefix answers the prefix's targets from its bucket -- every id of
+// sub(t, Ls), complete, so the exact top-k when it holds >= k ids (the candidates' full-key
+// order, f3_wave_answer) -- or, when the bucket is short of k ids or overflowed, hands its
+// targets to the K1 scan over all ids (K6's F4 pass, which exits at once on an empty list).
+// S2 re-zeroes the counters.  Prefix shards stream their shifted word-0 plane, as K6 does.
+namespace {
+constexpr uint32_t kSmallQ = 64;
+constexpr uint32_t kSmallCap = 512;                   // candidates per prefix bucket
+constexpr int kS1Threads = 512;
+constexpr uint32_t kS1Sub = 4 * kS1Threads;           // ids per sub-step (one uint4 per thread)
+constexpr int kS2Threads = scan::WAVES * 64;
+
+struct SmallArgs {
+    const uint32_t* w0; uint64_t n; uint64_t per_blk; uint32_t lim;
+    const uint32_t* tp; uint64_t ts; uint32_t q, shift, Ls;
+    uint32_t* cnt;      // [kSmallQ] bucket fill per distinct prefix (all-zero between calls)
+    uint2* cand;        // [kSmallQ][kSmallCap] {shifted w0, index}
+    uint32_t* tab;      // [kSmallQ + 1] the sorted distinct prefixes (S1 block 0), their number last
+    uint32_t* fb;       // [kSmallQ] targets for the K1 scan; fb_cnt[0] their number (S1 zeroes it)
+    uint32_t* fb_cnt;
+};
+
+// target qi's word 0 as the streamed plane holds it (shifted for a prefix shard)
+__device__ __forceinline__ uint32_t small_tw0(const SmallArgs& a, uint32_t qi) {
+    const uint32_t w = a.tp[qi];
+    return a.shift ? (w << a.shift) | (a.tp[a.ts + qi] >> (32 - a.shift)) : w;
+}
+
+__global__ __launch_bounds__(kS1Threads) void k_s1_filter(SmallArgs a) {
+    __shared__ uint32_t b16[2048];      // 2^16 bits: the targets' top hb prefix bits
+    __shared__ uint32_t tab[kSmallQ];   // sorted distinct level-Ls prefixes
+    __shared__ uint32_t ntab_s;
+    const uint32_t lane = lane_id();
+    const uint32_t hb = a.Ls < 16 ? a.Ls : 16u;
+    for (uint32_t i = threadIdx.x; i < 2048; i += kS1Threads) b16[i] = 0;
+    if (threadIdx.x < 64) {   // wave 0: the distinct prefixes, ranked (q <= 64: one per lane)
+        const bool v = lane < a.q;
+        const uint32_t pre = v ? top_bits(small_tw0(a, lane), a.Ls) : DHT_NONE;
+        bool first = v;
+        uint32_t rank = 0;
+        for (uint32_t o = 0; o < 64; ++o) {
+            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)pre, (int)o);
+            if (o < lane && x == pre) first = false;
+        }
+        const uint64_t fm = __ballot(first);
+        for (uint32_t o = 0; o < 64; ++o) {
+            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)pre, (int)o);
+            if (((fm >> o) & 1ull) && x < pre) ++rank;
+        }
+        if (first) tab[rank] = pre;
+        if (lane == 0) ntab_s = (uint32_t)__popcll(fm);
+        if (blockIdx.x == 0) {
+            if (first) a.tab[rank] = pre;
+            if (lane == 0) {
+                a.tab[kSmallQ] = (uint32_t)__popcll(fm);
+                a.fb_cnt[0] = 0;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t ntab = ntab_s;
+    if (threadIdx.x < ntab) {
+        const uint32_t h = tab[threadIdx.x] >> (a.Ls - hb);
+        atomicOr(b16 + (h >> 5), 1u << (h & 31));
+    }
+    __syncthreads();
+    const uint64_t lo64 = (uint64_t)blockIdx.x * a.per_blk;
+    if (lo64 >= a.n) return;
+    const uint32_t lo = (uint32_t)lo64;
+    const uint32_t hi = (uint32_t)(lo64 + a.per_blk < a.n ? lo64 + a.per_blk : a.n);
+    const uint32_t lim = min(a.lim, ((hi + 3u) & ~3u) - 4u);
+    auto load = [&](uint32_t c) {
+        uint32_t j = c + 4 * threadIdx.x;
+        j = j < lim ? j : lim;
+        return *reinterpret_cast<const uint4*>(a.w0 + j);
+    };
+    uint4 ring[kRing];
+#pragma unroll
+    for (uint32_t r = 0; r < kRing; ++r) ring[r] = load(lo + r * kS1Sub);
+    const uint32_t h_off = 32 - hb, tid4 = 4 * threadIdx.x;
+    for (uint32_t c0 = lo; c0 < hi; c0 += kRing * kS1Sub) {
+#pragma unroll
+        for (uint32_t r = 0; r < kRing; ++r) {
+            const uint32_t sb = c0 + r * kS1Sub;
+            if (sb < hi) {   // block-uniform
+                const uint32_t v4[4] = {ring[r].x, ring[r].y, ring[r].z, ring[r].w};
+                const uint32_t rem = hi - sb;
+                bool hit[4];
+#pragma unroll
+                for (uint32_t f = 0; f < 4; ++f) {
+                    const uint32_t h = __builtin_amdgcn_ubfe(v4[f], h_off, hb);
+                    hit[f] = ((b16[h >> 5] >> (h & 31)) & 1u) && tid4 + f < rem;
+                }
+                if (__ballot(hit[0] || hit[1] || hit[2] || hit[3])) {   // rare
+#pragma unroll
+                    for (uint32_t f = 0; f < 4; ++f) {
+                        if (!hit[f]) continue;
+                        const uint32_t pre = top_bits(v4[f], a.Ls);
+                        uint32_t lo_s = 0, n_s = ntab;   // the first entry >= pre
+                        while (n_s) {
+                            const uint32_t half = n_s >> 1;
+                            if (tab[lo_s + half] < pre) { lo_s += half + 1; n_s -= half + 1; }
+                            else n_s = half;
+                        }
+                        if (lo_s < ntab && tab[lo_s] == pre) {
+                            const uint32_t pos = atomicAdd(a.cnt + lo_s, 1u);
+                            if (pos < kSmallCap) a.cand[lo_s * kSmallCap + pos] = make_uint2(v4[f], sb + tid4 + f);
+                        }
+                    }
+                }
+            }
+            ring[r] = load(sb + kRing * kS1Sub);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kS2Threads) void k_s2_answer(F3Args a, SmallArgs sa) {
+    __shared__ uint2 S[kSmallCap];      // the bucket
+    __shared__ uint32_t tl[kSmallQ];
+    __shared__ uint32_t ntl_s;
+    const uint32_t s = blockIdx.x;
+    const uint32_t ntab = sa.tab[kSmallQ];
+    if (s >= ntab) return;   // block-uniform
+    const uint32_t pre_s = sa.tab[s];
+    const uint32_t c = sa.cnt[s];
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    if (threadIdx.x < 64) {   // this prefix's targets
+        const bool v = lane < sa.q && top_bits(small_tw0(sa, lane < sa.q ? lane : 0u), sa.Ls) == pre_s;
+        const uint64_t m = __ballot(v);
+        if (v) tl[__popcll(m & ((1ull << lane) - 1ull))] = lane;
+        if (lane == 0) ntl_s = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) sa.cnt[s] = 0;   // all-zero again (only this workgroup reads bucket s)
+    const uint32_t ntl = __builtin_amdgcn_readfirstlane(ntl_s);
+    const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
+    if (c >= want && c <= kSmallCap) {
+        for (uint32_t j = threadIdx.x; j < c; j += kS2Threads) S[j] = sa.cand[s * kSmallCap + j];
+        __syncthreads();
+        for (uint32_t i = wv; i < ntl; i += scan::WAVES) {
+            const uint32_t qi = __builtin_amdgcn_readfirstlane(tl[i]);
+            f3_wave_answer(a, S, 0, c, qi, __builtin_amdgcn_readfirstlane(small_tw0(sa, qi)), want, lane);
+        }
+    } else if (threadIdx.x == 0) {
+        // sub(t, Ls) short of k ids (or the bucket overflowed): the K1 scan over all ids
+        const uint32_t b = atomicAdd(sa.fb_cnt, ntl);
+        for (uint32_t i = 0; i < ntl; ++i) sa.fb[b + i] = tl[i];
+    }
+}
+
+}  // namespace
+
+bool small_supported(uint64_t n, uint32_t q, uint32_t k) {
+    return q >= 1 && q <= kSmallQ && k >= 1 && k <= DHTGPU_MAX_K_DEV && n >= 1 && n < (1ull << 31);
+}
+
+// cnt | tab | fb | fb_cnt | F4 scratch (list_scan_bytes(32): done counters first) | cand
+size_t small_bytes() {
+    return al256((size_t)kSmallQ * 4) + al256((size_t)(kSmallQ + 1) * 4) + al256((size_t)kSmallQ * 4) + 256 +
+           list_scan_bytes(DHTGPU_MAX_K_DEV) + (size_t)kSmallQ * kSmallCap * 8;
+}
+
+hipError_t launch_small_topk(const BatchCall& c, void* sws, hipStream_t s) {
+    uint8_t* w = static_cast<uint8_t*>(sws);
+    SmallArgs a{};
+    a.cnt = reinterpret_cast<uint32_t*>(w);
+    a.tab = reinterpret_cast<uint32_t*>(w + al256((size_t)kSmallQ * 4));
+    uint8_t* x = w + al256((size_t)kSmallQ * 4) + al256((size_t)(kSmallQ + 1) * 4);
+    a.fb = reinterpret_cast<uint32_t*>(x);
+    x += al256((size_t)kSmallQ * 4);
+    a.fb_cnt = reinterpret_cast<uint32_t*>(x);
+    x += 256;
+    void* fb_scratch = x;
+    x += list_scan_bytes(DHTGPU_MAX_K_DEV);
+    a.cand = reinterpret_cast<uint2*>(x);
+    const uint64_t n = c.n;
+    // level: the deepest with >= 4k ids per subtree on uniform ids (K6's rule), at most 31
+    a.Ls = 0;
+    while (a.Ls < 31 && (n >> (a.Ls + 1)) >= 4ull * c.k) ++a.Ls;
+    a.w0 = c.w0s ? c.w0s : c.planes;
+    a.n = n;
+    const uint64_t lim = (c.w0s ? c.stride : 5 * c.stride) - 4;
+    a.lim = (uint32_t)(lim < 0xFFFFFFF0ull ? lim : 0xFFFFFFF0ull);
+    a.tp = c.tp;
+    a.ts = c.ts;
+    a.q = c.q;
+    a.shift = c.w0s ? c.skip : 0u;
+    // S1: two workgroups per CU, ranges in whole sub-steps
+    const uint64_t g = (uint64_t)(c.num_cus > 0 ? c.num_cus : 256) * 2;
+    const uint64_t subs = (n + kS1Sub - 1) / kS1Sub;
+    a.per_blk = ((subs + g - 1) / g) * kS1Sub;
+    const uint32_t nblk = (uint32_t)((n + a.per_blk - 1) / a.per_blk);
+    F3Args f{};
+    f.planes = c.planes;
+    f.stride = c.stride;
+    f.n = n;
+    f.tp = c.tp;
+    f.ts = c.ts;
+    f.k = c.k;
+    f.gidx = c.gidx;
+    f.base = c.base;
+    f.out_idx = c.out_idx;
+    f.out_cnt = c.out_cnt;
+    hipEvent_t* ev = c.ev;
+    auto go = [&](int i, auto kern, dim3 gr, dim3 b, size_t l, auto... args) {
+        if (ev) hipExtLaunchKernelGGL(kern, gr, b, (uint32_t)l, s, ev[2 * i], ev[2 * i + 1], 0, args...);
+        else kern<<<gr, b, l, s>>>(args...);
+    };
+    if (ev) {   // no F1 here: an empty pair
+        (void)hipEventRecord(ev[0], s);
+        (void)hipEventRecord(ev[1], s);
+    }
+    go(1, k_s1_filter, dim3(nblk), dim3(kS1Threads), 0, a);
+    go(2, k_s2_answer, dim3(c.q), dim3(kS2Threads), 0, f, a);
+    // the K1 scan for the listed targets (K6's F4 pass; an empty list exits at once)
+    f.ctr = a.fb_cnt;
+    f.fb_list = a.fb;
+    const FbArgs fa{reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(fb_scratch) + al256((size_t)kFbBlocks * 4)),
+                    static_cast<uint32_t*>(fb_scratch), kFbBlocks, 0u};
+    const dim3 g4(kFbBlocks), b4(kF4Threads);
+    if (c.k <= 8) go(3, k_f4<8>, g4, b4, 0, f, fa);
+    else if (c.k <= 16) go(3, k_f4<16>, g4, b4, 0, f, fa);
+    else go(3, k_f4<32>, g4, b4, 0, f, fa);
+    return hipGetLastError();
+}
 
 // ---- target routing for prefix sub-partitions -------------------------------------------
 // list[*cnt++] = i for every target whose bits [sel_shift, sel_shift + sel_bits) hold a value

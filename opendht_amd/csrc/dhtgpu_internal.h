@@ -117,6 +117,12 @@ struct BatchCall {
 };
 // *dirty (nullable) = an experiment exit skipped the kernels that re-zero the workspace head
 hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty);
+// KS (batch.hip): batches of at most 64 targets -- one pass over word 0 and one workgroup per
+// distinct target prefix (K6's results).  sws: small_bytes(), zero before its first use (left
+// zero); ev (nullable) gets S1 as F2's pair and S2 as F3's, F1 / F4 pairs empty.
+bool small_supported(uint64_t n, uint32_t q, uint32_t k);
+size_t small_bytes();
+hipError_t launch_small_topk(const BatchCall& c, void* sws, hipStream_t s);
 // list[] = the targets whose bits [sel_shift, +sel_bits) (sel_bits <= 16) hold a value whose bit
 // is set in d_mask; *d_cnt = their number (zeroed first)
 hipError_t launch_select_targets(const uint32_t* tw0, uint32_t q, uint32_t sel_shift, uint32_t sel_bits,

@@ -630,3 +630,63 @@ def test_table_stats_lowbit_depth(ctx):
         lb, dp = ctx.table_stats(firsts)
         assert list(lb) == [O.lowbit(f) for f in firsts]
         assert list(dp) == [O.depth(firsts, b) for b in range(firsts.shape[0])]
+
+
+@pytest.mark.parametrize("n", [1, 7, 9, 100, 5000, 70001])
+@pytest.mark.parametrize("k", [1, 8, 14, 32])
+@pytest.mark.parametrize("q", [1, 13, 64])
+def test_small_batch_path(ctx, n, k, q):
+    """Batches of <= 64 targets take the small-batch path (one pass over word 0 + one
+    workgroup per target prefix, the K1 scan for short subtrees): bit-exact like K6."""
+    ids = O.gen_ids(3000 + n, n)
+    tg = O.gen_ids(3100 + q, q)
+    ctx.set_ids(ids)
+    want, wcnt = O.topk(ids, tg, k)
+    got, cnt = ctx.batch_topk(tg, k)
+    assert np.array_equal(cnt, wcnt)
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} targets differ, first {bad[:5]}"
+
+
+def test_small_batch_clusters_duplicates_fallback(ctx):
+    """Small batches over clustered ids (w0 ties, buckets past their capacity, subtrees short
+    of k ids: the K1 fallback), targets sharing a prefix (one bucket, several targets) and
+    duplicated ids."""
+    ids = O.gen_ids(51, 40000)
+    ids[:20000, :4] = ids[0, :4]          # 20,000 ids in one 32-bit prefix: bucket overflow
+    ids[:5000, 4:8] = ids[0, 4:8]
+    ids[20000:20003, :3] = 0              # 3 ids under a 24-bit prefix: short of k
+    ids = np.concatenate([ids, ids[30000:30050]])   # duplicates
+    tg = O.gen_ids(52, 64)
+    tg[:10, :4] = ids[0, :4]
+    tg[10:14, :8] = ids[0, :8]
+    tg[14:20, :3] = 0
+    tg[20:30] = tg[30:40]                 # repeated targets
+    tg[40:45] = ids[30000:30005]          # targets that are (duplicated) members
+    ctx.set_ids(ids)
+    for k in (8, 32):
+        want, wcnt = O.topk(ids, tg, k)
+        got, cnt = ctx.batch_topk(tg, k)
+        assert np.array_equal(cnt, wcnt) and np.array_equal(got, want), k
+
+
+@pytest.mark.parametrize("pbits,pval", [(1, 1), (3, 5)])
+def test_small_batch_prefix_shard(ctx, pbits, pval):
+    """Small batches on a prefix shard (the shifted word-0 plane), own and foreign targets,
+    global and shard-local indices."""
+    n = 120000
+    ids = O.gen_ids(91, n)
+    top = lambda a: a[:, 0].astype(np.uint32) >> (8 - pbits)
+    ctx.gen_ids_prefix(91, n, pbits, pval)
+    gl = np.nonzero(top(ids) == pval)[0].astype(np.uint32)
+    tg = O.gen_ids(95, 40)
+    tg[:30, 0] = (tg[:30, 0] & (0xFF >> pbits)) | (pval << (8 - pbits))
+    w, wc = O.topk(ids[gl], tg, 8)
+    got, cnt = ctx.batch_topk(tg, 8)
+    assert np.array_equal(cnt, wc) and np.array_equal(got, gl[w])
+    ctx.set_global_indices(False)
+    try:
+        loc, lcnt = ctx.batch_topk(tg, 8)
+    finally:
+        ctx.set_global_indices(True)
+    assert np.array_equal(lcnt, wc) and np.array_equal(loc, w)
