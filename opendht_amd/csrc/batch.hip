@@ -1473,8 +1473,8 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
 namespace {
 constexpr uint32_t kSmallQ = 64;
 constexpr uint32_t kSmallCap = 512;                   // candidates per prefix bucket
-constexpr int kS1Threads = 512;
-constexpr uint32_t kS1Sub = 4 * kS1Threads;           // ids per sub-step (one uint4 per thread)
+constexpr uint32_t kS1Queue = 512;                    // matched ids queued in LDS per block
+constexpr uint32_t kSmallFbBlocks = 32;               // K1 fallback scan workgroups
 constexpr int kS2Threads = scan::WAVES * 64;
 
 struct SmallArgs {
@@ -1493,13 +1493,30 @@ __device__ __forceinline__ uint32_t small_tw0(const SmallArgs& a, uint32_t qi) {
     return a.shift ? (w << a.shift) | (a.tp[a.ts + qi] >> (32 - a.shift)) : w;
 }
 
-__global__ __launch_bounds__(kS1Threads) void k_s1_filter(SmallArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
+    constexpr uint32_t kS1Sub = 4 * NT;
     __shared__ uint32_t b16[2048];      // 2^16 bits: the targets' top hb prefix bits
     __shared__ uint32_t tab[kSmallQ];   // sorted distinct level-Ls prefixes
-    __shared__ uint32_t ntab_s;
+    __shared__ uint4 hitq[kS1Queue];    // matched ids {w0, index, prefix slot}, appended after the stream
+    __shared__ uint32_t ntab_s, nhit;
     const uint32_t lane = lane_id();
     const uint32_t hb = a.Ls < 16 ? a.Ls : 16u;
-    for (uint32_t i = threadIdx.x; i < 2048; i += kS1Threads) b16[i] = 0;
+    const uint64_t lo64 = (uint64_t)blockIdx.x * a.per_blk;
+    const uint32_t lo = (uint32_t)(lo64 < a.n ? lo64 : a.n);
+    const uint32_t hi = (uint32_t)(lo64 + a.per_blk < a.n ? lo64 + a.per_blk : a.n);
+    const uint32_t lim = min(a.lim, ((hi + 3u) & ~3u) - 4u);
+    auto load = [&](uint32_t c) {
+        uint32_t j = c + 4 * threadIdx.x;
+        j = j < lim ? j : lim;
+        return *reinterpret_cast<const uint4*>(a.w0 + j);
+    };
+    // the id ring first: the setup below runs while its loads are in flight
+    uint4 ring[kRing];
+#pragma unroll
+    for (uint32_t r = 0; r < kRing; ++r) ring[r] = load(lo + r * kS1Sub);
+    for (uint32_t i = threadIdx.x; i < 2048; i += NT) b16[i] = 0;
+    if (threadIdx.x == 0) nhit = 0;
     if (threadIdx.x < 64) {   // wave 0: the distinct prefixes, ranked (q <= 64: one per lane)
         const bool v = lane < a.q;
         const uint32_t pre = v ? top_bits(small_tw0(a, lane), a.Ls) : DHT_NONE;
@@ -1531,19 +1548,17 @@ __global__ __launch_bounds__(kS1Threads) void k_s1_filter(SmallArgs a) {
         atomicOr(b16 + (h >> 5), 1u << (h & 31));
     }
     __syncthreads();
-    const uint64_t lo64 = (uint64_t)blockIdx.x * a.per_blk;
-    if (lo64 >= a.n) return;
-    const uint32_t lo = (uint32_t)lo64;
-    const uint32_t hi = (uint32_t)(lo64 + a.per_blk < a.n ? lo64 + a.per_blk : a.n);
-    const uint32_t lim = min(a.lim, ((hi + 3u) & ~3u) - 4u);
-    auto load = [&](uint32_t c) {
-        uint32_t j = c + 4 * threadIdx.x;
-        j = j < lim ? j : lim;
-        return *reinterpret_cast<const uint4*>(a.w0 + j);
+    // a matched id goes to the block's LDS queue (a returning global atomic inside the loop
+    // would wait for the whole ring: vmcnt is in order); past the queue, straight to its bucket
+    auto emit = [&](uint32_t w, uint32_t j, uint32_t slot) {
+        const uint32_t qi = atomicAdd(&nhit, 1u);
+        if (qi < kS1Queue) {
+            hitq[qi] = make_uint4(w, j, slot, 0u);
+        } else {
+            const uint32_t pos = atomicAdd(a.cnt + slot, 1u);
+            if (pos < kSmallCap) a.cand[slot * kSmallCap + pos] = make_uint2(w, j);
+        }
     };
-    uint4 ring[kRing];
-#pragma unroll
-    for (uint32_t r = 0; r < kRing; ++r) ring[r] = load(lo + r * kS1Sub);
     const uint32_t h_off = 32 - hb, tid4 = 4 * threadIdx.x;
     for (uint32_t c0 = lo; c0 < hi; c0 += kRing * kS1Sub) {
 #pragma unroll
@@ -1569,15 +1584,19 @@ __global__ __launch_bounds__(kS1Threads) void k_s1_filter(SmallArgs a) {
                             if (tab[lo_s + half] < pre) { lo_s += half + 1; n_s -= half + 1; }
                             else n_s = half;
                         }
-                        if (lo_s < ntab && tab[lo_s] == pre) {
-                            const uint32_t pos = atomicAdd(a.cnt + lo_s, 1u);
-                            if (pos < kSmallCap) a.cand[lo_s * kSmallCap + pos] = make_uint2(v4[f], sb + tid4 + f);
-                        }
+                        if (lo_s < ntab && tab[lo_s] == pre) emit(v4[f], sb + tid4 + f, lo_s);
                     }
                 }
             }
             ring[r] = load(sb + kRing * kS1Sub);
         }
+    }
+    __syncthreads();
+    const uint32_t nq = nhit < kS1Queue ? nhit : kS1Queue;
+    for (uint32_t i = threadIdx.x; i < nq; i += NT) {
+        const uint4 e = hitq[i];
+        const uint32_t pos = atomicAdd(a.cnt + e.z, 1u);
+        if (pos < kSmallCap) a.cand[e.z * kSmallCap + pos] = make_uint2(e.x, e.y);
     }
 }
 
@@ -1586,24 +1605,28 @@ __global__ __launch_bounds__(kS2Threads) void k_s2_answer(F3Args a, SmallArgs sa
     __shared__ uint32_t tl[kSmallQ];
     __shared__ uint32_t ntl_s;
     const uint32_t s = blockIdx.x;
-    const uint32_t ntab = sa.tab[kSmallQ];
-    if (s >= ntab) return;   // block-uniform
-    const uint32_t pre_s = sa.tab[s];
-    const uint32_t c = sa.cnt[s];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    // one round trip: the table, the bucket's count, the targets' words and (speculatively)
+    // the bucket's first kS2Threads slots
+    const uint32_t ntab = sa.tab[kSmallQ];
+    const uint32_t pre_s = sa.tab[s < kSmallQ ? s : 0u];
+    const uint32_t c = sa.cnt[s < kSmallQ ? s : 0u];
+    const uint32_t tw = threadIdx.x < 64 && lane < sa.q ? small_tw0(sa, lane) : 0u;
+    static_assert(kSmallCap == kS2Threads, "one speculative bucket slot per thread");
+    const uint2 e = sa.cand[(s < kSmallQ ? s : 0u) * kSmallCap + threadIdx.x];
+    if (s >= ntab) return;   // block-uniform
     if (threadIdx.x < 64) {   // this prefix's targets
-        const bool v = lane < sa.q && top_bits(small_tw0(sa, lane < sa.q ? lane : 0u), sa.Ls) == pre_s;
+        const bool v = lane < sa.q && top_bits(tw, sa.Ls) == pre_s;
         const uint64_t m = __ballot(v);
         if (v) tl[__popcll(m & ((1ull << lane) - 1ull))] = lane;
         if (lane == 0) ntl_s = (uint32_t)__popcll(m);
     }
+    if (threadIdx.x < c) S[threadIdx.x] = e;
     __syncthreads();
     if (threadIdx.x == 0) sa.cnt[s] = 0;   // all-zero again (only this workgroup reads bucket s)
     const uint32_t ntl = __builtin_amdgcn_readfirstlane(ntl_s);
     const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
     if (c >= want && c <= kSmallCap) {
-        for (uint32_t j = threadIdx.x; j < c; j += kS2Threads) S[j] = sa.cand[s * kSmallCap + j];
-        __syncthreads();
         for (uint32_t i = wv; i < ntl; i += scan::WAVES) {
             const uint32_t qi = __builtin_amdgcn_readfirstlane(tl[i]);
             f3_wave_answer(a, S, 0, c, qi, __builtin_amdgcn_readfirstlane(small_tw0(sa, qi)), want, lane);
@@ -1652,10 +1675,14 @@ hipError_t launch_small_topk(const BatchCall& c, void* sws, hipStream_t s) {
     a.ts = c.ts;
     a.q = c.q;
     a.shift = c.w0s ? c.skip : 0u;
-    // S1: two workgroups per CU, ranges in whole sub-steps
-    const uint64_t g = (uint64_t)(c.num_cus > 0 ? c.num_cus : 256) * 2;
-    const uint64_t subs = (n + kS1Sub - 1) / kS1Sub;
-    a.per_blk = ((subs + g - 1) / g) * kS1Sub;
+    // S1: two 512-thread workgroups per CU (measured against 1 x 1024, 2 x 1024 and 4 x 256:
+    // 2 x 1024 -- twice the loads in flight -- is 35 % slower, the others equal or slower),
+    // ranges in whole sub-steps
+    constexpr uint32_t nt = 512, bpc = 2;
+    const uint64_t g = (uint64_t)(c.num_cus > 0 ? c.num_cus : 256) * bpc;
+    const uint64_t sub = 4ull * nt;
+    const uint64_t subs = (n + sub - 1) / sub;
+    a.per_blk = ((subs + g - 1) / g) * sub;
     const uint32_t nblk = (uint32_t)((n + a.per_blk - 1) / a.per_blk);
     F3Args f{};
     f.planes = c.planes;
@@ -1677,14 +1704,16 @@ hipError_t launch_small_topk(const BatchCall& c, void* sws, hipStream_t s) {
         (void)hipEventRecord(ev[0], s);
         (void)hipEventRecord(ev[1], s);
     }
-    go(1, k_s1_filter, dim3(nblk), dim3(kS1Threads), 0, a);
+    go(1, k_s1_filter<nt>, dim3(nblk), dim3(nt), 0, a);
     go(2, k_s2_answer, dim3(c.q), dim3(kS2Threads), 0, f, a);
     // the K1 scan for the listed targets (K6's F4 pass; an empty list exits at once)
     f.ctr = a.fb_cnt;
     f.fb_list = a.fb;
+    // a smaller grid than K6's: the list holds at most 64 targets (one scan group) and is
+    // empty on all but strongly clustered id sets, where the dispatch of an empty grid is the cost
     const FbArgs fa{reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(fb_scratch) + al256((size_t)kFbBlocks * 4)),
-                    static_cast<uint32_t*>(fb_scratch), kFbBlocks, 0u};
-    const dim3 g4(kFbBlocks), b4(kF4Threads);
+                    static_cast<uint32_t*>(fb_scratch), kSmallFbBlocks, 0u};
+    const dim3 g4(kSmallFbBlocks), b4(kF4Threads);
     if (c.k <= 8) go(3, k_f4<8>, g4, b4, 0, f, fa);
     else if (c.k <= 16) go(3, k_f4<16>, g4, b4, 0, f, fa);
     else go(3, k_f4<32>, g4, b4, 0, f, fa);
