@@ -50,10 +50,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# Two batches in flight (--inflight) need their streams on different hardware queues; HIP's
-# default of 4 queues per process is shared round-robin by every stream the process creates
-# (torch's, the contexts'), so ask for 8 before the runtime starts.
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("DHT_BENCH_HW_QUEUES", "8")
+# Hardware queues: HIP's default (4 per process, shared round-robin by the streams) is kept.
+# Measured: 8 queues leave the cfg-2 step unchanged (40.6-41.0 vs 40.8-40.9 us) and make the
+# sub-partitioned cfg-3 shard 1.7x slower (0.60 vs 0.35 ms per call with two calls in flight).
+# DHT_BENCH_HW_QUEUES overrides it for experiments.
+if os.environ.get("DHT_BENCH_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["DHT_BENCH_HW_QUEUES"]
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

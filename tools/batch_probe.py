@@ -17,6 +17,7 @@ ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--algo", default="batch")
 ap.add_argument("--prefix", type=int, default=0, help="prefix shard: keep ids with top PREFIX bits == 0 of 2^PREFIX x n")
 ap.add_argument("--evict", action="store_true", help="write 512 MiB before every call (Infinity Cache evicted)")
+ap.add_argument("--inflight", type=int, default=1, help="calls alternate over this many streams")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
@@ -40,11 +41,19 @@ oc = torch.empty(a.q, dtype=torch.int32, device=dev)
 ebuf = torch.zeros(128 << 20, dtype=torch.int32, device=dev) if a.evict else None
 
 
+streams = [st] + [torch.cuda.Stream(dev) for _ in range(a.inflight - 1)]
+outs = [(oi, oc)] + [(torch.empty_like(oi), torch.empty_like(oc)) for _ in range(a.inflight - 1)]
+ncall = [0]
+
+
 def call():
     if ebuf is not None:
         ebuf.sum()
+    i = ncall[0] % a.inflight
+    ncall[0] += 1
     if a.algo == "batch":
-        ctx.batch_topk_dev(tp.data_ptr(), ts, a.q, a.k, oi.data_ptr(), oc.data_ptr(), None, 0, s)
+        ctx.batch_topk_dev(tp.data_ptr(), ts, a.q, a.k, outs[i][0].data_ptr(), outs[i][1].data_ptr(), None, 0,
+                           streams[i].cuda_stream)
     else:
         ctx.index_build(s)
         ctx.index_topk_dev(tp.data_ptr(), ts, a.q, a.k, oi.data_ptr(), oc.data_ptr(), None, 0, s)

@@ -22,4 +22,7 @@ echo pmc-ok &&
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $OUT/bench20.log 2>&1 && tail -1 $OUT/bench20.log > $OUT/bench20.json &&
 timeout -k 10 400 python bench.py > $OUT/bench.log 2>&1 && tail -1 $OUT/bench.log > $OUT/bench.json &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-extra > $OUT/kt.log 2>&1 &&
+python3 tools/kt_window.py $OUT/kt 5 20 > $OUT/kt_windows.txt && python3 tools/kt_window.py $OUT/kt 25 20 >> $OUT/kt_windows.txt &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt_small -o run --output-format csv -- python3 tools/small_probe.py > $OUT/kt_small.log 2>&1 &&
+DHTGPU_DBG=256 timeout -k 10 120 python3 tools/batch_probe.py --reps 1 > $OUT/phase_stamps_cfg2.log 2>&1 &&
 echo all-ok
