@@ -767,6 +767,38 @@ def cfg3_multi_leg(a, L, dev, stream, tstream, world, rank):
         ms = float(tm.item()) * 1e3 / steps
         out["broadcast"] = {"ms_per_step": ms, "qps": q / (ms * 1e-3), "ids_per_gpu": hi - lo,
                             "allgather_bytes_per_gpu": q * k * 24, "scaling": "strong (one global batch)"}
+        # the same route with an all-to-all by target slice: each rank receives and merges only
+        # its own q / world targets' candidates (q*k*24 B in per GPU instead of world times it)
+        tlo, thi = sharding.shard_range(q, world, rank)
+        qm = thi - tlo
+        exch = torch.empty((world * qm, k, 6), dtype=torch.int32, device=dev)
+        om = torch.empty((max(qm, 1), k), dtype=torch.int32, device=dev)
+        ocm = torch.empty(max(qm, 1), dtype=torch.int32, device=dev)
+
+        def astep():
+            c.batch_topk_dev(tp_all.data_ptr(), ts, q, k, None, None, rec.data_ptr(), lo, stream)
+            sharding.exchange_records(rec, out=exch)
+            if qm:
+                assert L.dhtgpu_merge_dev(exch.data_ptr(), world, qm, k, tp_all.data_ptr() + 4 * tlo, ts, k,
+                                          om.data_ptr(), ocm.data_ptr(), stream) == 0
+        astep()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            astep()
+        torch.cuda.synchronize()
+        dist.barrier()
+        tm = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        ms = float(tm.item()) * 1e3 / steps
+        torch.cuda.synchronize()
+        agree = bool(torch.equal(om[:qm], oi[tlo:thi]) and torch.equal(ocm[:qm], oc[tlo:thi])) if qm else True
+        out["broadcast_alltoall"] = {"ms_per_step": ms, "qps": q / (ms * 1e-3), "ids_per_gpu": hi - lo,
+                                     "exchange_bytes_in_per_gpu": q * k * 24,
+                                     "equals_allgather_route": agree,
+                                     "results": "distributed by target slice (shard_range(q, world, rank))",
+                                     "scaling": "strong (one global batch)"}
     finally:
         c.close()
         torch.cuda.synchronize()

@@ -60,6 +60,32 @@ def merge_records(gathered, targets, k):
     return out, cnt
 
 
+def _worker_a2a(rank, world, port, n, q, k, ret):
+    """The all-to-all route: each rank merges only the targets it owns."""
+    import oracle as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ids = O.gen_ids(7, n)
+    tg = O.gen_ids(8, q)
+    lo, hi = sharding.shard_range(n, world, rank)
+    idx, cnt = O.topk(ids[lo:hi], tg, k, threads=2)
+    got = sharding.exchange_records(records_from(ids[lo:hi], lo, idx, cnt))
+    tlo, thi = sharding.shard_range(q, world, rank)
+    assert got.shape[:2] == (world, thi - tlo)
+    out, ocnt = merge_records(got, tg[tlo:thi], k)
+    want, wcnt = O.topk(ids, tg[tlo:thi], k, threads=2)
+    ret[rank] = bool(np.array_equal(out, want) and np.array_equal(ocnt, wcnt))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,q", [(2, 3001, 41), (3, 500, 40), (3, 20, 2)])
+def test_exchange_records_gloo(world, n, q):
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker_a2a, args=(world, _free_port(), n, q, 8, ret), nprocs=world, join=True)
+    assert all(ret[r] for r in range(world)), dict(ret)
+
+
 def _worker(rank, world, port, n, q, k, ret):
     import oracle as O
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
