@@ -600,8 +600,8 @@ def find_closest_leg(ctx, a, dev):
 
 def cfg3_shard_leg(a, L, dev, stream, tstream):
     """One GPU's shard of cfg 3: 2^27 ids (~10^9 / 8), 131,072 targets.  The library splits the
-    set once into 8 prefix sub-partitions of 2^24 (setup, not timed) and runs one K6 pass per
-    sub-partition; its 8 w0 planes (537 MB) exceed the Infinity Cache, so F2 streams HBM."""
+    set once into 8 prefix sub-partitions of 2^24 (setup, not timed) and serves all of them with
+    ONE K6 launch sequence; their w0 planes (537 MB) exceed the Infinity Cache, so F2 streams HBM."""
     n, q, k = 1 << 27, 131072, a.k
     c = opendht_amd.Context(dev.index)
     try:
@@ -619,15 +619,14 @@ def cfg3_shard_leg(a, L, dev, stream, tstream):
         steps = 20
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        # back-to-back calls on one stream (each call already spreads its 8 sub-partition passes
-        # over the library's two internal streams; a second caller stream adds nothing but
-        # contention for the process's 4 hardware queues), no events in the timed loop
+        # back-to-back calls on one stream (one call is 2 x 256 F2 workgroups over 537 MB: it
+        # fills the chip alone), no events in the timed loop
         for i in range(steps):
             c.batch_topk_dev(tp.data_ptr(), ts, q, k, outs[i % 2][0].data_ptr(), outs[i % 2][1].data_ptr(), None, 0,
                              tstream.cuda_stream)
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / steps
-        reps = 8   # kernel times: sub-partition 0's kernels, serial calls after the timed window
+        reps = 8   # kernel times: serial calls after the timed window
         ev = EvSets(reps, tstream)
         for i in range(reps):
             ev.arm(c)
@@ -637,23 +636,22 @@ def cfg3_shard_leg(a, L, dev, stream, tstream):
         kms = ev.mean_ms()
         iso, fb, surv, slow = c.batch_topk_timed(tp.data_ptr(), ts, q, k, outs[0][0].data_ptr(), outs[0][1].data_ptr(),
                                                 stream)
-        n_sub = n // 8
-        q_sub = q // 8
-        kern = k6_kernels(kms, n_sub, q_sub, k, surv)
+        kern = k6_kernels(kms, n, q, k, surv)
         f2ms, f2b = kern["k_f2_filter"]
-        res = {"workload": f"{q} targets x {n} ids (2^27), k={k}: 8 prefix sub-partitions of ~2^24",
+        res = {"workload": f"{q} targets x {n} ids (2^27), k={k}: 8 prefix sub-partitions of ~2^24, one launch",
                "ms_per_step": ms, "qps": q / (ms * 1e-3), "setup_first_call_s": first_s,
-               "sub_partition_kernels_ms": {kk: v[0] for kk, v in kern.items()},
-               "kernel_timing": "sub-partition 0's kernels, 8 serial calls after the timed window (events)",
-               "sub_partition_kernels_ms_isolated": dict(zip(["k_f1_targets", "k_f2_filter", "k_f3_answer",
-                                                              "k_f4_fallback"], list(iso))),
+               "kernels_ms": {kk: v[0] for kk, v in kern.items()},
+               "kernel_timing": "the fused launch's kernels (all 8 sub-partitions), 8 serial calls after the "
+                                "timed window (events)",
+               "kernels_ms_isolated": dict(zip(["k_f1_targets", "k_f2_filter", "k_f3_answer", "k_f4_fallback"],
+                                               list(iso))),
                "roofline_f2_isolated_frac": f2b / (iso[1] * 1e-3) / 1e9 / HBM_PEAK_GBS,
                "roofline_f2": {"bound": "hbm", "achieved": f2b / (f2ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                                "unit": "GB/s", "frac": f2b / (f2ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                "alg_bytes_per_launch": f2b, "kernel_ms": f2ms,
                                "traffic_bytes_per_launch": pmc_traffic(f"cfg3shard:{n}x{q}x{k}", "k_f2_filter"),
                                "served_from": "HBM: 8 sub-partition w0 planes = 537 MB per step > 256 MiB L3"},
-               "sub0_survivors": surv, "sub0_fallback": fb, "sub0_wave_path": slow}
+               "survivors": surv, "fallback": fb, "wave_path": slow}
         if not a.no_cpu:
             O = oracle()
             rows = np.arange(0, q, q // 16)

@@ -88,7 +88,9 @@ struct dhtgpu_ctx {
         DevBuf ws;              // workspace; its zero-between-calls head (bitmap, counters) stays clean
         DevBuf out_idx, out_cnt;   // record mode: local results before the record conversion
         DevBuf sws;             // small-batch path workspace (zero between calls once cleaned)
-        bool clean = false, sclean = false;
+        size_t zeroed = 0;      // leading workspace bytes known zero (the last call's clean head)
+        uint64_t desc_sig = 0;  // sub-partition descriptors held by the workspace (launch_batch_topk)
+        bool sclean = false;
         hipEvent_t done = nullptr;
         hipStream_t last = nullptr;
     };
@@ -96,10 +98,12 @@ struct dhtgpu_ctx {
     BatchSlot bslot[kBatchDepth];
     int bnext = 0, blast = 0;
     bool last_small = false;   // the last K6-API call took the small-batch path
+    uint64_t last_n = 0;       // ... else its plan: largest sub-partition, planned targets, sub-partitions
+    uint32_t last_qp = 0, last_nsub = 1;
     // Prefix sub-partitions of a large id set (built on the first K6 call K6 cannot plan in
     // one piece, e.g. the 2^27-id cfg-3 shard): the ids whose next sub_bits bits (after the
-    // shard's own prefix) equal i, compacted in order, with their shifted word-0 plane; each
-    // K6 call then runs one sub-call per sub-partition on the two internal streams.
+    // shard's own prefix) equal i, compacted in order, with their shifted word-0 plane; one K6
+    // launch sequence then serves all of them.
     struct SubPart {
         DevBuf planes, map, gmap, w0s;   // planes: 5 * stride u32; map: sub -> ctx-local; gmap: sub -> global
         uint64_t n = 0, stride = 0;
@@ -107,11 +111,6 @@ struct dhtgpu_ctx {
     std::vector<SubPart> subs;
     uint32_t sub_bits = 0;
     bool subs_valid = false;
-    DevBuf sub_mask, sub_list, sub_scratch;   // deficient / unplannable sub-partitions: routed to the scan
-    bool sub_scratch_clean = false;
-    hipStream_t side[2] = {nullptr, nullptr};  // internal streams for sub-calls
-
-    hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
     uint32_t shard_pval = 0;
     // lexicographically sorted views (sort.hip): of the main set when it was uploaded unsorted
     // (built on the first cached_nodes call), and the NodeCache mirror (dhtgpu_cache_set)
@@ -202,8 +201,6 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
     if (!c) return;
     (void)c->bind();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (hipStream_t x : c->side)
-        if (x) (void)hipStreamSynchronize(x);
     for (auto& b : c->bslot) {   // slots last used on other streams: let that work finish
         if (b.last && b.last != c->stream) (void)hipStreamSynchronize(b.last);
         if (b.done) (void)hipEventDestroy(b.done);
@@ -213,16 +210,11 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
                       &c->net_sorted, &c->net_dead, &c->net_io})
         b->release();
     for (auto& b : c->bslot)
-        for (DevBuf* d : {&b.ws, &b.out_idx, &b.out_cnt}) d->release();
+        for (DevBuf* d : {&b.ws, &b.out_idx, &b.out_cnt, &b.sws}) d->release();
     c->invalidate_subs();
-    for (DevBuf* b : {&c->sub_mask, &c->sub_list, &c->sub_scratch, &c->stamps, &c->w0s, &c->sview.planes, &c->sview.perm,
+    for (DevBuf* b : {&c->stamps, &c->w0s, &c->sview.planes, &c->sview.perm,
                       &c->cache.planes, &c->cache.perm, &c->cache_in, &c->sort_scratch, &c->cache_acc, &c->srch})
         b->release();
-    for (hipStream_t x : c->side)
-        if (x) (void)hipStreamDestroy(x);
-    if (c->fork) (void)hipEventDestroy(c->fork);
-    for (hipEvent_t x : c->join)
-        if (x) (void)hipEventDestroy(x);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -560,21 +552,32 @@ static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hi
         DHT_TRY(hipEventRecord(b.done, b.last));
         DHT_TRY(hipStreamWaitEvent(s, b.done, 0));
     }
-    const size_t need = batch_bytes(bc.n, bc.q, bc.q_plan, bc.k, c->num_cus);
-    if (need > b.ws.cap) b.clean = false;
+    uint64_t n_plan = bc.nsub ? 0 : bc.n;   // the plan is the largest sub-partition's
+    for (uint32_t i = 0; i < bc.nsub; ++i) n_plan = std::max<uint64_t>(n_plan, bc.subs[i].n);
+    const uint32_t nsub = bc.nsub ? bc.nsub : 1u;
+    const size_t need = batch_bytes(n_plan, bc.q, bc.q_plan, bc.k, c->num_cus, nsub);
+    const size_t head = batch_clean_bytes(n_plan, bc.q_plan, bc.k, c->num_cus, nsub);
+    if (need > b.ws.cap) {   // reallocated: nothing of it is known
+        b.zeroed = 0;
+        b.desc_sig = 0;
+    }
     DHT_TRY(b.ws.ensure(need));
-    if (!b.clean) DHT_TRY(hipMemsetAsync(b.ws.p, 0, batch_clean_bytes(), s));
-    b.clean = false;   // re-established below once every launch went through
+    if (b.zeroed < head) DHT_TRY(hipMemsetAsync(b.ws.p, 0, head, s));
+    b.zeroed = 0;   // re-established below once every launch went through
     if (bc.dbg & 256) {
         DHT_TRY(c->stamps.ensure((size_t)2 * 8192 * 16 * 8));
         bc.stamps = c->stamps.as<unsigned long long>();
     }
     bc.ws = b.ws.p;
+    bc.desc_sig = &b.desc_sig;
     bool dirty = false;
     DHT_TRY(launch_batch_topk(bc, s, &dirty));
     b.last = s;
-    b.clean = !dirty;
+    b.zeroed = dirty ? 0 : head;   // the call leaves its clean head zero
     c->blast = si;
+    c->last_n = n_plan;
+    c->last_qp = bc.q_plan;
+    c->last_nsub = nsub;
     return DHTGPU_OK;
 }
 
@@ -623,102 +626,65 @@ static int build_subs(dhtgpu_ctx* c) {
     return DHTGPU_OK;
 }
 
-// A K6 call over prefix sub-partitions.  Sub-partition i answers the targets of its prefix
-// (F1 selects them) from its own ids: when it holds >= k ids, every id of it is XOR-closer to
-// such a target than every id outside it, so its top-k is the set's.  Sub-partitions with fewer
-// than k ids (their targets need ids outside), or that K6 cannot plan, send their targets to the
-// K1 scan (over the whole set, resp. the sub-partition).  The sub-calls alternate over the two
-// internal streams, forked from and joined back into s.
+// A K6 call over prefix sub-partitions, all of them in ONE launch sequence.  A target is
+// answered from its own sub-partition (F1 routes it by the sub_bits bits after the shard
+// prefix): when that holds >= k ids, every id of it is XOR-closer to the target than every id
+// outside it, so its top-k is the set's.  Targets whose sub-partition is short of k ids (or
+// whose partition overflowed) take F4's scan over the whole set.  A split K6 cannot plan
+// (strongly clustered ids: one sub-partition far above 2^24) takes the K1 scan.
 static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k, uint32_t* out_idx,
                           uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base, hipStream_t s, hipEvent_t* ev) {
     int r = build_subs(c);
     if (r) return r;
     const uint32_t sb = c->sub_bits, S = 1u << sb;
     const uint32_t P = c->shard_pbits + sb;
+    const uint32_t q_plan = std::max<uint32_t>(1u, (uint32_t)(((uint64_t)q + S - 1) >> sb));
+    uint64_t n_max = 0;
+    for (const auto& sp : c->subs) n_max = std::max<uint64_t>(n_max, sp.n);
+    if (!batch_supported(n_max, q_plan, k, c->num_cus, S))
+        return dhtgpu_topk_dev(c, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s);
     const bool global = c->has_gidx && c->map_global && !out_rec;
+    const int si = c->bnext;
+    c->bnext = (c->bnext + 1) % dhtgpu_ctx::kBatchDepth;
+    dhtgpu_ctx::BatchSlot& b = c->bslot[si];
     // record mode: context-local indices first (then records from the context's planes)
-    dhtgpu_ctx::BatchSlot& b0 = c->bslot[0];
     uint32_t* li = out_idx;
     uint32_t* lc = out_cnt;
     if (out_rec) {
-        DHT_TRY(b0.out_idx.ensure((size_t)q * k * 4));
-        DHT_TRY(b0.out_cnt.ensure((size_t)q * 4));
-        li = b0.out_idx.as<uint32_t>();
-        lc = b0.out_cnt.as<uint32_t>();
+        DHT_TRY(b.out_idx.ensure((size_t)q * k * 4));
+        DHT_TRY(b.out_cnt.ensure((size_t)q * 4));
+        li = b.out_idx.as<uint32_t>();
+        lc = b.out_cnt.as<uint32_t>();
     }
-    if (!c->side[0]) {   // created on first use: streams claim hardware queues round-robin
-        for (int i = 0; i < 2; ++i) DHT_TRY(hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking));
-        DHT_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
-        for (int i = 0; i < 2; ++i) DHT_TRY(hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming));
-    }
-    DHT_TRY(hipEventRecord(c->fork, s));
-    for (hipStream_t x : c->side) DHT_TRY(hipStreamWaitEvent(x, c->fork, 0));
-    const uint32_t q_plan = std::max<uint32_t>(1u, (uint32_t)(((uint64_t)q + S - 1) >> sb));
-    std::vector<uint32_t> deficient, scan_subs;
+    std::vector<SubSpec> specs(S);
     for (uint32_t i = 0; i < S; ++i) {
         const dhtgpu_ctx::SubPart& sp = c->subs[i];
-        if (sp.n < k) { deficient.push_back(i); continue; }
-        if (!batch_supported(sp.n, q_plan, k, c->num_cus)) { scan_subs.push_back(i); continue; }
-        BatchCall bc{};
-        bc.planes = sp.planes.as<uint32_t>();
-        bc.stride = sp.stride;
-        bc.n = sp.n;
-        bc.tp = tp;
-        bc.ts = ts;
-        bc.q = q;
-        bc.q_plan = q_plan;
-        bc.k = k;
-        bc.sel_shift = c->shard_pbits;
-        bc.sel_bits = sb;
-        bc.sel_val = i;
-        bc.skip = P;
-        bc.w0s = sp.w0s.as<uint32_t>();
-        bc.gidx = global ? sp.gmap.as<uint32_t>() : sp.map.as<uint32_t>();
-        bc.base = 0;
-        bc.out_idx = li;
-        bc.out_cnt = lc;
-        bc.num_cus = c->num_cus;
-        bc.dbg = c->dbg;
-        bc.ev = i == 0 ? ev : nullptr;   // diagnostics time sub-partition 0's kernels
-        r = batch_slot_run(c, (int)(i % dhtgpu_ctx::kBatchDepth), bc, c->side[i & 1], nullptr);
-        if (r) return r;
+        specs[i] = SubSpec{sp.planes.as<uint32_t>(), sp.w0s.as<uint32_t>(), sp.stride, sp.n,
+                           global ? sp.gmap.as<uint32_t>() : sp.map.as<uint32_t>(), 0u};
     }
-    if (!deficient.empty() || !scan_subs.empty()) {   // rare: strongly non-uniform id sets
-        hipStream_t x = c->side[0];
-        const size_t mwords = ((size_t)S + 31) / 32;
-        DHT_TRY(c->sub_mask.ensure(mwords * 4));
-        DHT_TRY(c->sub_list.ensure((size_t)q * 4 + 256));
-        if (c->sub_scratch.cap < list_scan_bytes(k)) c->sub_scratch_clean = false;
-        DHT_TRY(c->sub_scratch.ensure(list_scan_bytes(k)));
-        if (!c->sub_scratch_clean) DHT_TRY(hipMemsetAsync(c->sub_scratch.p, 0, list_scan_bytes(k), x));
-        c->sub_scratch_clean = true;
-        uint32_t* list = c->sub_list.as<uint32_t>();
-        uint32_t* d_cnt = reinterpret_cast<uint32_t*>(c->sub_list.as<uint8_t>() + (((size_t)q * 4 + 255) & ~size_t(255)));
-        auto route = [&](const std::vector<uint32_t>& which, const uint32_t* planes, uint64_t stride, uint64_t n,
-                         const uint32_t* gidx) -> int {
-            std::vector<uint32_t> mask(mwords, 0u);
-            for (uint32_t i : which) mask[i >> 5] |= 1u << (i & 31);
-            DHT_TRY(hipMemcpyAsync(c->sub_mask.p, mask.data(), mwords * 4, hipMemcpyHostToDevice, x));
-            DHT_TRY(launch_select_targets(tp, q, c->shard_pbits, sb, c->sub_mask.as<uint32_t>(), list, d_cnt, x));
-            DHT_TRY(launch_list_scan(planes, stride, n, tp, ts, k, list, d_cnt, gidx, 0, li, lc, c->sub_scratch.p, x));
-            DHT_TRY(hipStreamSynchronize(x));   // the host mask and the list are reused
-            return DHTGPU_OK;
-        };
-        if (!deficient.empty()) {
-            r = route(deficient, c->planes.as<uint32_t>(), c->stride, c->n, global ? c->gidx.as<uint32_t>() : nullptr);
-            if (r) return r;
-        }
-        for (uint32_t i : scan_subs) {
-            const dhtgpu_ctx::SubPart& sp = c->subs[i];
-            r = route(std::vector<uint32_t>{i}, sp.planes.as<uint32_t>(), sp.stride, sp.n,
-                      global ? sp.gmap.as<uint32_t>() : sp.map.as<uint32_t>());
-            if (r) return r;
-        }
-    }
-    for (int i = 0; i < 2; ++i) {
-        DHT_TRY(hipEventRecord(c->join[i], c->side[i]));
-        DHT_TRY(hipStreamWaitEvent(s, c->join[i], 0));
-    }
+    BatchCall bc{};
+    bc.planes = c->planes.as<uint32_t>();   // F4's scan: the whole set
+    bc.stride = c->stride;
+    bc.n = c->n;
+    bc.tp = tp;
+    bc.ts = ts;
+    bc.q = q;
+    bc.q_plan = q_plan;
+    bc.k = k;
+    bc.skip = P;
+    bc.gidx = global ? c->gidx.as<uint32_t>() : nullptr;
+    bc.base = 0;
+    bc.out_idx = li;
+    bc.out_cnt = lc;
+    bc.num_cus = c->num_cus;
+    bc.dbg = c->dbg;
+    bc.ev = ev;
+    bc.subs = specs.data();
+    bc.nsub = S;
+    bc.sub_shift = c->shard_pbits;
+    bc.sub_bits = sb;
+    r = batch_slot_run(c, si, bc, s, ev);
+    if (r) return r;
     if (out_rec) {
         DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, c->out_map(),
                                     out_rec, s));
@@ -863,7 +829,6 @@ int dhtgpu_batch_topk_timed(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     hipEvent_t ev[8];   // start/stop per kernel, recorded by the kernels' own dispatches
     for (int i = 0; i < 8; ++i) DHT_TRY(hipEventCreate(&ev[i]));
-    const bool subs = needs_subs(c, q, k);
     int r = batch_run(c, tp, ts, q, k, out_idx, out_cnt, nullptr, 0, s, ev);
     hipError_t e = r ? hipSuccess : hipStreamSynchronize(s);
     if (!r && e == hipSuccess) e = hipEventSynchronize(ev[7]);
@@ -874,13 +839,8 @@ int dhtgpu_batch_topk_timed(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint
     if (stats4 && c->last_small) {   // the small-batch path keeps no statistics
         for (int i = 0; i < 4; ++i) stats4[i] = 0;
     } else if (stats4) {
-        if (subs) {   // sub-partition 0's call (slot 0)
-            const auto& sp = c->subs[0];
-            const uint32_t qp = std::max<uint32_t>(1u, (uint32_t)(((uint64_t)q + (1u << c->sub_bits) - 1) >> c->sub_bits));
-            DHT_TRY(batch_read_stats(c->bslot[0].ws.p, sp.n, q, qp, k, c->num_cus, stats4, s));
-        } else {
-            DHT_TRY(batch_read_stats(c->bslot[c->blast].ws.p, c->n, q, q, k, c->num_cus, stats4, s));
-        }
+        DHT_TRY(batch_read_stats(c->bslot[c->blast].ws.p, c->last_n, q, c->last_qp, k, c->num_cus, stats4, s,
+                                 c->last_nsub));
     }
     return DHTGPU_OK;
 }

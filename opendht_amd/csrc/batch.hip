@@ -143,32 +143,44 @@ __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
 // ctr[kSpill]); F3 moves the spill list to the F4 fallback list.
 constexpr uint32_t kSpill = 8;   // ctr word: spilled targets (all-zero between calls)
 
-// Sub-partition calls (dhtgpu_ctx's prefix sub-partitions of a large id set) keep only the
-// targets whose bits [sel_shift, sel_shift + sel_bits) equal sel_val; the others belong to
-// another sub-partition's call.
+// Prefix sub-partitions (dhtgpu_ctx: a set too large for one plan is split by the next
+// sub_bits id bits after its shard prefix, each part compacted with its own shifted word-0
+// plane): ONE launch sequence serves all of them.  A target's sub-partition is its bits
+// [sub_shift, sub_shift + sub_bits); every sub-partition has its own bitmap and its own np
+// partitions (global partition = sub * np + p); F2's workgroups are dealt to the
+// sub-partitions in proportion to their ids; F3 / F4 read the tie words and map the results
+// through the target's sub-partition.  A set that needs no split is the one sub-partition.
+struct SubDesc {
+    const uint32_t* w0;       // streamed word-0 plane (shifted for shards / sub-partitions)
+    const uint32_t* planes;   // unshifted word planes (tie words)
+    uint64_t stride, n;
+    const uint32_t* gidx;     // result index map (nullable) ...
+    uint32_t base;            // ... or offset
+    uint32_t lim;             // last 16-B aligned word offset loadable inside w0's allocation
+    uint32_t blk0, nblk;      // its F2 workgroups
+    uint64_t per_blk;         // F2 ids per workgroup
+};
 
 struct F1Args {
     const uint32_t* tw0; const uint32_t* tw1;
-    uint32_t q, Lm, b1, shift, sel_shift, sel_bits, sel_val;
+    uint32_t q, Lm, b1, shift;
+    uint32_t sub_shift, sub_bits;   // a target's sub-partition: its bits [sub_shift, sub_shift + sub_bits)
+    uint32_t np, nwords;            // partitions and bitmap words per sub-partition
     uint32_t* bitmap;
     uint32_t* tcount; uint2* tbuf; uint32_t tcap;
     uint32_t* ctr; uint32_t* tspill;
 };
-
-__device__ __forceinline__ bool f1_keep(const F1Args& a, uint32_t w) {
-    return !a.sel_bits || ((w << a.sel_shift) >> (32 - a.sel_bits)) == a.sel_val;
-}
 
 __global__ __launch_bounds__(kF1Threads) void k_f1_targets(F1Args a) {
     if (blockIdx.x == 0 && threadIdx.x < 4) a.ctr[threadIdx.x] = 0;   // fallback, survivors, wave path, -
     const uint32_t i = blockIdx.x * kF1Threads + threadIdx.x;
     if (i >= a.q) return;
     const uint32_t w = a.tw0[i];
-    if (!f1_keep(a, w)) return;
+    const uint32_t sub = a.sub_bits ? (w << a.sub_shift) >> (32 - a.sub_bits) : 0u;
     const uint32_t v = a.shift ? (w << a.shift) | (a.tw1[i] >> (32 - a.shift)) : w;
     const uint32_t pre = top_bits(v, a.Lm);
-    atomicOr(a.bitmap + (pre >> 5), 1u << (pre & 31));
-    const uint32_t p = top_bits(v, a.b1);
+    atomicOr(a.bitmap + sub * a.nwords + (pre >> 5), 1u << (pre & 31));
+    const uint32_t p = sub * a.np + top_bits(v, a.b1);
     const uint32_t slot = atomicAdd(a.tcount + p * kCtrStride, 1u);
     if (slot < a.tcap) {
         a.tbuf[(uint64_t)p * a.tcap + slot] = make_uint2(v, i);
@@ -198,16 +210,17 @@ __host__ __device__ inline uint32_t f2_fixed_words(uint32_t nwords, uint32_t np)
 }
 
 struct F2Args {
-    const uint32_t* w0; uint64_t n; uint64_t per_blk;
+    const SubDesc* subs; const uint8_t* blk_sub;   // sub-partitions; workgroup -> sub-partition
+    SubDesc one; uint32_t nsub;                    // nsub == 1: the one sub-partition (no table loads)
+    uint32_t np_all;                               // partitions over all sub-partitions
     uint32_t Lm, b1;
     const uint32_t* bitmap; uint32_t nwords;
-    uint32_t* pcount;             // [kSets][np] survivors per set and partition (all-zero between calls)
-    uint2* pbuf;                  // [np][kSets][pcap] survivors, partition- and set-major
+    uint32_t* pcount;             // [kSets][np_all] survivors per set and partition (all-zero between calls)
+    uint2* pbuf;                  // [np_all][kSets][pcap] survivors, partition- and set-major
     uint32_t pcap;
     uint32_t* ctr;                // shared counters (F2 writes none; the survivor total is sum(pcount))
     uint32_t stage;               // LDS stage capacity (entries, <= kStage)
     uint32_t dbg;                 // experiment switches (0 in production)
-    uint32_t lim;                 // last 16-B aligned word offset loadable inside the plane allocation
     uint32_t sparse;              // 1: no per-sub-step barrier (plan: the stage holds a block's survivors)
     unsigned long long* stamps;   // dbg & 256: per-block phase timestamps [nblk2][16]
 };
@@ -220,7 +233,7 @@ struct F2Args {
 // atomic per partition reserved.  A partition that outgrows pcap keeps counting (F3 then
 // sends its targets to the fallback).
 constexpr uint32_t kStagePer = (kStage + 1023) / 1024;
-__device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* hist, uint32_t* wsum) {
+__device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* hist, uint32_t* wsum, uint32_t poff) {
     const uint32_t np = 1u << a.b1;
     if (a.dbg & 128) { sync_lds(); return; }
     for (uint32_t i = threadIdx.x; i <= np; i += kF2Threads) hist[i] = 0;
@@ -238,7 +251,7 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
     sync_lds();
     // reserve the partitions' slots (before the scan overwrites the counts)
     uint32_t res[8];
-    const uint32_t set = blockIdx.x % kSets, set_off = set * np;   // this block's bucket set
+    const uint32_t set = blockIdx.x % kSets, set_off = set * a.np_all + poff;   // this block's bucket set
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) {
         const uint32_t p = i * kF2Threads + threadIdx.x;
@@ -274,7 +287,7 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
             const uint2 x = stage[j];
             const uint32_t p = top_bits(x.x, a.b1);
             const uint32_t pos = hist[p] + j;
-            if (pos < a.pcap) a.pbuf[(uint64_t)(p * kSets + set) * a.pcap + pos] = x;
+            if (pos < a.pcap) a.pbuf[(uint64_t)((poff + p) * kSets + set) * a.pcap + pos] = x;
         }
     }
     sync_lds();
@@ -306,11 +319,15 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     uint32_t* wsum = hist + np + 1;
     uint32_t* lost = wsum + 17;   // sparse mode: partitions that lost survivors past a full stage
     uint2* stage = reinterpret_cast<uint2*>(sh + f2_fixed_words(a.nwords, np));
-    const uint64_t lo64 = (uint64_t)blockIdx.x * a.per_blk;
-    if (lo64 >= a.n) return;
+    const uint32_t sub = a.nsub == 1 ? 0u : (uint32_t)a.blk_sub[blockIdx.x];
+    const SubDesc d = a.nsub == 1 ? a.one : a.subs[sub];
+    const uint64_t lo64 = (uint64_t)(blockIdx.x - d.blk0) * d.per_blk;
+    if (lo64 >= d.n) return;
     F2_STAMP(0);
+    const uint32_t* const w0 = d.w0;
+    const uint32_t poff = sub * np;   // this sub-partition's first partition
     const uint32_t lo = (uint32_t)lo64;
-    const uint32_t hi = (uint32_t)(lo64 + a.per_blk < a.n ? lo64 + a.per_blk : a.n);
+    const uint32_t hi = (uint32_t)(lo64 + d.per_blk < d.n ? lo64 + d.per_blk : d.n);
     const uint32_t lane = lane_id();
     // level-Lm prefix = bits [32 - Lm, 32) of w0: one v_bfe
     const uint32_t pre_off = 32 - a.Lm;
@@ -320,7 +337,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     // per block than ring-first; per-XCD copies stored by F1 -- L2-resident on paper -- did not
     // shorten this phase either: it is the fabric, not the source); indices past the end are
     // clamped, so a clamped lane rewrites a word with its own value
-    const uint32_t* bsrc = a.bitmap;
+    const uint32_t* bsrc = a.bitmap + sub * a.nwords;
     if ((a.nwords & 3) == 0) {
         for (uint32_t i0 = 0; i0 < a.nwords; i0 += kF2Threads * 16) {
             uint4 t[4];
@@ -342,10 +359,10 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     // Loads past the block's range are clamped to its last 16 B (cache hits, masked).
     // (the ring's first loads take most of this phase's ~4 µs: all CUs start their streams at
     // once; the 64 KB bitmap copy alone is ~1 µs)
-    const uint32_t lim = min(a.lim, ((hi + 3u) & ~3u) - 4u);
+    const uint32_t lim = min(d.lim, ((hi + 3u) & ~3u) - 4u);
     uint4 ring[kRing];
 #pragma unroll
-    for (uint32_t r = 0; r < kRing; ++r) ring[r] = f2_load1(a.w0, lo + r * kF2Sub, lim);
+    for (uint32_t r = 0; r < kRing; ++r) ring[r] = f2_load1(w0, lo + r * kF2Sub, lim);
     if (threadIdx.x < 3) misc[threadIdx.x] = 0;
     for (uint32_t i = threadIdx.x; i <= np / 32; i += kF2Threads) lost[i] = 0;
     sync_lds();
@@ -364,7 +381,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                 cnt += ring[r].x ^ ring[r].y ^ ring[r].z ^ ring[r].w;
             } else if (sb < hi) {   // block-uniform
                 if (Mode == kF2Dense && cnt > a.stage - kF2Sub) {
-                    f2_flush(a, cnt, stage, hist, wsum);
+                    f2_flush(a, cnt, stage, hist, wsum, poff);
                     cnt = 0;
                 }
                 const uint32_t j0 = sb + 4 * threadIdx.x;
@@ -430,7 +447,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                     cnt += misc[s3 == 0 ? 2u : s3 - 1];
                 }
             }
-            ring[r] = f2_load1(a.w0, sb + kRing * kF2Sub, lim);
+            ring[r] = f2_load1(w0, sb + kRing * kF2Sub, lim);
         }
     }
     if (Mode == kF2Stream) { if (cnt == 0x12345678u) a.ctr[4] = cnt; return; }
@@ -439,14 +456,14 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
         cnt = misc[0] < a.stage ? misc[0] : a.stage;
     }
     F2_STAMP(2);
-    if (cnt) f2_flush(a, cnt, stage, hist, wsum);
+    if (cnt) f2_flush(a, cnt, stage, hist, wsum, poff);
     if (Mode == kF2Sparse) {   // partitions that lost entries: count past any stage (F3 -> fallback)
         for (uint32_t i = threadIdx.x; i <= np / 32; i += kF2Threads) {
             uint32_t m = lost[i];
             while (m) {
                 const uint32_t b = (uint32_t)__ffs(m) - 1;
                 m &= m - 1;
-                atomicAdd(a.pcount + (blockIdx.x % kSets) * np + 32 * i + b, a.pcap + 1u);
+                atomicAdd(a.pcount + (blockIdx.x % kSets) * a.np_all + poff + 32 * i + b, a.pcap + 1u);
             }
         }
     }
@@ -509,6 +526,7 @@ struct F3Args {
     uint4* tie_hdr;                      // [np][kTieSlots] deferred ties {qi, t0, count, 0}
     uint2* tie_cand;                     // [np][kTieSlots][64] their candidates {w0, idx}
     uint32_t* tie_cnt;                   // [np] deferred-tie slots in use per partition (all-zero between calls)
+    const SubDesc* subs; uint32_t np_sub;   // sub-partitions, partitions per sub-partition
     uint32_t dbg;
     unsigned long long* stamps;          // dbg & 256: per-block phase timestamps [np][16]
 };
@@ -629,7 +647,15 @@ __device__ __forceinline__ void f3_merge(uint32_t (&key)[K], uint32_t& lmin) {
 template <int K, bool Diag, bool Exact>
 __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     extern __shared__ uint32_t sh[];
-    const uint32_t p = blockIdx.x, np = gridDim.x;
+    const uint32_t p = blockIdx.x, np = gridDim.x;   // partition over all sub-partitions
+    const uint32_t sub = p / a.np_sub, pl = p - sub * a.np_sub;
+    if (a.np_sub != np) {   // tie words and result maps of the partition's sub-partition (a.n stays the set's)
+        const SubDesc d = a.subs[sub];
+        a.planes = d.planes;
+        a.stride = d.stride;
+        a.gidx = d.gidx;
+        a.base = d.base;
+    }
     F3_STAMP(0);
     if (Diag && (a.dbg & 1024)) __builtin_amdgcn_s_setprio(3);   // experiment: loads/sort first
     // survivors are sorted by their prefix bits [b1, Lq); a target answers from the deepest
@@ -641,8 +667,9 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     uint32_t* ntie = slow + kF3Threads + 1;   // [0] deferred-tie slots taken, [1] wave-path targets (stat)
     uint2* S = reinterpret_cast<uint2*>(sh + f3_words(nsub));
     uint2* T = S + kF3Cap;
-    // the bitmap is no longer read in this call: clear this block's share of it
-    for (uint32_t i = p + np * threadIdx.x; i < a.nwords; i += np * kF3Threads) a.bitmap[i] = 0;
+    // the bitmap is no longer read in this call: clear this block's share of its sub-partition's
+    for (uint32_t i = pl + a.np_sub * threadIdx.x; i < a.nwords; i += a.np_sub * kF3Threads)
+        a.bitmap[sub * a.nwords + i] = 0;
     for (uint32_t i = threadIdx.x; i <= nsub; i += kF3Threads) sofs[i] = 0;
     if (threadIdx.x == 0) ntie[0] = ntie[1] = 0;
     // survivors of this partition in each of the kSets bucket sets (F2), its targets (F1), and
@@ -1036,10 +1063,19 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
         for (uint32_t t = wv; t < total; t += scan::WAVES) {
             const uint32_t j = (uint32_t)__popcll(__ballot(inc <= t));   // partition j holds tie t
             const uint32_t before = j ? (uint32_t)__builtin_amdgcn_readlane((int)inc, (int)j - 1) : 0u;
-            const uint32_t g = (blockIdx.x + j * gridDim.x) * kTieSlots + (t - before);
+            const uint32_t part = blockIdx.x + j * gridDim.x;
+            const uint32_t g = part * kTieSlots + (t - before);
             const uint4 h = a.tie_hdr[g];
             const uint2 c = a.tie_cand[(uint64_t)g * 64 + lane];
-            wave_rank_answer(a, c, __builtin_amdgcn_readfirstlane(h.z), __builtin_amdgcn_readfirstlane(h.x),
+            F3Args as = a;   // the partition's sub-partition: tie words and result map
+            if (a.np_sub != f.np_ties) {
+                const SubDesc d = a.subs[__builtin_amdgcn_readfirstlane(part / a.np_sub)];
+                as.planes = d.planes;
+                as.stride = d.stride;
+                as.gidx = d.gidx;
+                as.base = d.base;
+            }
+            wave_rank_answer(as, c, __builtin_amdgcn_readfirstlane(h.z), __builtin_amdgcn_readfirstlane(h.x),
                              __builtin_amdgcn_readfirstlane(h.y), want, lane);
         }
         if (total) {   // block-uniform: every wave has read the counts before they are cleared
@@ -1187,15 +1223,15 @@ size_t f3_lds(const BatchPlan& P) {
 
 // DHTGPU_DBG=256: per-block phase profiles of F2 and F3 from their s_memrealtime stamps
 // (100 MHz real-time counter: 10 ns ticks), printed to stderr (synchronises s)
-void print_phase_profile(const BatchPlan& P, uint32_t np, unsigned long long* stamps, hipStream_t s) {
+void print_phase_profile(const BatchPlan& P, uint32_t nblk2, uint32_t np, unsigned long long* stamps, hipStream_t s) {
     if (!stamps) return;
     const uint32_t dbg = 256;
     if (dbg & 256) {   // phase profile of F2 (100 MHz real-time stamps: 10 ns ticks)
-        std::vector<unsigned long long> h((size_t)P.nblk2 * 16);
+        std::vector<unsigned long long> h((size_t)nblk2 * 16);
         (void)hipMemcpyAsync(h.data(), stamps + 8192 * 16, h.size() * 8, hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);
         unsigned long long t0 = ~0ull;
-        for (uint32_t b = 0; b < P.nblk2; ++b) t0 = h[b * 16] && h[b * 16] < t0 ? h[b * 16] : t0;
+        for (uint32_t b = 0; b < nblk2; ++b) t0 = h[b * 16] && h[b * 16] < t0 ? h[b * 16] : t0;
         auto pct2 = [](std::vector<double> d) {
             std::sort(d.begin(), d.end());
             const size_t m = d.size();
@@ -1206,12 +1242,12 @@ void print_phase_profile(const BatchPlan& P, uint32_t np, unsigned long long* st
         const char* nm[] = {"", "bitmap+ring", "stream+filter", "flush hist", "flush reserve+scan", "flush writes"};
         for (int i = 1; i <= 5; ++i) {
             std::vector<double> d;
-            for (uint32_t b = 0; b < P.nblk2; ++b)
+            for (uint32_t b = 0; b < nblk2; ++b)
                 if (h[b * 16 + 5]) d.push_back((double)(h[b * 16 + i] - h[b * 16 + i - 1]) / 100.0);
             if (!d.empty()) fprintf(stderr, "  F2 %-20s %s\n", nm[i], pct2(d).c_str());
         }
         std::vector<double> st, en;
-        for (uint32_t b = 0; b < P.nblk2; ++b)
+        for (uint32_t b = 0; b < nblk2; ++b)
             if (h[b * 16 + 5]) { st.push_back((double)(h[b * 16] - t0) / 100.0); en.push_back((double)(h[b * 16 + 5] - t0) / 100.0); }
         if (!st.empty()) fprintf(stderr, "  F2 start %s\n  F2 end   %s\n", pct2(st).c_str(), pct2(en).c_str());
     }
@@ -1301,46 +1337,120 @@ void set_lds_attributes() {
     for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
 }
 
-// workspace: bitmap (64 KB) | ctr[64] | pcount[kSets * kMaxParts] | tcount[kMaxParts * kCtrStride] |
-// tie_hdr[kMaxParts * kTieSlots] | fb done[kFbBlocks] | tie_cnt[kMaxParts] -- all-zero between calls -- |
-// fb_list[q] |
-// tspill[q] | pstat[np] | tbuf[np * tcap] | tie_cand[np * kTieSlots * 64] | pbuf[np * kSets * scap] |
-// fb rec[kFbBlocks * kFbGroup * k * 6]
-constexpr uint32_t kMaxParts = 1u << 13;
+// workspace: ctr[64] | bitmap[nsub][nwords] | pcount[kSets][NP] | tcount[NP * kCtrStride] |
+// tie_hdr[NP * kTieSlots] | fb done[kFbBlocks] | tie_cnt[NP] -- all-zero between calls -- |
+// fb_list[q] | tspill[q] | pstat[NP] | tbuf[NP * tcap] | tie_cand[NP * kTieSlots * 64] |
+// pbuf[NP * kSets * scap] | fb rec[kFbBlocks * kFbGroup * k * 6] | sub descriptors | F2 map
+// (NP = nsub * np partitions over all sub-partitions)
+constexpr uint32_t kMaxParts = 1u << 15;
+constexpr uint32_t kMaxSubs = 256;            // F2's workgroup -> sub-partition map is u8
+constexpr uint32_t kMaxF2Blocks = 65536;
 inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
+
+struct WsLayout {
+    size_t ctr, bitmap, pcount, tcount, tie_hdr, fb_done, tie_cnt, clean;
+    size_t fb_list, tspill, pstat, tbuf, tie_cand, pbuf, fb_rec, desc, blk_sub, total;
+};
+
+WsLayout ws_layout(const BatchPlan& P, uint32_t nsub, uint32_t q, uint32_t k) {
+    const size_t NP = (size_t)nsub << P.b1;
+    WsLayout L{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t r = off;
+        off += al256(bytes);
+        return r;
+    };
+    L.ctr = take(256);
+    L.bitmap = take((size_t)nsub * P.nwords * 4);
+    L.pcount = take((size_t)kSets * NP * 4);
+    L.tcount = take(NP * kCtrStride * 4);
+    L.tie_hdr = take(NP * kTieSlots * 16);
+    L.fb_done = take((size_t)kFbBlocks * 4);
+    L.tie_cnt = take(NP * 4);
+    L.clean = off;
+    L.fb_list = take((size_t)q * 4);
+    L.tspill = take((size_t)q * 4);
+    L.pstat = take(NP * 4);
+    L.tbuf = take(NP * P.tcap * 8);
+    L.tie_cand = take(NP * kTieSlots * 64 * 8);
+    L.pbuf = take(NP * kSets * P.scap * 8);
+    L.fb_rec = take((size_t)kFbBlocks * kFbGroup * k * 24);
+    L.desc = take((size_t)kMaxSubs * sizeof(SubDesc));
+    L.blk_sub = take(kMaxF2Blocks);
+    L.total = off;
+    return L;
+}
+
+// F2's workgroups over the sub-partitions: whole rounds of num_cus workgroups, each
+// sub-partition's share in proportion to its ids, and (sparse mode) no workgroup with more
+// ids than its stage holds on uniform ids (mean + 8 sigma + 256 survivors)
+uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, uint32_t q_plan, int num_cus,
+                        SubDesc* d) {
+    const double f = 1.0 - std::exp(-(double)q_plan / (double)(1ull << P.Lm));
+    uint64_t pb_cap = 1ull << 40;   // dense mode: no cap
+    if (P.sparse) {
+        pb_cap = kF2Step;
+        for (uint64_t pb = kF2Step; pb <= (1ull << 31); pb += kF2Step) {
+            const double mean = (double)pb * f, sd = std::sqrt(mean * (1.0 - f));
+            if (mean + 8.0 * sd + 256.0 > (double)P.stage) break;
+            pb_cap = pb;
+        }
+    }
+    const uint64_t g = num_cus > 0 ? (uint64_t)num_cus : 256;
+    uint64_t n_tot = 0, need = 0;
+    for (uint32_t i = 0; i < nsub; ++i) {
+        n_tot += subs[i].n;
+        need += (subs[i].n + pb_cap - 1) / pb_cap;
+    }
+    const uint64_t total = std::max<uint64_t>(1, (need + g - 1) / g) * g;
+    uint32_t blk = 0;
+    for (uint32_t i = 0; i < nsub; ++i) {
+        const uint64_t n = subs[i].n;
+        uint64_t want = n_tot ? (uint64_t)std::llround((double)total * (double)n / (double)n_tot) : 0;
+        want = std::max<uint64_t>(want, (n + pb_cap - 1) / pb_cap);
+        if (n && !want) want = 1;
+        uint64_t per = want ? (n + want - 1) / want : kF2Step;
+        per = (per + kF2Step - 1) / kF2Step * kF2Step;
+        if (per > pb_cap) per = pb_cap;
+        const uint64_t nb = n ? (n + per - 1) / per : 0;
+        const uint64_t lim = (subs[i].w0s ? subs[i].stride : 5 * subs[i].stride) - 4;
+        d[i] = SubDesc{subs[i].w0s ? subs[i].w0s : subs[i].planes, subs[i].planes, subs[i].stride, n, subs[i].gidx,
+                       subs[i].base, (uint32_t)(lim < 0xFFFFFFF0ull ? lim : 0xFFFFFFF0ull), blk, (uint32_t)nb, per};
+        blk += (uint32_t)nb;
+    }
+    return blk;
+}
 
 }  // namespace
 
-bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
-    if (k == 0 || k > DHTGPU_MAX_K_DEV || n >= (1ull << 31)) return false;
+bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t nsub) {
+    if (k == 0 || k > DHTGPU_MAX_K_DEV || n >= (1ull << 31) || nsub == 0 || nsub > kMaxSubs) return false;
     const BatchPlan P = plan_batch(n, q, k, num_cus);
-    if (q > kMaxQ) return false;
+    if ((uint64_t)q * nsub > kMaxQ) return false;
+    if (((uint64_t)nsub << P.b1) > kMaxParts) return false;
     // dense mode flushes whenever less than one sub-step of room is left
     if (!P.fits || P.Lm - P.b1 > 13 || (!P.sparse && P.stage < kF2Sub + 1024)) return false;
     return f3_lds(P) <= kLdsMax && f2_lds(P) <= kLdsMax;
 }
 
-size_t batch_clean_bytes() {
-    return 65536 + 256 + (size_t)kSets * kMaxParts * 4 + (size_t)kMaxParts * kCtrStride * 4 + (size_t)kMaxParts * kTieSlots * 16 +
-           al256((size_t)kFbBlocks * 4) + (size_t)kMaxParts * 4;
+size_t batch_clean_bytes(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub) {
+    return ws_layout(plan_batch(n, q_plan, k, num_cus), nsub, 0, k).clean;
 }
 
-size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus) {
-    const BatchPlan P = plan_batch(n, q_plan, k, num_cus);
-    const size_t np = 1ull << P.b1;
-    return batch_clean_bytes() + 2 * al256((size_t)q * 4) + al256(np * 4) + al256(np * P.tcap * 8) +
-           al256(np * kTieSlots * 64 * 8) + al256(kSets * np * P.scap * 8) + al256((size_t)kFbBlocks * kFbGroup * k * 24);
+size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub) {
+    return ws_layout(plan_batch(n, q_plan, k, num_cus), nsub, q, k).total;
 }
 
 hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus,
-                            uint32_t* stats4, hipStream_t s) {
+                            uint32_t* stats4, hipStream_t s, uint32_t nsub) {
     const BatchPlan P = plan_batch(n, q_plan, k, num_cus);
-    const size_t np = 1ull << P.b1;
+    const WsLayout Ly = ws_layout(P, nsub, q, k);
+    const size_t NP = (size_t)nsub << P.b1;
     const uint8_t* w = static_cast<const uint8_t*>(ws);
-    std::vector<uint32_t> ps(np);
-    hipError_t e = hipMemcpyAsync(stats4, w + 65536, 16, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(ps.data(), w + batch_clean_bytes() + 2 * al256((size_t)q * 4), np * 4, hipMemcpyDeviceToHost, s);
+    std::vector<uint32_t> ps(NP);
+    hipError_t e = hipMemcpyAsync(stats4, w + Ly.ctr, 16, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(ps.data(), w + Ly.pstat, NP * 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     uint64_t tot = 0;
     for (uint32_t v : ps) tot += v;
@@ -1362,36 +1472,69 @@ hipError_t launch_shift_w0(const uint32_t* planes, uint64_t stride, uint32_t shi
 
 hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     if (dirty) *dirty = false;
-    if (c.skip && !c.w0s) return hipErrorInvalidValue;
+    if (c.skip && !c.w0s && !c.nsub) return hipErrorInvalidValue;
+    if (c.nsub > kMaxSubs) return hipErrorInvalidValue;
     if (!c.q) return hipSuccess;
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDevices) std::call_once(g_attr_once[dev], set_lds_attributes);
-    const uint64_t n = c.n;
     const uint32_t q = c.q, k = c.k;
-    const BatchPlan P = plan_batch(n, c.q_plan, k, c.num_cus);
-    const uint32_t np = 1u << P.b1;
-    const uint32_t dbg = c.dbg;
+    // the sub-partitions (a set that needs no split is its own one sub-partition); the plan is
+    // the largest one's
+    const SubSpec one{c.planes, c.w0s, c.stride, c.n, c.gidx, c.base};
+    const SubSpec* subs = c.nsub ? c.subs : &one;
+    const uint32_t nsub = c.nsub ? c.nsub : 1u;
+    uint64_t n_max = 0;
+    for (uint32_t i = 0; i < nsub; ++i) n_max = std::max<uint64_t>(n_max, subs[i].n);
+    const BatchPlan P = plan_batch(n_max, c.q_plan, k, c.num_cus);
+    const uint32_t np = 1u << P.b1, NP = nsub * np;
+    uint32_t dbg = c.dbg;
     hipEvent_t* ev = c.ev;
-    uint8_t* w = static_cast<uint8_t*>(c.ws);
-    auto take = [&](size_t bytes) {
-        uint8_t* r = w;
-        w += al256(bytes);
-        return r;
-    };
-    uint32_t* bitmap = reinterpret_cast<uint32_t*>(take(65536));
-    uint32_t* ctr = reinterpret_cast<uint32_t*>(take(256));
-    uint32_t* pcount = reinterpret_cast<uint32_t*>(take((size_t)kSets * kMaxParts * 4));
-    uint32_t* tcount = reinterpret_cast<uint32_t*>(take((size_t)kMaxParts * kCtrStride * 4));
-    uint4* tie_hdr = reinterpret_cast<uint4*>(take((size_t)kMaxParts * kTieSlots * 16));
-    uint32_t* fb_done = reinterpret_cast<uint32_t*>(take((size_t)kFbBlocks * 4));
-    uint32_t* tie_cnt = reinterpret_cast<uint32_t*>(take((size_t)kMaxParts * 4));
-    uint32_t* fb_list = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
-    uint32_t* tspill = reinterpret_cast<uint32_t*>(take((size_t)q * 4));
-    uint32_t* pstat = reinterpret_cast<uint32_t*>(take((size_t)np * 4));
-    uint2* tbuf = reinterpret_cast<uint2*>(take((size_t)np * P.tcap * 8));
-    uint2* tie_cand = reinterpret_cast<uint2*>(take((size_t)np * kTieSlots * 64 * 8));
-    uint2* pbuf = reinterpret_cast<uint2*>(take((size_t)kSets * np * P.scap * 8));
-    uint32_t* fb_rec = reinterpret_cast<uint32_t*>(take((size_t)kFbBlocks * kFbGroup * k * 24));
+    const WsLayout Ly = ws_layout(P, nsub, q, k);
+    uint8_t* const w = static_cast<uint8_t*>(c.ws);
+    uint32_t* bitmap = reinterpret_cast<uint32_t*>(w + Ly.bitmap);
+    uint32_t* ctr = reinterpret_cast<uint32_t*>(w + Ly.ctr);
+    uint32_t* pcount = reinterpret_cast<uint32_t*>(w + Ly.pcount);
+    uint32_t* tcount = reinterpret_cast<uint32_t*>(w + Ly.tcount);
+    uint4* tie_hdr = reinterpret_cast<uint4*>(w + Ly.tie_hdr);
+    uint32_t* fb_done = reinterpret_cast<uint32_t*>(w + Ly.fb_done);
+    uint32_t* tie_cnt = reinterpret_cast<uint32_t*>(w + Ly.tie_cnt);
+    uint32_t* fb_list = reinterpret_cast<uint32_t*>(w + Ly.fb_list);
+    uint32_t* tspill = reinterpret_cast<uint32_t*>(w + Ly.tspill);
+    uint32_t* pstat = reinterpret_cast<uint32_t*>(w + Ly.pstat);
+    uint2* tbuf = reinterpret_cast<uint2*>(w + Ly.tbuf);
+    uint2* tie_cand = reinterpret_cast<uint2*>(w + Ly.tie_cand);
+    uint2* pbuf = reinterpret_cast<uint2*>(w + Ly.pbuf);
+    uint32_t* fb_rec = reinterpret_cast<uint32_t*>(w + Ly.fb_rec);
+    SubDesc* d_desc = reinterpret_cast<SubDesc*>(w + Ly.desc);
+    uint8_t* d_blk = w + Ly.blk_sub;
+    // sub-partition descriptors and F2's workgroup map: one sub-partition travels in the kernel
+    // arguments; several are uploaded when they differ from what this workspace holds
+    // (steady-state calls upload nothing)
+    SubDesc hd[kMaxSubs];
+    const uint32_t nblk2 = deal_f2_blocks(P, subs, nsub, c.q_plan, c.num_cus, hd);
+    if (nblk2 > kMaxF2Blocks) return hipErrorInvalidValue;
+    if (NP > 8192 || nblk2 > 8192) dbg &= ~256u;   // phase stamps hold 8192 workgroups per kernel
+    if (nsub > 1) {
+        uint64_t sig = 1469598103934665603ull;
+        auto mix = [&](const void* p, size_t b) {
+            const uint8_t* x = static_cast<const uint8_t*>(p);
+            for (size_t i = 0; i < b; ++i) sig = (sig ^ x[i]) * 1099511628211ull;
+        };
+        mix(hd, nsub * sizeof(SubDesc));
+        mix(&nsub, 4);
+        mix(&nblk2, 4);
+        if (sig == 0) sig = 1;
+        if (!c.desc_sig || *c.desc_sig != sig) {
+            std::vector<uint8_t> bs(nblk2);
+            for (uint32_t i = 0; i < nsub; ++i)
+                for (uint32_t b = 0; b < hd[i].nblk; ++b) bs[hd[i].blk0 + b] = (uint8_t)i;
+            hipError_t e = hipMemcpyAsync(d_desc, hd, nsub * sizeof(SubDesc), hipMemcpyHostToDevice, s);
+            if (e == hipSuccess && nblk2) e = hipMemcpyAsync(d_blk, bs.data(), nblk2, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);   // the host copies are released below
+            if (e != hipSuccess) return e;
+            if (c.desc_sig) *c.desc_sig = sig;
+        }
+    }
     // ev (diagnostics): 8 events, a start/stop pair per kernel recorded by the kernel's own
     // dispatch (hipExtLaunchKernel), so the pairs time the kernels themselves
     auto go = [&](int i, auto kern, dim3 g, dim3 b, size_t lds, auto... args) {
@@ -1400,18 +1543,13 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     };
     unsigned long long* stamps = (dbg & 256) ? c.stamps : nullptr;   // F3 [8192][16] then F2 [8192][16]
     if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)2 * 8192 * 16 * 8, s);
-    const F1Args a1{c.tp, c.tp + c.ts, q, P.Lm, P.b1, c.skip, c.sel_shift, c.sel_bits, c.sel_val, bitmap, tcount, tbuf,
-                    P.tcap, ctr, tspill};
+    const F1Args a1{c.tp, c.tp + c.ts, q, P.Lm, P.b1, c.skip, c.sub_shift, c.nsub ? c.sub_bits : 0u, np, P.nwords,
+                    bitmap, tcount, tbuf, P.tcap, ctr, tspill};
     go(0, k_f1_targets, dim3((q + kF1Threads - 1) / kF1Threads), dim3(kF1Threads), 0, a1);
-    const uint32_t* planes = c.planes;
-    const uint64_t stride = c.stride;
-    if (n) {
-        // F2 streams word 0, or the shifted word-0 plane of a prefix shard (stride words)
-        const uint64_t lim = (c.w0s ? stride : 5 * stride) - 4;
-        F2Args a2{c.w0s ? c.w0s : planes, n, P.per_blk, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, P.scap, ctr, P.stage, dbg,
-                  (uint32_t)(lim < 0xFFFFFFF0ull ? lim : 0xFFFFFFF0ull), P.sparse,
+    if (nblk2) {
+        F2Args a2{d_desc, d_blk, hd[0], nsub, NP, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, P.scap, ctr, P.stage, dbg, P.sparse,
                   stamps ? stamps + 8192 * 16 : nullptr};
-        const dim3 g2(P.nblk2), b2(kF2Threads);
+        const dim3 g2(nblk2), b2(kF2Threads);
         const size_t l2 = f2_lds(P);
         if (dbg & 64) go(1, k_f2_filter<kF2Stream>, g2, b2, l2, a2);
         else if (P.sparse) go(1, k_f2_filter<kF2Sparse>, g2, b2, l2, a2);
@@ -1426,14 +1564,15 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         return hipGetLastError();
     }
     if (dirty && (dbg & 48u)) *dirty = true;   // F3 ablation exits leave counters behind
-    F3Args a{pbuf, pcount, P.scap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, planes, stride, n,
-             c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, pstat, tie_hdr, tie_cand, tie_cnt, dbg,
-             stamps};
+    // the base arguments are the whole set's: F4's scan (fallback targets) runs over all its ids
+    F3Args a{pbuf, pcount, P.scap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, c.planes, c.stride,
+             c.n, c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, pstat, tie_hdr, tie_cand, tie_cnt,
+             d_desc, np, dbg, stamps};
     size_t l3 = f3_lds(P);
     if (dbg & 4096) l3 = l3 > 81920 ? l3 : 81920;   // experiment: 2 F3 blocks per CU
     if (dbg & 8192) l3 = l3 > 54000 ? l3 : 54000;   // experiment: 3 F3 blocks per CU
-    const dim3 g3(np), b3(kF3Threads);
-    const bool ex = n >= k && (k == 8 || k == 16 || k == 32);
+    const dim3 g3(NP), b3(kF3Threads);
+    const bool ex = c.n >= k && (k == 8 || k == 16 || k == 32);
 #define F3_GO(KK, DD)                                                         \
     do {                                                                      \
         if (ex) go(2, k_f3_answer<KK, DD, true>, g3, b3, l3, a);            \
@@ -1449,8 +1588,8 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         else F3_GO(32, false);
     }
 #undef F3_GO
-    if (dbg & 256) print_phase_profile(P, np, stamps, s);
-    const FbArgs fa{fb_rec, fb_done, kFbBlocks, np};
+    if (dbg & 256) print_phase_profile(P, nblk2, NP, stamps, s);
+    const FbArgs fa{fb_rec, fb_done, kFbBlocks, NP};
     const dim3 g4(kFbBlocks), b4(kF4Threads);
     if (k <= 8) go(3, k_f4<8>, g4, b4, 0, a, fa);
     else if (k <= 16) go(3, k_f4<16>, g4, b4, 0, a, fa);
@@ -1640,6 +1779,9 @@ __global__ __launch_bounds__(kS2Threads) void k_s2_answer(F3Args a, SmallArgs sa
 
 }  // namespace
 
+// F4 scratch for a list scan: done counters | split records
+static size_t list_scan_bytes(uint32_t k) { return al256((size_t)kFbBlocks * 4) + al256((size_t)kFbBlocks * kFbGroup * k * 24); }
+
 bool small_supported(uint64_t n, uint32_t q, uint32_t k) {
     return q >= 1 && q <= kSmallQ && k >= 1 && k <= DHTGPU_MAX_K_DEV && n >= 1 && n < (1ull << 31);
 }
@@ -1717,61 +1859,6 @@ hipError_t launch_small_topk(const BatchCall& c, void* sws, hipStream_t s) {
     if (c.k <= 8) go(3, k_f4<8>, g4, b4, 0, f, fa);
     else if (c.k <= 16) go(3, k_f4<16>, g4, b4, 0, f, fa);
     else go(3, k_f4<32>, g4, b4, 0, f, fa);
-    return hipGetLastError();
-}
-
-// ---- target routing for prefix sub-partitions -------------------------------------------
-// list[*cnt++] = i for every target whose bits [sel_shift, sel_shift + sel_bits) hold a value
-// v with bit v set in mask (order within the list does not matter: results are written to
-// the targets' own rows)
-__global__ __launch_bounds__(256) void k_select_targets(const uint32_t* __restrict__ tw0, uint32_t q, uint32_t sel_shift,
-                                                        uint32_t sel_bits, const uint32_t* __restrict__ mask,
-                                                        uint32_t* __restrict__ list, uint32_t* __restrict__ cnt) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t v = i < q ? (tw0[i] << sel_shift) >> (32 - sel_bits) : 0u;
-    const bool take = i < q && ((mask[v >> 5] >> (v & 31)) & 1u);
-    const uint64_t b = __ballot(take);
-    if (!b) return;
-    const uint32_t lane = lane_id(), first = (uint32_t)__ffsll((long long)b) - 1;
-    uint32_t base = 0;
-    if (lane == first) base = atomicAdd(cnt, (uint32_t)__popcll(b));
-    base = (uint32_t)__shfl((int)base, (int)first);
-    if (take) list[base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = i;
-}
-
-hipError_t launch_select_targets(const uint32_t* tw0, uint32_t q, uint32_t sel_shift, uint32_t sel_bits,
-                                 const uint32_t* d_mask, uint32_t* list, uint32_t* d_cnt, hipStream_t s) {
-    if (sel_bits == 0 || sel_bits > 16 || sel_shift + sel_bits > 32) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(d_cnt, 0, 4, s);
-    if (e != hipSuccess || !q) return e;
-    k_select_targets<<<(q + 255) / 256, 256, 0, s>>>(tw0, q, sel_shift, sel_bits, d_mask, list, d_cnt);
-    return hipGetLastError();
-}
-
-size_t list_scan_bytes(uint32_t k) { return al256((size_t)kFbBlocks * 4) + al256((size_t)kFbBlocks * kFbGroup * k * 24); }
-
-hipError_t launch_list_scan(const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp, uint64_t ts,
-                            uint32_t k, const uint32_t* list, const uint32_t* d_cnt, const uint32_t* gidx, uint32_t base,
-                            uint32_t* out_idx, uint32_t* out_cnt, void* scratch, hipStream_t s) {
-    uint8_t* w = static_cast<uint8_t*>(scratch);
-    F3Args a{};
-    a.planes = planes;
-    a.stride = stride;
-    a.n = n;
-    a.tp = tp;
-    a.ts = ts;
-    a.k = k;
-    a.gidx = gidx;
-    a.base = base;
-    a.out_idx = out_idx;
-    a.out_cnt = out_cnt;
-    a.ctr = const_cast<uint32_t*>(d_cnt);          // F4 reads the list length from ctr[0]
-    a.fb_list = const_cast<uint32_t*>(list);
-    const FbArgs fa{reinterpret_cast<uint32_t*>(w + al256((size_t)kFbBlocks * 4)), reinterpret_cast<uint32_t*>(w),
-                    kFbBlocks, 0u};
-    if (k <= 8) k_f4<8><<<kFbBlocks, kF4Threads, 0, s>>>(a, fa);
-    else if (k <= 16) k_f4<16><<<kFbBlocks, kF4Threads, 0, s>>>(a, fa);
-    else k_f4<32><<<kFbBlocks, kF4Threads, 0, s>>>(a, fa);
     return hipGetLastError();
 }
 

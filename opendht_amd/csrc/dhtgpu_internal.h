@@ -87,18 +87,25 @@ hipError_t launch_index_query(const void* ws, uint64_t n, uint32_t B, const uint
                               uint32_t* out_cnt, hipStream_t s);
 
 // batch.hip: K6 per-batch target-prefix filter + exact top-k (no persistent index).
-// q_plan: targets the call is planned for (= q, or the expected share of a sub-partition call
-// whose F1 keeps only the targets of its prefix).
-bool batch_supported(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus);
-size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus);
-// leading workspace bytes that must be zero before the first call (they are left zero)
-size_t batch_clean_bytes();
+// n: ids of the largest sub-partition (or of the set); q_plan: the targets one sub-partition
+// is planned for (q / nsub); nsub: sub-partitions served by the call (1: the set itself).
+bool batch_supported(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1);
+size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1);
+// leading workspace bytes that must be zero before a call (the call leaves them zero)
+size_t batch_clean_bytes(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1);
 // stats4 = {fallback targets, survivors, wave-path targets, 0} of the last call on workspace ws
 // (synchronises s)
 hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus,
-                            uint32_t* stats4, hipStream_t s);
+                            uint32_t* stats4, hipStream_t s, uint32_t nsub = 1);
 // prefix shards: out[i] = planes word 0 << shift | word 1 >> (32 - shift), i < stride
 hipError_t launch_shift_w0(const uint32_t* planes, uint64_t stride, uint32_t shift, uint32_t* out, hipStream_t s);
+// One prefix sub-partition of a K6 call's id set (host view; see batch.hip SubDesc).
+struct SubSpec {
+    const uint32_t* planes; const uint32_t* w0s;   // unshifted planes; shifted word-0 plane (nullable)
+    uint64_t stride, n;
+    const uint32_t* gidx; uint32_t base;           // result index map (nullable) or offset
+};
+
 struct BatchCall {
     void* ws;                              // workspace (batch_bytes), head zero (batch_clean_bytes)
     const uint32_t* planes; uint64_t stride; uint64_t n;   // the id set (unshifted word planes)
@@ -106,7 +113,9 @@ struct BatchCall {
     uint32_t q;                            // targets F1 reads (the whole batch)
     uint32_t q_plan;                       // targets the plan is sized for
     uint32_t k;
-    uint32_t sel_shift, sel_bits, sel_val; // F1 keeps targets whose bits [sel_shift, +sel_bits) == sel_val
+    const SubSpec* subs; uint32_t nsub;    // prefix sub-partitions (nsub 0: the set planes/n/w0s/gidx/base)
+    uint32_t sub_shift, sub_bits;          // a target's sub-partition: its bits [sub_shift, +sub_bits)
+    uint64_t* desc_sig;                    // the workspace's uploaded sub-partition descriptors (signature)
     uint32_t skip; const uint32_t* w0s;    // w0s = 32 id bits from bit `skip` (every id shares its top skip bits)
     const uint32_t* gidx; uint32_t base;   // result index map (nullable) or offset
     uint32_t* out_idx; uint32_t* out_cnt;  // rows of the ORIGINAL target indices
@@ -123,17 +132,6 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty);
 bool small_supported(uint64_t n, uint32_t q, uint32_t k);
 size_t small_bytes();
 hipError_t launch_small_topk(const BatchCall& c, void* sws, hipStream_t s);
-// list[] = the targets whose bits [sel_shift, +sel_bits) (sel_bits <= 16) hold a value whose bit
-// is set in d_mask; *d_cnt = their number (zeroed first)
-hipError_t launch_select_targets(const uint32_t* tw0, uint32_t q, uint32_t sel_shift, uint32_t sel_bits,
-                                 const uint32_t* d_mask, uint32_t* list, uint32_t* d_cnt, hipStream_t s);
-// exact top-k of the listed targets (count *d_cnt, on the device) by the K1 scan over the id
-// set, results in the targets' own rows (K6's F4 fallback pass run on its own); scratch:
-// list_scan_bytes(k), its first kFbBlocks words zero before the first call (left zero)
-size_t list_scan_bytes(uint32_t k);
-hipError_t launch_list_scan(const uint32_t* planes, uint64_t stride, uint64_t n, const uint32_t* tp, uint64_t ts,
-                            uint32_t k, const uint32_t* list, const uint32_t* d_cnt, const uint32_t* gidx, uint32_t base,
-                            uint32_t* out_idx, uint32_t* out_cnt, void* scratch, hipStream_t s);
 
 // sort.hip: lexicographic sort of an id set (stable LSD radix over the 160-bit keys).
 // out_planes (out_stride >= n) = the ids in ascending InfoHash order, perm[j] = the input index
