@@ -93,18 +93,31 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
 }
 
 // Exclusive scan of a[0, len) in LDS by a block of NT threads; returns the total.  Every
-// thread must call it.  wsum: NT / 64 + 1 words of LDS scratch.
+// thread must call it.  wsum: NT / 64 + 1 words of LDS scratch.  Wave w owns a contiguous
+// run of rows; a row is 4 consecutive entries per lane (one 16-B LDS access each, 256 entries
+// at consecutive addresses: no bank conflicts -- one thread per contiguous run of len / NT
+// entries was a stride-(len / NT) pattern, 7 us for 4096 bins) scanned with DPP, carrying
+// the row total.  Unaligned or ragged arrays take rows of one entry per lane.
 template <int NT>
 __device__ uint32_t scan_lds(uint32_t* a, uint32_t len, uint32_t* wsum) {
     constexpr int NW = NT / 64;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
-    const uint32_t per = (len + NT - 1) / NT;
-    const uint32_t b = threadIdx.x * per;
-    const uint32_t e = b + per < len ? b + per : len;
+    const bool vec = (len & 3u) == 0 && ((uintptr_t)a & 15u) == 0;
+    const uint32_t per = vec ? 4u : 1u, rl = 64u * per;
+    const uint32_t rows = (len + rl - 1) / rl, rpw = (rows + NW - 1) / NW;
+    const uint32_t r0 = w * rpw < rows ? w * rpw : rows, r1 = r0 + rpw < rows ? r0 + rpw : rows;
+    auto ld = [&](uint32_t r) {
+        const uint32_t i = r * rl + lane * per;
+        if (vec) return i < len ? *reinterpret_cast<const uint4*>(a + i) : make_uint4(0u, 0u, 0u, 0u);
+        return make_uint4(i < len ? a[i] : 0u, 0u, 0u, 0u);
+    };
     uint32_t s = 0;
-    for (uint32_t i = b; i < e; ++i) s += a[i];
-    const uint32_t x = wave_scan_incl(s);
-    if (lane == 63) wsum[w] = x;
+    for (uint32_t r = r0; r < r1; ++r) {
+        const uint4 v = ld(r);
+        s += v.x + v.y + v.z + v.w;
+    }
+    const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(s), 63);
+    if (lane == 0) wsum[w] = ws;
     sync_lds();
     if (threadIdx.x < 64) {
         const uint32_t v = lane < (uint32_t)NW ? wsum[lane] : 0u;
@@ -113,11 +126,17 @@ __device__ uint32_t scan_lds(uint32_t* a, uint32_t len, uint32_t* wsum) {
         if (lane == (uint32_t)NW - 1) wsum[NW] = xv;
     }
     sync_lds();
-    uint32_t run = wsum[w] + x - s;
-    for (uint32_t i = b; i < e; ++i) {
-        const uint32_t v = a[i];
-        a[i] = run;
-        run += v;
+    uint32_t carry = wsum[w];
+    for (uint32_t r = r0; r < r1; ++r) {
+        const uint4 v = ld(r);
+        const uint32_t t = v.x + v.y + v.z + v.w;
+        const uint32_t x = wave_scan_incl(t);
+        const uint32_t e0 = carry + x - t, i = r * rl + lane * per;
+        if (i < len) {
+            if (vec) *reinterpret_cast<uint4*>(a + i) = make_uint4(e0, e0 + v.x, e0 + v.x + v.y, e0 + v.x + v.y + v.z);
+            else a[i] = e0;
+        }
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
     }
     const uint32_t total = wsum[NW];
     sync_lds();
