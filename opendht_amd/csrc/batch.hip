@@ -240,7 +240,8 @@ struct F2Args {
     uint32_t* ctr;                // shared counters (F2 writes none; the survivor total is sum(pcount))
     uint32_t stage;               // LDS stage capacity (entries, <= kStage)
     uint32_t dbg;                 // experiment switches (0 in production)
-    uint32_t sparse;              // 1: no per-sub-step barrier (plan: the stage holds a block's survivors)
+    uint32_t sparse;              // 1: no per-sub-step barrier (plan: the stage holds a segment's survivors)
+    uint32_t seg;                 // sparse mode: ids per segment (the stage is flushed after each)
     unsigned long long* stamps;   // dbg & 256: per-block phase timestamps [nblk2][16]
 };
 #define F2_STAMP(i) \
@@ -393,6 +394,13 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     // Sparse mode: one counter misc[0] for the whole block, read after the final barrier.
     uint32_t cnt = 0, s3 = 0;
     for (uint32_t c0 = lo; c0 < hi; c0 += kRing * kF2Sub) {
+        if (Mode == kF2Sparse && c0 != lo && (c0 - lo) % a.seg == 0) {
+            // segment boundary (block-uniform): flush while the ring's next loads are in flight
+            sync_lds();
+            f2_flush(a, misc[0] < a.stage ? misc[0] : a.stage, stage, hist, wsum, poff);
+            if (threadIdx.x == 0) misc[0] = 0;
+            sync_lds();
+        }
 #pragma unroll
         for (uint32_t r = 0; r < kRing; ++r) {
             const uint32_t sb = c0 + r * kF2Sub;
@@ -1402,10 +1410,12 @@ WsLayout ws_layout(const BatchPlan& P, uint32_t nsub, uint32_t q, uint32_t k) {
 }
 
 // F2's workgroups over the sub-partitions: whole rounds of num_cus workgroups, each
-// sub-partition's share in proportion to its ids, and (sparse mode) no workgroup with more
-// ids than its stage holds on uniform ids (mean + 8 sigma + 256 survivors)
+// sub-partition's share in proportion to its ids.  Sparse mode: the stage is flushed every
+// *seg ids, the most it holds on uniform ids (mean + 8 sigma + 256 survivors) in whole ring
+// turns -- one round of workgroups however large the set; when not even one ring turn fits, no
+// workgroup gets more ids than that bound.
 uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, uint32_t q_plan, int num_cus,
-                        SubDesc* d) {
+                        SubDesc* d, uint32_t* seg) {
     const double f = 1.0 - std::exp(-(double)q_plan / (double)(1ull << P.Lm));
     uint64_t pb_cap = 1ull << 40;   // dense mode: no cap
     if (P.sparse) {
@@ -1415,6 +1425,12 @@ uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, 
             if (mean + 8.0 * sd + 256.0 > (double)P.stage) break;
             pb_cap = pb;
         }
+    }
+    *seg = 0xFFFFFFFFu;
+    constexpr uint64_t turn = (uint64_t)kRing * kF2Sub;
+    if (P.sparse && pb_cap >= turn) {
+        *seg = (uint32_t)std::min<uint64_t>(pb_cap / turn * turn, 0x80000000ull);
+        pb_cap = 1ull << 40;
     }
     const uint64_t g = num_cus > 0 ? (uint64_t)num_cus : 256;
     uint64_t n_tot = 0, need = 0;
@@ -1530,7 +1546,8 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     // arguments; several are uploaded when they differ from what this workspace holds
     // (steady-state calls upload nothing)
     SubDesc hd[kMaxSubs];
-    const uint32_t nblk2 = deal_f2_blocks(P, subs, nsub, c.q_plan, c.num_cus, hd);
+    uint32_t seg = 0;
+    const uint32_t nblk2 = deal_f2_blocks(P, subs, nsub, c.q_plan, c.num_cus, hd, &seg);
     if (nblk2 > kMaxF2Blocks) return hipErrorInvalidValue;
     if (NP > 8192 || nblk2 > 8192) dbg &= ~256u;   // phase stamps hold 8192 workgroups per kernel
     if (nsub > 1) {
@@ -1541,7 +1558,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         };
         mix(hd, nsub * sizeof(SubDesc));
         mix(&nsub, 4);
-        mix(&nblk2, 4);
+        mix(&nblk2, 4);   // (seg travels in the kernel arguments)
         if (sig == 0) sig = 1;
         if (!c.desc_sig || *c.desc_sig != sig) {
             std::vector<uint8_t> bs(nblk2);
@@ -1566,7 +1583,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
                     bitmap, tcount, tbuf, P.tcap, ctr, tspill};
     go(0, k_f1_targets, dim3((q + kF1Threads - 1) / kF1Threads), dim3(kF1Threads), 0, a1);
     if (nblk2) {
-        F2Args a2{d_desc, d_blk, hd[0], nsub, NP, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, P.scap, ctr, P.stage, dbg, P.sparse,
+        F2Args a2{d_desc, d_blk, hd[0], nsub, NP, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, P.scap, ctr, P.stage, dbg, P.sparse, seg,
                   stamps ? stamps + 8192 * 16 : nullptr};
         const dim3 g2(nblk2), b2(kF2Threads);
         const size_t l2 = f2_lds(P);
