@@ -125,6 +125,7 @@ struct dhtgpu_ctx {
     DevBuf srch;            // search_insert / table_stats staging
     // diagnostics (DHTGPU_DBG, read once at creation; phase stamps per context)
     uint32_t dbg = 0;
+    uint32_t f2_seg = 0;          // DHTGPU_F2SEG: F2 sparse-mode segment override (ids; 0 = plan's)
     hipEvent_t next_ev[8] = {};   // dhtgpu_batch_events: the next K6 call records its kernels here
     bool has_next_ev = false;
     DevBuf stamps;
@@ -185,6 +186,7 @@ int dhtgpu_ctx_create(int device, dhtgpu_ctx** out) {
     hipError_t e = c->bind();
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (const char* d = getenv("DHTGPU_DBG")) c->dbg = (uint32_t)atoi(d);
+    if (const char* d = getenv("DHTGPU_F2SEG")) c->f2_seg = (uint32_t)atoi(d);
     if (e == hipSuccess) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
@@ -678,6 +680,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     bc.out_cnt = lc;
     bc.num_cus = c->num_cus;
     bc.dbg = c->dbg;
+    bc.f2_seg = c->f2_seg;
     bc.ev = ev;
     bc.subs = specs.data();
     bc.nsub = S;
@@ -790,6 +793,7 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     bc.out_cnt = lc;
     bc.num_cus = c->num_cus;
     bc.dbg = c->dbg;
+    bc.f2_seg = c->f2_seg;
     bc.ev = ev;
     int r = batch_slot_run(c, si, bc, s, ev);
     if (r) return r;

@@ -325,9 +325,13 @@ __device__ __forceinline__ uint4 f2_load1(const uint32_t* __restrict__ w0, uint3
 
 // Modes: kF2Dense flushes the stage whenever a sub-step could overflow it (one barrier
 // per sub-step); kF2Sparse (the plan proved a block's survivors fit the stage) has no
-// barrier in the loop and flushes once at the end; kF2Stream is the streaming-only
+// barrier in the loop and flushes once at the end; kF2Seg is kF2Sparse with a flush every
+// a.seg ids (ranges longer than one stage-full: large sub-partitioned sets) -- its own
+// instantiation, because the flush inlined in the loop keeps the ring live across it (128
+// VGPRs, the whole register file at 16 waves per CU, where kF2Sparse needs 68 and leaves
+// room for the other stream's F1 / F4 waves); kF2Stream is the streaming-only
 // ablation (DHTGPU_DBG & 64).
-constexpr uint32_t kF2Dense = 0, kF2Sparse = 1, kF2Stream = 2;
+constexpr uint32_t kF2Dense = 0, kF2Sparse = 1, kF2Stream = 2, kF2Seg = 3;
 
 template <uint32_t Mode>
 __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
@@ -394,7 +398,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     // Sparse mode: one counter misc[0] for the whole block, read after the final barrier.
     uint32_t cnt = 0, s3 = 0;
     for (uint32_t c0 = lo; c0 < hi; c0 += kRing * kF2Sub) {
-        if (Mode == kF2Sparse && c0 != lo && (c0 - lo) % a.seg == 0) {
+        if (Mode == kF2Seg && c0 != lo && (c0 - lo) % a.seg == 0) {
             // segment boundary (block-uniform): flush while the ring's next loads are in flight
             sync_lds();
             f2_flush(a, misc[0] < a.stage ? misc[0] : a.stage, stage, hist, wsum, poff);
@@ -430,7 +434,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                 const uint32_t tot = (uint32_t)(__popcll(bal[0]) + __popcll(bal[1]) + __popcll(bal[2]) +
                                                 __popcll(bal[3]));
                 uint32_t base = 0;
-                const uint32_t ctr_i = Mode == kF2Sparse ? 0u : s3;
+                const uint32_t ctr_i = Mode == kF2Dense ? s3 : 0u;
                 if (lane == 0 && tot) base = atomicAdd(misc + ctr_i, tot);
                 uint32_t pos = __builtin_amdgcn_readfirstlane(base);
                 if (Mode == kF2Dense) {
@@ -478,13 +482,13 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
         }
     }
     if (Mode == kF2Stream) { if (cnt == 0x12345678u) a.ctr[4] = cnt; return; }
-    if (Mode == kF2Sparse) {
+    if (Mode == kF2Sparse || Mode == kF2Seg) {
         sync_lds();
         cnt = misc[0] < a.stage ? misc[0] : a.stage;
     }
     F2_STAMP(2);
     if (cnt) f2_flush(a, cnt, stage, hist, wsum, poff);
-    if (Mode == kF2Sparse) {   // partitions that lost entries: count past any stage (F3 -> fallback)
+    if (Mode == kF2Sparse || Mode == kF2Seg) {   // partitions that lost entries: count past any stage (F3 -> fallback)
         for (uint32_t i = threadIdx.x; i <= np / 32; i += kF2Threads) {
             uint32_t m = lost[i];
             while (m) {
@@ -1354,7 +1358,7 @@ std::once_flag g_attr_once[kMaxDevices];
 
 void set_lds_attributes() {
     const void* fs[] = {(const void*)k_f2_filter<kF2Dense>, (const void*)k_f2_filter<kF2Sparse>,
-                        (const void*)k_f2_filter<kF2Stream>,
+                        (const void*)k_f2_filter<kF2Stream>, (const void*)k_f2_filter<kF2Seg>,
                         (const void*)k_f3_answer<8, false, true>,  (const void*)k_f3_answer<16, false, true>,
                         (const void*)k_f3_answer<32, false, true>, (const void*)k_f3_answer<8, true, true>,
                         (const void*)k_f3_answer<16, true, true>,  (const void*)k_f3_answer<32, true, true>,
@@ -1548,6 +1552,12 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     SubDesc hd[kMaxSubs];
     uint32_t seg = 0;
     const uint32_t nblk2 = deal_f2_blocks(P, subs, nsub, c.q_plan, c.num_cus, hd, &seg);
+    if (c.f2_seg && P.sparse && seg != 0xFFFFFFFFu) {   // experiment: segments of whole ring turns
+        constexpr uint32_t turn = kRing * kF2Sub;
+        seg = std::max<uint32_t>(turn, c.f2_seg / turn * turn);
+    }
+    bool seg_used = false;   // some workgroup's range spans more than one segment
+    for (uint32_t i = 0; i < nsub; ++i) seg_used = seg_used || (hd[i].nblk && hd[i].per_blk > seg);
     if (nblk2 > kMaxF2Blocks) return hipErrorInvalidValue;
     if (NP > 8192 || nblk2 > 8192) dbg &= ~256u;   // phase stamps hold 8192 workgroups per kernel
     if (nsub > 1) {
@@ -1588,6 +1598,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         const dim3 g2(nblk2), b2(kF2Threads);
         const size_t l2 = f2_lds(P);
         if (dbg & 64) go(1, k_f2_filter<kF2Stream>, g2, b2, l2, a2);
+        else if (P.sparse && seg_used) go(1, k_f2_filter<kF2Seg>, g2, b2, l2, a2);
         else if (P.sparse) go(1, k_f2_filter<kF2Sparse>, g2, b2, l2, a2);
         else go(1, k_f2_filter<kF2Dense>, g2, b2, l2, a2);
     } else if (ev) {

@@ -121,6 +121,7 @@ struct BatchCall {
     uint32_t* out_idx; uint32_t* out_cnt;  // rows of the ORIGINAL target indices
     int num_cus;
     uint32_t dbg;                          // DHTGPU_DBG experiment switches (0 in production)
+    uint32_t f2_seg;                       // F2 sparse-mode segment override in ids (0: the plan's)
     unsigned long long* stamps;            // dbg & 256: phase stamps [2 * 8192 * 16]
     hipEvent_t* ev;                        // nullable: 8 events around F1..F4
 };

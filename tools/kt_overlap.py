@@ -10,7 +10,7 @@ import sys
 rows = []
 for f in glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        m = re.search(r"(k_f\d_\w+)", r["Kernel_Name"])
+        m = re.search(r"(k_f\d\w*)", r["Kernel_Name"])
         if m:
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), m.group(1)))
 rows.sort()
