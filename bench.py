@@ -45,6 +45,7 @@ import ctypes
 import json
 import os
 import platform
+import subprocess
 import sys
 import time
 
@@ -846,6 +847,20 @@ def cpu_baseline(O, ids, tg, a):
                     f"{a.cpu_threads} threads, {dt:.2f} s wall",
           "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "compiler": "g++ -O2 (the reference's Release)",
           "one_core": {"value": m1 / dt1, "unit": "queries/s", "sample": f"{m1} targets, {dt1:.2f} s"}}
+    # the same port built with g++ -O3 -march=native on this host
+    try:
+        with O.native():
+            t0 = time.perf_counter()
+            got_n, _ = O.topk(ids, tg, a.k, threads=a.cpu_threads)
+            dn = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            O.topk(ids, tg[:m1], a.k, threads=1)
+            dn1 = time.perf_counter() - t0
+        cb["O3_march_native"] = {"value": tg.shape[0] / dn, "unit": "queries/s", "cores": a.cpu_threads,
+                                 "one_core": {"value": m1 / dn1, "unit": "queries/s"},
+                                 "same_results": bool(np.array_equal(got_n, want))}
+    except (OSError, subprocess.CalledProcessError) as e:
+        cb["O3_march_native"] = {"error": str(e)[:200]}
     # cfg 1: findClosestNodes per target over a RoutingTable-shaped snapshot
     rng = np.random.default_rng(a.seed)
     myid = np.frombuffer(rng.bytes(20), dtype=np.uint8).copy()

@@ -1,9 +1,11 @@
 """ctypes wrapper around oracle/liboracle.so -- the CPU restatement used as the
 parity CHECKER.  Test infrastructure only: imported by tests/, __graft_entry__.smoke()
 and bench.py's cpu_baseline leg; never by the opendht_amd product path."""
+import contextlib
 import ctypes
 import os
 import subprocess
+import tempfile
 
 import numpy as np
 
@@ -25,51 +27,79 @@ def lib():
     if _lib is None:
         if not os.path.exists(_LIB):
             build()
-        L = ctypes.CDLL(_LIB)
-        L.orc_gen_ids.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u8p]
-        L.orc_xor_cmp.argtypes = [u8p, u8p, u8p]
-        L.orc_xor_cmp.restype = ctypes.c_int
-        L.orc_common_bits.argtypes = [u8p, u8p]
-        L.orc_common_bits.restype = ctypes.c_uint
-        L.orc_lowbit.argtypes = [u8p]
-        L.orc_lowbit.restype = ctypes.c_int
-        L.orc_cmp.argtypes = [u8p, u8p]
-        L.orc_cmp.restype = ctypes.c_int
-        L.orc_topk.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint32, ctypes.c_uint32,
-                               u32p, u32p, ctypes.c_int]
-        L.orc_table_new.argtypes = [u8p, ctypes.c_int]
-        L.orc_table_new.restype = ctypes.c_void_p
-        L.orc_table_free.argtypes = [ctypes.c_void_p]
-        L.orc_table_insert.argtypes = [ctypes.c_void_p, u8p]
-        L.orc_table_insert.restype = ctypes.c_int
-        L.orc_table_nbuckets.argtypes = [ctypes.c_void_p]
-        L.orc_table_nbuckets.restype = ctypes.c_uint32
-        L.orc_table_nnodes.argtypes = [ctypes.c_void_p]
-        L.orc_table_nnodes.restype = ctypes.c_uint32
-        L.orc_table_export.argtypes = [ctypes.c_void_p, u8p, u32p, u8p]
-        L.orc_find_bucket.argtypes = [ctypes.c_uint32, u8p, u8p]
-        L.orc_find_bucket.restype = ctypes.c_int
-        L.orc_depth.argtypes = [ctypes.c_uint32, u8p, ctypes.c_uint32]
-        L.orc_depth.restype = ctypes.c_uint
-        L.orc_find_closest.argtypes = [ctypes.c_uint32, u8p, u32p, u8p, u8p, u8p, ctypes.c_uint32, u32p]
-        L.orc_find_closest.restype = ctypes.c_uint32
-        L.orc_classify.argtypes = [ctypes.c_uint32, u8p, u8p, u8p, ctypes.c_uint64, u8p, u64p]
-        L.orc_search_insert.argtypes = [u8p, u8p, u8p, ctypes.c_uint32, ctypes.c_uint32, u32p, u8p, u32p, u8p, u64p,
-                                        u32p, u8p, u8p, ctypes.c_int]
-        L.orc_find_closest_batch.argtypes = [ctypes.c_uint32, u8p, u32p, u8p, u8p, u8p, ctypes.c_uint32,
-                                             ctypes.c_uint32, u32p, u32p, ctypes.c_int]
-        L.orc_cached_nodes_batch.argtypes = [u8p, ctypes.c_uint64, u8p, u8p, ctypes.c_uint32, ctypes.c_uint32,
-                                             u32p, u32p, ctypes.c_int]
-        L.orc_cached_nodes.argtypes = [u8p, ctypes.c_uint64, u8p, u8p, ctypes.c_uint32, u32p]
-        L.orc_cached_nodes.restype = ctypes.c_uint32
-        L.orc_buffer_nodes.argtypes = [u8p, u8p, ctypes.c_uint32, u8p, u32p, ctypes.c_uint32, u8p]
-        L.orc_buffer_nodes.restype = ctypes.c_uint32
-        L.orc_deserialize_node.argtypes = [u8p, ctypes.c_uint32, u8p, ctypes.c_uint32, u8p, u8p]
-        L.orc_deserialize_node.restype = ctypes.c_int
-        L.orc_search_batch.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint64, u8p, u32p, ctypes.c_uint32,
-                                       ctypes.c_uint32, u32p, u8p, u32p, u32p, u32p, ctypes.c_int]
-        _lib = L
+        _lib = _load(_LIB)
     return _lib
+
+
+_native = None
+
+
+@contextlib.contextmanager
+def native():
+    """The same restatement compiled here with g++ -O3 -march=native (SURVEY 8(d)(ii)'s second
+    CPU-baseline build), active inside the with-block.  Built on first use into a temp dir on
+    the host that runs it (march=native must be this host's CPU)."""
+    global _lib, _native
+    if _native is None:
+        d = tempfile.mkdtemp(prefix="oracle_native_")
+        so = os.path.join(d, "liboracle_native.so")
+        src = [os.path.join(ROOT, "oracle", f) for f in ("dht_oracle.cpp", "crawl_oracle.cpp")]
+        subprocess.check_call(["g++", "-O3", "-march=native", "-std=c++11", "-fPIC", "-pthread", "-shared",
+                               "-o", so] + src)
+        _native = _load(so)
+    saved = lib()
+    _lib = _native
+    try:
+        yield
+    finally:
+        _lib = saved
+
+
+def _load(path):
+    L = ctypes.CDLL(path)
+    L.orc_gen_ids.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u8p]
+    L.orc_xor_cmp.argtypes = [u8p, u8p, u8p]
+    L.orc_xor_cmp.restype = ctypes.c_int
+    L.orc_common_bits.argtypes = [u8p, u8p]
+    L.orc_common_bits.restype = ctypes.c_uint
+    L.orc_lowbit.argtypes = [u8p]
+    L.orc_lowbit.restype = ctypes.c_int
+    L.orc_cmp.argtypes = [u8p, u8p]
+    L.orc_cmp.restype = ctypes.c_int
+    L.orc_topk.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint32, ctypes.c_uint32,
+                           u32p, u32p, ctypes.c_int]
+    L.orc_table_new.argtypes = [u8p, ctypes.c_int]
+    L.orc_table_new.restype = ctypes.c_void_p
+    L.orc_table_free.argtypes = [ctypes.c_void_p]
+    L.orc_table_insert.argtypes = [ctypes.c_void_p, u8p]
+    L.orc_table_insert.restype = ctypes.c_int
+    L.orc_table_nbuckets.argtypes = [ctypes.c_void_p]
+    L.orc_table_nbuckets.restype = ctypes.c_uint32
+    L.orc_table_nnodes.argtypes = [ctypes.c_void_p]
+    L.orc_table_nnodes.restype = ctypes.c_uint32
+    L.orc_table_export.argtypes = [ctypes.c_void_p, u8p, u32p, u8p]
+    L.orc_find_bucket.argtypes = [ctypes.c_uint32, u8p, u8p]
+    L.orc_find_bucket.restype = ctypes.c_int
+    L.orc_depth.argtypes = [ctypes.c_uint32, u8p, ctypes.c_uint32]
+    L.orc_depth.restype = ctypes.c_uint
+    L.orc_find_closest.argtypes = [ctypes.c_uint32, u8p, u32p, u8p, u8p, u8p, ctypes.c_uint32, u32p]
+    L.orc_find_closest.restype = ctypes.c_uint32
+    L.orc_classify.argtypes = [ctypes.c_uint32, u8p, u8p, u8p, ctypes.c_uint64, u8p, u64p]
+    L.orc_search_insert.argtypes = [u8p, u8p, u8p, ctypes.c_uint32, ctypes.c_uint32, u32p, u8p, u32p, u8p, u64p,
+                                    u32p, u8p, u8p, ctypes.c_int]
+    L.orc_find_closest_batch.argtypes = [ctypes.c_uint32, u8p, u32p, u8p, u8p, u8p, ctypes.c_uint32,
+                                         ctypes.c_uint32, u32p, u32p, ctypes.c_int]
+    L.orc_cached_nodes_batch.argtypes = [u8p, ctypes.c_uint64, u8p, u8p, ctypes.c_uint32, ctypes.c_uint32,
+                                         u32p, u32p, ctypes.c_int]
+    L.orc_cached_nodes.argtypes = [u8p, ctypes.c_uint64, u8p, u8p, ctypes.c_uint32, u32p]
+    L.orc_cached_nodes.restype = ctypes.c_uint32
+    L.orc_buffer_nodes.argtypes = [u8p, u8p, ctypes.c_uint32, u8p, u32p, ctypes.c_uint32, u8p]
+    L.orc_buffer_nodes.restype = ctypes.c_uint32
+    L.orc_deserialize_node.argtypes = [u8p, ctypes.c_uint32, u8p, ctypes.c_uint32, u8p, u8p]
+    L.orc_deserialize_node.restype = ctypes.c_int
+    L.orc_search_batch.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint64, u8p, u32p, ctypes.c_uint32,
+                                   ctypes.c_uint32, u32p, u8p, u32p, u32p, u32p, ctypes.c_int]
+    return L
 
 
 def _p(a, t):
