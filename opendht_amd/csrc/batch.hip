@@ -317,10 +317,18 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
 // ring stays in flight): addresses past the id range are clamped into the plane
 // allocation and their words are masked by the caller's range test.
 constexpr uint32_t kRing = 8;
-__device__ __forceinline__ uint4 f2_load1(const uint32_t* __restrict__ w0, uint32_t c, uint32_t lim) {
+// The ring loads are buffer loads through a descriptor based at the workgroup's first id
+// (f2_rsrc): the plane pointers come from sub-partition descriptors in memory, whose address
+// space the compiler cannot infer -- plain loads through them are FLAT loads, which also count
+// on lgkmcnt, so every LDS wait in the loop would wait for the ring.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t f2_rsrc(const uint32_t* w0, uint32_t lo, uint32_t lim) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(w0 + lo), (short)0, (int)((lim - lo + 4u) * 4u), 0x00020000);
+}
+__device__ __forceinline__ uint4 f2_load1(__amdgpu_buffer_rsrc_t rs, uint32_t lo, uint32_t c, uint32_t lim) {
     uint32_t j = c + 4 * threadIdx.x;
     j = j < lim ? j : lim;
-    return *reinterpret_cast<const uint4*>(w0 + j);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((j - lo) * 4u), 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
 // Modes: kF2Dense flushes the stage whenever a sub-step could overflow it (one barrier
@@ -384,9 +392,10 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     // (the ring's first loads take most of this phase's ~4 µs: all CUs start their streams at
     // once; the 64 KB bitmap copy alone is ~1 µs)
     const uint32_t lim = min(d.lim, ((hi + 3u) & ~3u) - 4u);
+    const __amdgpu_buffer_rsrc_t rs = f2_rsrc(w0, lo, lim);
     uint4 ring[kRing];
 #pragma unroll
-    for (uint32_t r = 0; r < kRing; ++r) ring[r] = f2_load1(w0, lo + r * kF2Sub, lim);
+    for (uint32_t r = 0; r < kRing; ++r) ring[r] = f2_load1(rs, lo, lo + r * kF2Sub, lim);
     if (threadIdx.x < 3) misc[threadIdx.x] = 0;
     for (uint32_t i = threadIdx.x; i <= np / 32; i += kF2Threads) lost[i] = 0;
     sync_lds();
@@ -478,7 +487,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                     cnt += misc[s3 == 0 ? 2u : s3 - 1];
                 }
             }
-            ring[r] = f2_load1(w0, sb + kRing * kF2Sub, lim);
+            ring[r] = f2_load1(rs, lo, sb + kRing * kF2Sub, lim);
         }
     }
     if (Mode == kF2Stream) { if (cnt == 0x12345678u) a.ctr[4] = cnt; return; }
@@ -675,12 +684,15 @@ __device__ __forceinline__ void f3_merge(uint32_t (&key)[K], uint32_t& lmin) {
 
 // Diag: the DHTGPU_DBG build (phase stamps and ablation exits); production launches Diag = false.
 // Exact: k == K and n >= k, so want == K is a compile-time constant (no per-place masks).
-template <int K, bool Diag, bool Exact>
+// Subs: the call serves several prefix sub-partitions (tie words and result maps per partition);
+// the one-set instantiation keeps every pointer a kernel argument, so the compiler emits global
+// (not flat) loads through them
+template <int K, bool Diag, bool Exact, bool Subs>
 __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     extern __shared__ uint32_t sh[];
     const uint32_t p = blockIdx.x, np = gridDim.x;   // partition over all sub-partitions
     const uint32_t sub = p / a.np_sub, pl = p - sub * a.np_sub;
-    if (a.np_sub != np) {   // tie words and result maps of the partition's sub-partition (a.n stays the set's)
+    if (Subs && a.np_sub != np) {   // tie words and result maps of the partition's sub-partition (a.n stays the set's)
         const SubDesc d = a.subs[sub];
         a.planes = d.planes;
         a.stride = d.stride;
@@ -1359,12 +1371,15 @@ std::once_flag g_attr_once[kMaxDevices];
 void set_lds_attributes() {
     const void* fs[] = {(const void*)k_f2_filter<kF2Dense>, (const void*)k_f2_filter<kF2Sparse>,
                         (const void*)k_f2_filter<kF2Stream>, (const void*)k_f2_filter<kF2Seg>,
-                        (const void*)k_f3_answer<8, false, true>,  (const void*)k_f3_answer<16, false, true>,
-                        (const void*)k_f3_answer<32, false, true>, (const void*)k_f3_answer<8, true, true>,
-                        (const void*)k_f3_answer<16, true, true>,  (const void*)k_f3_answer<32, true, true>,
-                        (const void*)k_f3_answer<8, false, false>, (const void*)k_f3_answer<16, false, false>,
-                        (const void*)k_f3_answer<32, false, false>, (const void*)k_f3_answer<8, true, false>,
-                        (const void*)k_f3_answer<16, true, false>, (const void*)k_f3_answer<32, true, false>};
+                        (const void*)k_f3_answer<8, false, true, false>,  (const void*)k_f3_answer<16, false, true, false>,
+                        (const void*)k_f3_answer<32, false, true, false>, (const void*)k_f3_answer<8, true, true, false>,
+                        (const void*)k_f3_answer<16, true, true, false>,  (const void*)k_f3_answer<32, true, true, false>,
+                        (const void*)k_f3_answer<8, false, false, false>, (const void*)k_f3_answer<16, false, false, false>,
+                        (const void*)k_f3_answer<32, false, false, false>, (const void*)k_f3_answer<8, true, false, false>,
+                        (const void*)k_f3_answer<16, true, false, false>, (const void*)k_f3_answer<32, true, false, false>,
+                        (const void*)k_f3_answer<8, false, true, true>,  (const void*)k_f3_answer<16, false, true, true>,
+                        (const void*)k_f3_answer<32, false, true, true>, (const void*)k_f3_answer<8, false, false, true>,
+                        (const void*)k_f3_answer<16, false, false, true>, (const void*)k_f3_answer<32, false, false, true>};
     for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
 }
 
@@ -1620,19 +1635,23 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     if (dbg & 8192) l3 = l3 > 54000 ? l3 : 54000;   // experiment: 3 F3 blocks per CU
     const dim3 g3(NP), b3(kF3Threads);
     const bool ex = c.n >= k && (k == 8 || k == 16 || k == 32);
-#define F3_GO(KK, DD)                                                         \
+#define F3_GO(KK, DD, SS)                                                     \
     do {                                                                      \
-        if (ex) go(2, k_f3_answer<KK, DD, true>, g3, b3, l3, a);            \
-        else go(2, k_f3_answer<KK, DD, false>, g3, b3, l3, a);              \
+        if (ex) go(2, k_f3_answer<KK, DD, true, SS>, g3, b3, l3, a);        \
+        else go(2, k_f3_answer<KK, DD, false, SS>, g3, b3, l3, a);          \
     } while (0)
-    if (dbg) {
-        if (k <= 8) F3_GO(8, true);
-        else if (k <= 16) F3_GO(16, true);
-        else F3_GO(32, true);
+    if (nsub > 1) {   // (no phase-stamp build for sub-partitioned calls)
+        if (k <= 8) F3_GO(8, false, true);
+        else if (k <= 16) F3_GO(16, false, true);
+        else F3_GO(32, false, true);
+    } else if (dbg) {
+        if (k <= 8) F3_GO(8, true, false);
+        else if (k <= 16) F3_GO(16, true, false);
+        else F3_GO(32, true, false);
     } else {
-        if (k <= 8) F3_GO(8, false);
-        else if (k <= 16) F3_GO(16, false);
-        else F3_GO(32, false);
+        if (k <= 8) F3_GO(8, false, false);
+        else if (k <= 16) F3_GO(16, false, false);
+        else F3_GO(32, false, false);
     }
 #undef F3_GO
     if (dbg & 256) print_phase_profile(P, nblk2, NP, stamps, s);
