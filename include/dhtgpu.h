@@ -156,14 +156,14 @@ int dhtgpu_index_topk(dhtgpu_ctx* ctx, const uint8_t* targets20_be, uint32_t q, 
  * Large sets (n > 2^24 where one plan cannot cover the batch, e.g. the 2^27-id cfg-3 shard at
  * 131,072 targets): the set is split once into 2^s prefix sub-partitions of <= 2^24 ids (built
  * on the first such call, kept until the set changes: 28 B/id of extra HBM) and every call runs
- * one K6 pass per sub-partition, each answering the targets of its prefix; a sub-partition
- * with fewer than k ids sends its targets to the K1 scan over the whole set.
+ * ONE K6 launch sequence over all sub-partitions, each answering the targets of its prefix; a
+ * sub-partition with fewer than k ids sends its targets to the K1 scan over the whole set.
  * DHTGPU_ERANGE only when q > 2^22 (or n >= 2^32).
  * Stream-ordered, no host sync (except the one-time sub-partition build).  A context keeps four
  * workspaces used in turn, so up to four consecutive calls issued on different streams run
  * concurrently (one batch's latency-bound answer phase overlaps the next batch's HBM-bound id
  * stream); a call that reuses a workspace last used on another stream first waits for that
- * stream.  Sub-partitioned calls fork onto two context-internal streams and join back. */
+ * stream. */
 int dhtgpu_batch_topk_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
                           uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec,
                           uint32_t idx_base, void* stream);
@@ -171,8 +171,8 @@ int dhtgpu_batch_topk_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_
  * dispatch; synchronises and returns per-kernel device milliseconds ms4 = {F1 bucket
  * targets, F2 filter ids, F3 answer, F4 ties + fallback scan} and (nullable) stats4 =
  * {targets answered by the fallback scan, surviving ids, targets answered by an exact wave
- * (w0 ties, large subtrees), 0}.  Sub-partitioned calls: the kernels and statistics of
- * sub-partition 0. */
+ * (w0 ties, large subtrees), 0}.  Sub-partitioned calls: the one launch sequence over all
+ * sub-partitions. */
 int dhtgpu_batch_topk_timed(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
                             uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, void* stream, float* ms4,
                             uint32_t* stats4);
