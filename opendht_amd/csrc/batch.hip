@@ -562,6 +562,7 @@ struct F3Args {
     const uint32_t* gidx; uint32_t base;
     uint32_t* out_idx; uint32_t* out_cnt;
     uint32_t* ctr; uint32_t* fb_list;   // ctr[0] = fallback targets
+    uint8_t* fb_sub;                     // [q] the listed target's sub-partition (255: scan the whole set)
     uint32_t* pstat;                     // [np] survivors per partition (statistics; plain stores)
     uint4* tie_hdr;                      // [np][kTieSlots] deferred ties {qi, t0, count, 0}
     uint2* tie_cand;                     // [np][kTieSlots][64] their candidates {w0, idx}
@@ -740,7 +741,10 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         if (nsp) {   // one reservation for the block
             if (threadIdx.x == 0) ntie[2] = atomicAdd(a.ctr, nsp);
             sync_lds();
-            for (uint32_t j = threadIdx.x; j < nsp; j += kF3Threads) a.fb_list[ntie[2] + j] = a.tspill[j];
+            for (uint32_t j = threadIdx.x; j < nsp; j += kF3Threads) {
+                a.fb_list[ntie[2] + j] = a.tspill[j];
+                a.fb_sub[ntie[2] + j] = 255;
+            }
         }
     }
     sync_lds();   // every thread has read the counts
@@ -771,7 +775,10 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         // strongly clustered ids: this partition's targets take the exact brute-force path
         if (threadIdx.x == 0) ntie[2] = atomicAdd(a.ctr, mt);   // one reservation for the block
         sync_lds();
-        for (uint32_t j = threadIdx.x; j < mt; j += kF3Threads) a.fb_list[ntie[2] + j] = tsrc[j].y;
+        for (uint32_t j = threadIdx.x; j < mt; j += kF3Threads) {
+            a.fb_list[ntie[2] + j] = tsrc[j].y;
+            a.fb_sub[ntie[2] + j] = (uint8_t)sub;
+        }
         return;
     }
     const uint32_t smask = nsub - 1u;
@@ -845,7 +852,11 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
             const uint32_t mm = hi - lo;
             if (t0i == 0) F3_STAMP(8);
             if (mm < want) {
-                if (gj == 0) a.fb_list[atomicAdd(a.ctr, 1u)] = qi;
+                if (gj == 0) {
+                    const uint32_t at = atomicAdd(a.ctr, 1u);
+                    a.fb_list[at] = qi;
+                    a.fb_sub[at] = (uint8_t)sub;
+                }
             } else if (mm > kLaneMax || a.Lm == 0) {
                 if (gj == 0) {
                     slow[atomicAdd(slow + kF3Threads, 1u)] = slot;
@@ -1008,6 +1019,7 @@ constexpr uint32_t kF4Threads = scan::WAVES * 64;                 // 512
 constexpr uint32_t kFbGroup = scan::WAVES * kScanTargets;          // targets per scan role
 constexpr uint32_t kFbBlocks = 256;                                // fallback-scan workgroups
 constexpr uint32_t kFbCands = 256;                                 // merge: splits * k <= 256
+constexpr uint32_t kFbSingle = 64;                                 // per-target groups up to this many listed
 
 struct FbArgs {
     uint32_t* rec;      // [kFbBlocks * kFbGroup * k * 6] split lists (S > 1 only)
@@ -1026,13 +1038,15 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
     return x;
 }
 
-// merge the S sorted split lists of every target of group g (one wave per target)
-__device__ void fb_merge(const F3Args& a, const FbArgs& f, uint32_t g, uint32_t S, uint32_t cnt, uint32_t* lds) {
+// merge the S sorted split lists of every target of group g (one wave per target); gsize:
+// targets per group (kFbGroup, or 1 for the per-target groups of short sub-partitioned lists)
+__device__ void fb_merge(const F3Args& a, const FbArgs& f, uint32_t g, uint32_t S, uint32_t cnt, uint32_t* lds,
+                         uint32_t gsize = kFbGroup) {
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-    const uint32_t k = a.k, nt = cnt - g * kFbGroup < kFbGroup ? cnt - g * kFbGroup : kFbGroup;
+    const uint32_t k = a.k, nt = cnt - g * gsize < gsize ? cnt - g * gsize : gsize;
     uint32_t* buf = lds + wv * 2 * kFbCands;   // this wave's candidates: {w0 distance, local index}
     for (uint32_t j = wv; j < nt; j += scan::WAVES) {
-        const uint32_t qr = __builtin_amdgcn_readfirstlane(a.fb_list[g * kFbGroup + j]);
+        const uint32_t qr = __builtin_amdgcn_readfirstlane(a.fb_list[g * gsize + j]);
         uint32_t t[DHT_W];
         load_target(a.tp, a.ts, qr, t);
         for (uint32_t c = lane; c < S * k; c += 64) {
@@ -1128,6 +1142,48 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
     }
     const uint32_t cnt = a.ctr[0];
     if (cnt == 0) return;
+    if (a.np_sub != f.np_ties && cnt <= min(kFbSingle, f.np_ties / a.np_sub)) {
+        // sub-partitioned call, short list (on uniform ids: the rare target whose level-Lm
+        // subtree holds < k ids): every target is its own group and scans only its own
+        // sub-partition -- which holds its top-k when it holds >= k ids -- over S splits (a
+        // scan of the whole set cost a single target ~3 ms at 2^28 ids).  Up to one target per
+        // sub-partition: past that, one scan of the whole set for all of them reads less.
+        const uint32_t S = min(kFbCands / a.k, max(1u, f.nfb / cnt));
+        for (uint32_t role = blockIdx.x; role < cnt * S; role += f.nfb) {
+            const uint32_t g = role / S, sp = role - g * S;
+            const uint32_t sb = __builtin_amdgcn_readfirstlane((uint32_t)a.fb_sub[g]);
+            F3Args as = a;   // the target's sub-partition (or the whole set)
+            if (sb != 255u) {
+                const SubDesc d = a.subs[sb];
+                if (d.n >= a.k) {
+                    as.planes = d.planes;
+                    as.stride = d.stride;
+                    as.n = d.n;
+                    as.gidx = d.gidx;
+                    as.base = d.base;
+                }
+            }
+            const uint64_t nt = (as.n + scan::TILE - 1) / scan::TILE;
+            const uint64_t split_len = (nt ? (nt + S - 1) / S : 1) * scan::TILE;
+            const uint64_t lo = (uint64_t)sp * split_len < as.n ? (uint64_t)sp * split_len : as.n;
+            const uint64_t hi = lo + split_len < as.n ? lo + split_len : as.n;
+            // the target's split list goes to record slot (g * S + sp) * kFbGroup (fb_merge's layout)
+            const scan::ScanOut o{as.out_idx, as.out_cnt, as.gidx, as.base, S > 1 ? f.rec : nullptr,
+                                  ((uint64_t)g * S + sp) * kFbGroup - g, 0u};
+            scan::scan_run<K, kScanTargets>(lds, as.planes, as.stride, lo, hi, as.tp, as.ts, as.fb_list,
+                                            wv == 0 ? g : g + 1, g + 1, as.k, o);
+            if (S == 1) continue;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) last = atomicAdd(f.done + g, 1u) == S - 1 ? 1u : 0u;
+            __syncthreads();
+            if (!last) continue;
+            fb_merge(as, f, g, S, cnt, lds, 1u);
+            if (threadIdx.x == 0) f.done[g] = 0;
+            __syncthreads();
+        }
+        return;
+    }
     const uint32_t groups = (cnt + kFbGroup - 1) / kFbGroup;
     const uint64_t ntiles = (a.n + scan::TILE - 1) / scan::TILE;
     uint32_t S = f.nfb / groups;
@@ -1395,7 +1451,7 @@ inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
 struct WsLayout {
     size_t ctr, bitmap, pcount, tcount, tie_hdr, fb_done, tie_cnt, clean;
-    size_t fb_list, tspill, pstat, tbuf, tie_cand, pbuf, fb_rec, desc, blk_sub, total;
+    size_t fb_list, fb_sub, tspill, pstat, tbuf, tie_cand, pbuf, fb_rec, desc, blk_sub, total;
 };
 
 WsLayout ws_layout(const BatchPlan& P, uint32_t nsub, uint32_t q, uint32_t k) {
@@ -1416,6 +1472,7 @@ WsLayout ws_layout(const BatchPlan& P, uint32_t nsub, uint32_t q, uint32_t k) {
     L.tie_cnt = take(NP * 4);
     L.clean = off;
     L.fb_list = take((size_t)q * 4);
+    L.fb_sub = take((size_t)q);
     L.tspill = take((size_t)q * 4);
     L.pstat = take(NP * 4);
     L.tbuf = take(NP * P.tcap * 8);
@@ -1464,6 +1521,10 @@ uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, 
         uint64_t want = n_tot ? (uint64_t)std::llround((double)total * (double)n / (double)n_tot) : 0;
         want = std::max<uint64_t>(want, (n + pb_cap - 1) / pb_cap);
         if (n && !want) want = 1;
+        // whole groups of kSets workgroups: block b writes bucket set b % kSets, and scap plans
+        // every set for 1 / kSets of a partition's survivors (a sub-partition dealt 4 workgroups
+        // would fill only 4 sets, each twice over: overflowing partitions, fallback scans)
+        want = (want + kSets - 1) / kSets * kSets;
         uint64_t per = want ? (n + want - 1) / want : kF2Step;
         per = (per + kF2Step - 1) / kF2Step * kF2Step;
         if (per > pb_cap) per = pb_cap;
@@ -1553,6 +1614,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     uint32_t* fb_done = reinterpret_cast<uint32_t*>(w + Ly.fb_done);
     uint32_t* tie_cnt = reinterpret_cast<uint32_t*>(w + Ly.tie_cnt);
     uint32_t* fb_list = reinterpret_cast<uint32_t*>(w + Ly.fb_list);
+    uint8_t* fb_sub = w + Ly.fb_sub;
     uint32_t* tspill = reinterpret_cast<uint32_t*>(w + Ly.tspill);
     uint32_t* pstat = reinterpret_cast<uint32_t*>(w + Ly.pstat);
     uint2* tbuf = reinterpret_cast<uint2*>(w + Ly.tbuf);
@@ -1628,7 +1690,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     if (dirty && (dbg & 48u)) *dirty = true;   // F3 ablation exits leave counters behind
     // the base arguments are the whole set's: F4's scan (fallback targets) runs over all its ids
     F3Args a{pbuf, pcount, P.scap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, c.planes, c.stride,
-             c.n, c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, pstat, tie_hdr, tie_cand, tie_cnt,
+             c.n, c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, fb_sub, pstat, tie_hdr, tie_cand, tie_cnt,
              d_desc, np, dbg, stamps};
     size_t l3 = f3_lds(P);
     if (dbg & 4096) l3 = l3 > 81920 ? l3 : 81920;   // experiment: 2 F3 blocks per CU

@@ -82,6 +82,31 @@ def test_subpartition_with_fewer_than_k_ids(ctx):
     assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
 
 
+def test_subpartition_deficient_subtree_targets(ctx):
+    """Sub-partitioned call (2^26 ids, 2^18 targets: 4 sub-partitions) where two targets' own
+    level-18 subtrees (bits 2..19 after the 2 sub-partition bits; the mark level is 18 or 19)
+    are emptied down to 3 ids:
+    F3 lists them for the fallback scan, which for so short a list scans each target's own
+    sub-partition (it holds >= k ids, so their top-k lies inside it).  Whole batch == K1 scan,
+    the two targets == std::partial_sort(xorCmp)."""
+    n, q, k = 1 << 26, 1 << 18, 8
+    ids = O.gen_ids(2828, n)
+    tg = O.gen_ids(2829, q)
+    key = lambda a: ((a[:, 0].astype(np.uint32) << 16) | (a[:, 1].astype(np.uint32) << 8) | a[:, 2]) >> 4
+    tk, ik = key(tg), key(ids)
+    picks = [101, 202]
+    for t in picks:
+        inside = np.nonzero(ik == tk[t])[0][3:]
+        ids[inside, 2] ^= 0x10           # bit 19: into the sibling subtree, same sub-partition
+        ik = key(ids)
+    ctx.set_ids(ids)
+    got, cnt = ctx.batch_topk(tg, k)
+    sc, scnt = ctx.topk(tg, k)
+    assert np.array_equal(cnt, scnt) and np.array_equal(got, sc)
+    want, wcnt = O.topk(ids, tg[picks], k, threads=16)
+    assert np.array_equal(got[picks], want) and np.array_equal(cnt[picks], wcnt)
+
+
 @pytest.mark.parametrize("k", [8, 32])
 def test_clustered_ids_fallback_scan(ctx, k):
     """Verdict item 4: 2^24 ids of which 25 % share one 24-bit prefix, and targets inside the
