@@ -21,6 +21,7 @@ pmc cfg3 "cfg3shard:134217728x131072x8" "--n 134217728 --q 131072" &&
 echo pmc-ok &&
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $OUT/bench20.log 2>&1 && tail -1 $OUT/bench20.log > $OUT/bench20.json &&
 timeout -k 10 400 python bench.py > $OUT/bench.log 2>&1 && tail -1 $OUT/bench.log > $OUT/bench.json &&
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-extra > $OUT/kt.log 2>&1 &&
 python3 tools/kt_window.py $OUT/kt 5 20 > $OUT/kt_windows.txt && python3 tools/kt_window.py $OUT/kt 25 20 >> $OUT/kt_windows.txt &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt_small -o run --output-format csv -- python3 tools/small_probe.py > $OUT/kt_small.log 2>&1 &&
