@@ -82,6 +82,21 @@ def test_subpartition_with_fewer_than_k_ids(ctx):
     assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
 
 
+@pytest.mark.parametrize("k", [16, 32])
+def test_subpartitions_larger_k(ctx, k):
+    """2^26 ids, 2^18 targets (4 prefix sub-partitions, one K6 launch sequence) at k = 16 and
+    32: whole batch == K1 scan, a sample == std::partial_sort(xorCmp)."""
+    n, q = 1 << 26, 1 << 18
+    ctx.gen_ids(2929, n)
+    tg = O.gen_ids(2930, q)
+    got, cnt = ctx.batch_topk(tg, k)
+    sc, scnt = ctx.topk(tg, k)
+    assert np.array_equal(cnt, scnt) and np.array_equal(got, sc)
+    rows = sample_rows(q, 16)
+    want, wcnt = O.topk(O.gen_ids(2929, n), tg[rows], k, threads=16)
+    assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
+
+
 def test_subpartition_deficient_subtree_targets(ctx):
     """Sub-partitioned call (2^26 ids, 2^18 targets: 4 sub-partitions) where two targets' own
     level-18 subtrees (bits 2..19 after the 2 sub-partition bits; the mark level is 18 or 19)
