@@ -1142,17 +1142,30 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
     }
     const uint32_t cnt = a.ctr[0];
     if (cnt == 0) return;
-    if (a.np_sub != f.np_ties && cnt <= min(kFbSingle, f.np_ties / a.np_sub)) {
-        // sub-partitioned call, short list (on uniform ids: the rare target whose level-Lm
-        // subtree holds < k ids): every target is its own group and scans only its own
-        // sub-partition -- which holds its top-k when it holds >= k ids -- over S splits (a
-        // scan of the whole set cost a single target ~3 ms at 2^28 ids).  Up to one target per
-        // sub-partition: past that, one scan of the whole set for all of them reads less.
-        const uint32_t S = min(kFbCands / a.k, max(1u, f.nfb / cnt));
-        for (uint32_t role = blockIdx.x; role < cnt * S; role += f.nfb) {
-            const uint32_t g = role / S, sp = role - g * S;
+    // Sub-partitioned call with a short list (on uniform ids: the rare target whose level-Lm
+    // subtree holds < k ids): every target is its own group and scans only its own
+    // sub-partition -- which holds its top-k when it holds >= k ids -- over S splits (a scan of
+    // the whole set cost a single target ~3 ms at 2^28 ids).  Up to one target per
+    // sub-partition: past that, one scan of the whole set for all of them reads less.  (One
+    // scan_run call site for both forms: a second inlined copy doubled this kernel's VGPRs.)
+    const bool single = a.np_sub != f.np_ties && cnt <= min(kFbSingle, f.np_ties / a.np_sub);
+    const uint32_t gsize = single ? 1u : kFbGroup;
+    const uint32_t groups = (cnt + gsize - 1) / gsize;
+    const uint32_t smax = kFbCands / a.k;
+    uint32_t S = f.nfb / groups;
+    S = S < 1 ? 1u : S > smax ? smax : S;
+    if (!single) {
+        const uint64_t ntiles = (a.n + scan::TILE - 1) / scan::TILE;
+        if ((uint64_t)S > ntiles) S = ntiles ? (uint32_t)ntiles : 1u;
+        const uint64_t sl = (ntiles ? (ntiles + S - 1) / S : 1) * scan::TILE;
+        if (ntiles) S = (uint32_t)((a.n + sl - 1) / sl);
+    }
+    const uint32_t roles = groups * S;
+    for (uint32_t role = blockIdx.x; role < roles; role += f.nfb) {
+        const uint32_t g = role / S, sp = role - g * S;
+        F3Args as = a;   // single: the target's sub-partition (or the whole set)
+        if (single) {
             const uint32_t sb = __builtin_amdgcn_readfirstlane((uint32_t)a.fb_sub[g]);
-            F3Args as = a;   // the target's sub-partition (or the whole set)
             if (sb != 255u) {
                 const SubDesc d = a.subs[sb];
                 if (d.n >= a.k) {
@@ -1163,43 +1176,18 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
                     as.base = d.base;
                 }
             }
-            const uint64_t nt = (as.n + scan::TILE - 1) / scan::TILE;
-            const uint64_t split_len = (nt ? (nt + S - 1) / S : 1) * scan::TILE;
-            const uint64_t lo = (uint64_t)sp * split_len < as.n ? (uint64_t)sp * split_len : as.n;
-            const uint64_t hi = lo + split_len < as.n ? lo + split_len : as.n;
-            // the target's split list goes to record slot (g * S + sp) * kFbGroup (fb_merge's layout)
-            const scan::ScanOut o{as.out_idx, as.out_cnt, as.gidx, as.base, S > 1 ? f.rec : nullptr,
-                                  ((uint64_t)g * S + sp) * kFbGroup - g, 0u};
-            scan::scan_run<K, kScanTargets>(lds, as.planes, as.stride, lo, hi, as.tp, as.ts, as.fb_list,
-                                            wv == 0 ? g : g + 1, g + 1, as.k, o);
-            if (S == 1) continue;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (threadIdx.x == 0) last = atomicAdd(f.done + g, 1u) == S - 1 ? 1u : 0u;
-            __syncthreads();
-            if (!last) continue;
-            fb_merge(as, f, g, S, cnt, lds, 1u);
-            if (threadIdx.x == 0) f.done[g] = 0;
-            __syncthreads();
         }
-        return;
-    }
-    const uint32_t groups = (cnt + kFbGroup - 1) / kFbGroup;
-    const uint64_t ntiles = (a.n + scan::TILE - 1) / scan::TILE;
-    uint32_t S = f.nfb / groups;
-    const uint32_t smax = kFbCands / a.k;
-    S = S < 1 ? 1u : S > smax ? smax : S;
-    if ((uint64_t)S > ntiles) S = ntiles ? (uint32_t)ntiles : 1u;
-    const uint64_t split_len = (ntiles ? (ntiles + S - 1) / S : 1) * scan::TILE;
-    if (ntiles) S = (uint32_t)((a.n + split_len - 1) / split_len);
-    const uint32_t roles = groups * S;
-    for (uint32_t role = blockIdx.x; role < roles; role += f.nfb) {
-        const uint32_t g = role / S, sp = role - g * S;
-        const uint64_t lo = (uint64_t)sp * split_len, hi = lo + split_len < a.n ? lo + split_len : a.n;
-        const scan::ScanOut o{a.out_idx, a.out_cnt, a.gidx, a.base, S > 1 ? f.rec : nullptr,
-                              (uint64_t)g * kFbGroup * (S - 1) + (uint64_t)sp * kFbGroup, 0u};
-        scan::scan_run<K, kScanTargets>(lds, a.planes, a.stride, lo, hi, a.tp, a.ts, a.fb_list,
-                                        g * kFbGroup + wv * kScanTargets, cnt, a.k, o);
+        const uint64_t nt = (as.n + scan::TILE - 1) / scan::TILE;
+        const uint64_t split_len = (nt ? (nt + S - 1) / S : 1) * scan::TILE;
+        const uint64_t lo = (uint64_t)sp * split_len < as.n ? (uint64_t)sp * split_len : as.n;
+        const uint64_t hi = lo + split_len < as.n ? lo + split_len : as.n;
+        // split lists at record slot (g * S + sp) * kFbGroup + target-in-group (fb_merge's layout)
+        const uint64_t rb = single ? ((uint64_t)g * S + sp) * kFbGroup - g
+                                   : (uint64_t)g * kFbGroup * (S - 1) + (uint64_t)sp * kFbGroup;
+        const scan::ScanOut o{as.out_idx, as.out_cnt, as.gidx, as.base, S > 1 ? f.rec : nullptr, rb, 0u};
+        const uint32_t qb = single ? (wv == 0 ? g : g + 1) : g * kFbGroup + wv * kScanTargets;
+        scan::scan_run<K, kScanTargets>(lds, as.planes, as.stride, lo, hi, as.tp, as.ts, as.fb_list, qb,
+                                        single ? g + 1 : cnt, as.k, o);
         if (S == 1) continue;
         // hand-off: every wave's sc1 record stores drained, then one agent-scope add per block;
         // the block whose add completes the group merges it (its waves load after the barrier)
@@ -1208,7 +1196,7 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
         if (threadIdx.x == 0) last = atomicAdd(f.done + g, 1u) == S - 1 ? 1u : 0u;
         __syncthreads();
         if (!last) continue;
-        fb_merge(a, f, g, S, cnt, lds);
+        fb_merge(as, f, g, S, cnt, lds, gsize);
         if (threadIdx.x == 0) f.done[g] = 0;   // all-zero again for the next call
         __syncthreads();                       // lds is reused by this block's next role
     }
