@@ -324,6 +324,11 @@ constexpr uint32_t kRing = 8;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t f2_rsrc(const uint32_t* w0, uint32_t lo, uint32_t lim) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)(w0 + lo), (short)0, (int)((lim - lo + 4u) * 4u), 0x00020000);
 }
+__device__ __forceinline__ uint4 f2_load1g(const uint32_t* __restrict__ w0, uint32_t c, uint32_t lim) {
+    uint32_t j = c + 4 * threadIdx.x;
+    j = j < lim ? j : lim;
+    return *reinterpret_cast<const uint4*>(w0 + j);
+}
 __device__ __forceinline__ uint4 f2_load1(__amdgpu_buffer_rsrc_t rs, uint32_t lo, uint32_t c, uint32_t lim) {
     uint32_t j = c + 4 * threadIdx.x;
     j = j < lim ? j : lim;
@@ -341,7 +346,10 @@ __device__ __forceinline__ uint4 f2_load1(__amdgpu_buffer_rsrc_t rs, uint32_t lo
 // ablation (DHTGPU_DBG & 64).
 constexpr uint32_t kF2Dense = 0, kF2Sparse = 1, kF2Stream = 2, kF2Seg = 3;
 
-template <uint32_t Mode>
+// Subs: several sub-partitions (descriptors read from memory, ring through buffer loads); the
+// one-set instantiation takes its descriptor from the kernel arguments and streams with plain
+// global loads
+template <uint32_t Mode, bool Subs>
 __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     extern __shared__ uint32_t sh[];   // (32 spare) | misc[8] | bm[nwords] | hist[np + 1] | wsum[17] | lost[np/32 + 1] | stage
     const uint32_t np = 1u << a.b1;
@@ -351,8 +359,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     uint32_t* wsum = hist + np + 1;
     uint32_t* lost = wsum + 17;   // sparse mode: partitions that lost survivors past a full stage
     uint2* stage = reinterpret_cast<uint2*>(sh + f2_fixed_words(a.nwords, np));
-    const uint32_t sub = a.nsub == 1 ? 0u : (uint32_t)a.blk_sub[blockIdx.x];
-    const SubDesc d = a.nsub == 1 ? a.one : a.subs[sub];
+    const uint32_t sub = Subs ? (uint32_t)a.blk_sub[blockIdx.x] : 0u;
+    const SubDesc d = Subs ? a.subs[sub] : a.one;
     const uint64_t lo64 = (uint64_t)(blockIdx.x - d.blk0) * d.per_blk;
     if (lo64 >= d.n) return;
     F2_STAMP(0);
@@ -395,7 +403,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     const __amdgpu_buffer_rsrc_t rs = f2_rsrc(w0, lo, lim);
     uint4 ring[kRing];
 #pragma unroll
-    for (uint32_t r = 0; r < kRing; ++r) ring[r] = f2_load1(rs, lo, lo + r * kF2Sub, lim);
+    for (uint32_t r = 0; r < kRing; ++r)
+        ring[r] = Subs ? f2_load1(rs, lo, lo + r * kF2Sub, lim) : f2_load1g(w0, lo + r * kF2Sub, lim);
     if (threadIdx.x < 3) misc[threadIdx.x] = 0;
     for (uint32_t i = threadIdx.x; i <= np / 32; i += kF2Threads) lost[i] = 0;
     sync_lds();
@@ -487,7 +496,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                     cnt += misc[s3 == 0 ? 2u : s3 - 1];
                 }
             }
-            ring[r] = f2_load1(rs, lo, sb + kRing * kF2Sub, lim);
+            ring[r] = Subs ? f2_load1(rs, lo, sb + kRing * kF2Sub, lim) : f2_load1g(w0, sb + kRing * kF2Sub, lim);
         }
     }
     if (Mode == kF2Stream) { if (cnt == 0x12345678u) a.ctr[4] = cnt; return; }
@@ -1413,8 +1422,10 @@ constexpr int kMaxDevices = 64;
 std::once_flag g_attr_once[kMaxDevices];
 
 void set_lds_attributes() {
-    const void* fs[] = {(const void*)k_f2_filter<kF2Dense>, (const void*)k_f2_filter<kF2Sparse>,
-                        (const void*)k_f2_filter<kF2Stream>, (const void*)k_f2_filter<kF2Seg>,
+    const void* fs[] = {(const void*)k_f2_filter<kF2Dense, false>, (const void*)k_f2_filter<kF2Sparse, false>,
+                        (const void*)k_f2_filter<kF2Stream, false>, (const void*)k_f2_filter<kF2Seg, false>,
+                        (const void*)k_f2_filter<kF2Dense, true>, (const void*)k_f2_filter<kF2Sparse, true>,
+                        (const void*)k_f2_filter<kF2Stream, true>, (const void*)k_f2_filter<kF2Seg, true>,
                         (const void*)k_f3_answer<8, false, true, false>,  (const void*)k_f3_answer<16, false, true, false>,
                         (const void*)k_f3_answer<32, false, true, false>, (const void*)k_f3_answer<8, true, true, false>,
                         (const void*)k_f3_answer<16, true, true, false>,  (const void*)k_f3_answer<32, true, true, false>,
@@ -1427,7 +1438,7 @@ void set_lds_attributes() {
     for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
 }
 
-// workspace: ctr[64] | bitmap[nsub][nwords] | pcount[kSets][NP] | tcount[NP * kCtrStride] |
+// workspace: bitmap[nsub][nwords] | ctr[64] | pcount[kSets][NP] | tcount[kMaxParts * kCtrStride] |
 // tie_hdr[NP * kTieSlots] | fb done[kFbBlocks] | tie_cnt[NP] -- all-zero between calls -- |
 // fb_list[q] | tspill[q] | pstat[NP] | tbuf[NP * tcap] | tie_cand[NP * kTieSlots * 64] |
 // pbuf[NP * kSets * scap] | fb rec[kFbBlocks * kFbGroup * k * 6] | sub descriptors | F2 map
@@ -1451,13 +1462,16 @@ WsLayout ws_layout(const BatchPlan& P, uint32_t nsub, uint32_t q, uint32_t k) {
         off += al256(bytes);
         return r;
     };
+    // bitmap first and the counter arrays sized for kMaxParts partitions: the compact layout
+    // (counters right behind one another) cost F1 0.5 us and the pipelined cfg-2 step 0.3 us
+    // (measured); the clean head is memset once per workspace
+    L.bitmap = take(std::max<size_t>(65536, (size_t)nsub * P.nwords * 4));
     L.ctr = take(256);
-    L.bitmap = take((size_t)nsub * P.nwords * 4);
     L.pcount = take((size_t)kSets * NP * 4);
-    L.tcount = take(NP * kCtrStride * 4);
-    L.tie_hdr = take(NP * kTieSlots * 16);
+    L.tcount = take((size_t)kMaxParts * kCtrStride * 4);
+    L.tie_hdr = take((size_t)kMaxParts * kTieSlots * 16);
     L.fb_done = take((size_t)kFbBlocks * 4);
-    L.tie_cnt = take(NP * 4);
+    L.tie_cnt = take((size_t)kMaxParts * 4);
     L.clean = off;
     L.fb_list = take((size_t)q * 4);
     L.fb_sub = take((size_t)q);
@@ -1662,10 +1676,16 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
                   stamps ? stamps + 8192 * 16 : nullptr};
         const dim3 g2(nblk2), b2(kF2Threads);
         const size_t l2 = f2_lds(P);
-        if (dbg & 64) go(1, k_f2_filter<kF2Stream>, g2, b2, l2, a2);
-        else if (P.sparse && seg_used) go(1, k_f2_filter<kF2Seg>, g2, b2, l2, a2);
-        else if (P.sparse) go(1, k_f2_filter<kF2Sparse>, g2, b2, l2, a2);
-        else go(1, k_f2_filter<kF2Dense>, g2, b2, l2, a2);
+#define F2_GO(MM)                                                    \
+    do {                                                             \
+        if (nsub > 1) go(1, k_f2_filter<MM, true>, g2, b2, l2, a2);  \
+        else go(1, k_f2_filter<MM, false>, g2, b2, l2, a2);          \
+    } while (0)
+        if (dbg & 64) F2_GO(kF2Stream);
+        else if (P.sparse && seg_used) F2_GO(kF2Seg);
+        else if (P.sparse) F2_GO(kF2Sparse);
+        else F2_GO(kF2Dense);
+#undef F2_GO
     } else if (ev) {
         (void)hipEventRecord(ev[2], s);
         (void)hipEventRecord(ev[3], s);
