@@ -1110,14 +1110,15 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[scan::lds_words<kScanTargets>()];
     __shared__ uint32_t last;
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-    // deferred ties of the block's partitions p = blockIdx + j * gridDim (j < ppb <= 64): lane j
-    // loads partition j's count, a wave scan numbers the block's ties, and the waves take them
-    // round-robin -- every tie in flight at once (one round trip for the counts)
-    if (f.np_ties) {
+    // deferred ties of the block's partitions p = blockIdx + j * gridDim, 64 at a time (j0 + lane
+    // = j < ppb): lane j loads partition j's count, a wave scan numbers the round's ties, and
+    // the waves take them round-robin -- every tie in flight at once (one round trip for the
+    // counts; one round unless np_ties > 64 * gridDim)
+    const uint32_t ppb = f.np_ties ? (f.np_ties + gridDim.x - 1) / gridDim.x : 0u;
+    for (uint32_t j0 = 0; j0 < ppb; j0 += 64) {
         const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
-        const uint32_t ppb = (f.np_ties + gridDim.x - 1) / gridDim.x;
-        const uint32_t pj = blockIdx.x + lane * gridDim.x;
-        const bool mine = lane < ppb && pj < f.np_ties;
+        const uint32_t pj = blockIdx.x + (j0 + lane) * gridDim.x;
+        const bool mine = j0 + lane < ppb && pj < f.np_ties;
         const uint32_t myc = mine ? a.tie_cnt[pj] : 0u;
         uint32_t inc = myc;
 #pragma unroll
@@ -1129,7 +1130,7 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
         for (uint32_t t = wv; t < total; t += scan::WAVES) {
             const uint32_t j = (uint32_t)__popcll(__ballot(inc <= t));   // partition j holds tie t
             const uint32_t before = j ? (uint32_t)__builtin_amdgcn_readlane((int)inc, (int)j - 1) : 0u;
-            const uint32_t part = blockIdx.x + j * gridDim.x;
+            const uint32_t part = blockIdx.x + (j0 + j) * gridDim.x;
             const uint32_t g = part * kTieSlots + (t - before);
             const uint4 h = a.tie_hdr[g];
             const uint2 c = a.tie_cand[(uint64_t)g * 64 + lane];
