@@ -111,9 +111,10 @@ def parse():
     ap.add_argument("--no-extra", action="store_true", help="skip the extra legs (small batch, cfg 1/3/4/5)")
     ap.add_argument("--no-scan", action="store_true", help="skip the reference K1 scan measurement")
     ap.add_argument("--verify", type=int, default=16, help="targets re-checked against the oracle (rank 0)")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="batch algo: consecutive steps alternate over this many streams, so one step's "
-                         "latency-bound F3/F4 overlaps the next step's HBM-bound F2 (1 = strictly serial)")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="batch algo: consecutive steps rotate over this many streams, so one step's "
+                         "latency-bound F3/F4 overlaps the other steps' HBM-bound F2 (1 = strictly serial; "
+                         "3 measured best: 2 leaves each stream's F1-F4 chain exposed, 4 over-subscribes F2)")
     return ap.parse_args()
 
 

@@ -543,6 +543,22 @@ int dhtgpu_index_topk(dhtgpu_ctx* c, const uint8_t* t20, uint32_t q, uint32_t k,
 }
 
 // ---- K6 -------------------------------------------------------------------------------------
+// The workspace slot for a call on stream s: the next slot (round-robin) whose last user was s
+// (stream order suffices, no wait), else the next unused one, else the next in turn (which
+// then waits for its last stream).  Stream-affine, so that up to kBatchDepth streams in flight
+// never wait on each other (plain round-robin over 3 streams made every call wait).
+static int pick_slot(dhtgpu_ctx* c, hipStream_t s) {
+    constexpr int D = dhtgpu_ctx::kBatchDepth;
+    int si = -1;
+    for (int i = 0; i < D && si < 0; ++i)
+        if (c->bslot[(c->bnext + i) % D].last == s) si = (c->bnext + i) % D;
+    for (int i = 0; i < D && si < 0; ++i)
+        if (!c->bslot[(c->bnext + i) % D].last) si = (c->bnext + i) % D;
+    if (si < 0) si = c->bnext;
+    c->bnext = (si + 1) % D;
+    return si;
+}
+
 // One K6 launch sequence on workspace slot `si` (stream s): waits for the slot's previous user
 // when that was another stream, cleans the workspace head when needed.
 static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hipEvent_t* ev) {
@@ -646,8 +662,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     if (!batch_supported(n_max, q_plan, k, c->num_cus, S))
         return dhtgpu_topk_dev(c, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s);
     const bool global = c->has_gidx && c->map_global && !out_rec;
-    const int si = c->bnext;
-    c->bnext = (c->bnext + 1) % dhtgpu_ctx::kBatchDepth;
+    const int si = pick_slot(c, s);
     dhtgpu_ctx::BatchSlot& b = c->bslot[si];
     // record mode: context-local indices first (then records from the context's planes)
     uint32_t* li = out_idx;
@@ -700,8 +715,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
 // Batches of at most 64 targets: one pass over word 0 + one workgroup per target prefix (KS).
 static int small_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k, uint32_t* out_idx,
                      uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base, hipStream_t s, hipEvent_t* ev) {
-    const int si = c->bnext;
-    c->bnext = (c->bnext + 1) % dhtgpu_ctx::kBatchDepth;
+    const int si = pick_slot(c, s);
     dhtgpu_ctx::BatchSlot& b = c->bslot[si];
     if (b.last && b.last != s) {   // the slot's previous user on another stream
         if (!b.done) DHT_TRY(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
@@ -764,8 +778,7 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     c->last_small = false;
     if (needs_subs(c, q, k)) return batch_run_subs(c, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s, ev);
     if (!batch_supported(c->n, q, k, c->num_cus)) return DHTGPU_ERANGE;
-    const int si = c->bnext;
-    c->bnext = (c->bnext + 1) % dhtgpu_ctx::kBatchDepth;
+    const int si = pick_slot(c, s);
     dhtgpu_ctx::BatchSlot& b = c->bslot[si];
     const uint32_t* gidx = c->out_map();
     uint32_t* li = out_idx;

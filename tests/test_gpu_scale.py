@@ -213,3 +213,40 @@ def test_two_contexts_two_threads():
     for t in th:
         t.join(timeout=100)
     assert not errors, errors
+
+
+def test_batches_over_three_streams(ctx):
+    """Nine calls issued back to back over three streams without a synchronisation between them
+    (the bench's --inflight 3: each stream keeps its own workspace slot), then the same batches
+    one by one on the context's stream (every slot then changes streams: the cross-stream wait):
+    the results agree, and a sample == std::partial_sort(xorCmp)."""
+    import torch
+    import opendht_amd
+    n, q, k = 1 << 22, 16384, 8
+    ctx.gen_ids(3131, n)
+    dev = torch.device("cuda", 0)
+    L = opendht_amd.lib()
+    ts = (q + 63) // 64 * 64
+    tgs = [O.gen_ids(3200 + i, q) for i in range(9)]
+    tps = []
+    for tg in tgs:
+        tp = torch.zeros(5 * ts, dtype=torch.int32, device=dev)
+        tb = torch.from_numpy(tg.reshape(-1)).to(dev)
+        torch.cuda.synchronize()
+        assert L.dhtgpu_pack_dev(tb.data_ptr(), q, tp.data_ptr(), ts, ctx.stream) == 0
+        tps.append(tp)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    outs = [(torch.empty((q, k), dtype=torch.int32, device=dev), torch.empty(q, dtype=torch.int32, device=dev))
+            for _ in tgs]
+    for i, tp in enumerate(tps):
+        ctx.batch_topk_dev(tp.data_ptr(), ts, q, k, outs[i][0].data_ptr(), outs[i][1].data_ptr(), None, 0,
+                           streams[i % 3].cuda_stream)
+    torch.cuda.synchronize()
+    for i, tg in enumerate(tgs):
+        got, cnt = ctx.batch_topk(tg, k)
+        assert np.array_equal(outs[i][0].cpu().numpy().view(np.uint32), got), f"batch {i}"
+        assert np.array_equal(outs[i][1].cpu().numpy().view(np.uint32), cnt), f"batch {i}"
+    rows = sample_rows(q, 16)
+    want, wcnt = O.topk(O.gen_ids(3131, n), tgs[4][rows], k, threads=16)
+    assert np.array_equal(outs[4][0].cpu().numpy().view(np.uint32)[rows], want)
