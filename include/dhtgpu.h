@@ -160,10 +160,10 @@ int dhtgpu_index_topk(dhtgpu_ctx* ctx, const uint8_t* targets20_be, uint32_t q, 
  * sub-partition with fewer than k ids sends its targets to the K1 scan over the whole set.
  * DHTGPU_ERANGE only when q > 2^22 (or n >= 2^32).
  * Stream-ordered, no host sync (except the one-time sub-partition build).  A context keeps four
- * workspaces used in turn, so up to four consecutive calls issued on different streams run
- * concurrently (one batch's latency-bound answer phase overlaps the next batch's HBM-bound id
- * stream); a call that reuses a workspace last used on another stream first waits for that
- * stream. */
+ * workspaces and gives each stream its own (the one it last used, else a free one), so calls
+ * issued on up to four streams run concurrently (one batch's latency-bound answer phase
+ * overlaps the other batches' HBM-bound id streams); a call that must take a workspace last
+ * used on another stream (a fifth stream) first waits for that stream. */
 int dhtgpu_batch_topk_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
                           uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec,
                           uint32_t idx_base, void* stream);
