@@ -1027,7 +1027,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
 constexpr uint32_t kF4Threads = scan::WAVES * 64;                 // 512
 constexpr uint32_t kFbGroup = scan::WAVES * kScanTargets;          // targets per scan role
 constexpr uint32_t kFbBlocks = 256;                                // fallback-scan workgroups
-constexpr uint32_t kFbCands = 256;                                 // merge: splits * k <= 256
+constexpr uint32_t kFbCands = 256;                                 // merge: splits * k <= 256, splits <= 64
 constexpr uint32_t kFbSingle = 64;                                 // per-target groups up to this many listed
 
 struct FbArgs {
@@ -1161,7 +1161,9 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
     const bool single = a.np_sub != f.np_ties && cnt <= min(kFbSingle, f.np_ties / a.np_sub);
     const uint32_t gsize = single ? 1u : kFbGroup;
     const uint32_t groups = (cnt + gsize - 1) / gsize;
-    const uint32_t smax = kFbCands / a.k;
+    // splits: S * k candidates fit the merge buffer, and one list head per lane (S <= 64; at
+    // k < 4 the buffer alone allowed up to 256 splits, whose lists past lane 63 were dropped)
+    const uint32_t smax = kFbCands / a.k < 64u ? kFbCands / a.k : 64u;
     uint32_t S = f.nfb / groups;
     S = S < 1 ? 1u : S > smax ? smax : S;
     if (!single) {

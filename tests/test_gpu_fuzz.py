@@ -1,0 +1,54 @@
+"""Randomised GPU parity sweep: seeded random shapes (n from 1 to 2^21 ids, q from 1 to 4,096
+targets, k from 1 to 32) and id distributions the fixed cases do not combine -- uniform, a few
+shared 16-bit prefixes (clustered subtrees), a small pool drawn with replacement (equal ids:
+ties break by the lower index, `xorCmp` + `partial_sort` order), low-entropy ids (only the last
+bytes vary: w0 ties everywhere) -- with targets that are partly ids of the set.  K1 (scan),
+K4/K5 (bucket index) and K6 (batch prefix filter, and its small-batch path for q <= 64) are all
+compared with std::partial_sort(xorCmp) over every target.  Marked gpu."""
+import numpy as np
+import pytest
+
+import oracle as O
+from test_gpu_parity import check_topk
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import opendht_amd
+    c = opendht_amd.Context(0)
+    yield c
+    c.close()
+
+
+def make_case(seed):
+    rng = np.random.default_rng(seed)
+    n = int(np.exp(rng.uniform(0, np.log(1 << 20))))
+    q = int(rng.choice([1, 7, 64, 65, int(rng.integers(1, 3001))]))
+    if seed >= 24:   # K6's full-batch plans: 2^20..2^21 ids, 1,024..4,096 targets
+        n = int(rng.integers(1 << 20, (1 << 21) + 1))
+        q = int(rng.integers(1024, 4097))
+    k = int(rng.choice([1, 3, 8, 8, 16, 20, 32]))
+    kind = ("uniform", "clustered", "pool", "lowentropy")[seed % 4]
+    ids = rng.integers(0, 256, size=(n, 20), dtype=np.uint8)
+    if kind == "clustered":
+        heads = rng.integers(0, 256, size=(int(rng.integers(1, 9)), 2), dtype=np.uint8)
+        ids[:, :2] = heads[rng.integers(0, len(heads), n)]
+    elif kind == "pool":
+        pool = rng.integers(0, 256, size=(max(1, n // 3), 20), dtype=np.uint8)
+        ids = pool[rng.integers(0, len(pool), n)]
+    elif kind == "lowentropy":
+        ids[:, :17] = rng.integers(0, 256, size=17, dtype=np.uint8)
+    tg = rng.integers(0, 256, size=(q, 20), dtype=np.uint8)
+    if kind != "uniform":   # targets from the ids' distribution: inside the dense subtrees
+        take = rng.random(q) < 0.5
+        tg[take] = ids[rng.integers(0, n, int(take.sum()))]
+        tg[take, 19] ^= rng.integers(0, 256, int(take.sum()), dtype=np.uint8)
+    return np.ascontiguousarray(ids), np.ascontiguousarray(tg), k, kind
+
+
+@pytest.mark.parametrize("seed", range(32))
+def test_random_shapes(ctx, seed):
+    ids, tg, k, kind = make_case(seed)
+    check_topk(ctx, ids, tg, k)

@@ -690,3 +690,19 @@ def test_small_batch_prefix_shard(ctx, pbits, pval):
     finally:
         ctx.set_global_indices(True)
     assert np.array_equal(lcnt, wc) and np.array_equal(loc, w)
+
+
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_fallback_scan_small_k(ctx, k):
+    """k < 4 with targets whose level-Lm subtree is empty (about 80 of 2,790 here at k = 1): F4's
+    fallback scan may use up to 256 / k id-range splits, but its merge walks one split list per
+    lane, so the splits are capped at 64 (lists past lane 63 were dropped: found by the
+    randomised sweep, tests/test_gpu_fuzz.py seed 24)."""
+    ids = O.gen_ids(2401, 1871338)
+    tg = O.gen_ids(2402, 2790)
+    ctx.set_ids(ids)
+    want, wcnt = O.topk(ids, tg, k, threads=16)
+    got, cnt = ctx.batch_topk(tg, k)
+    assert np.array_equal(cnt, wcnt)
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} targets differ, first {bad[:5]}"
