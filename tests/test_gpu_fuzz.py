@@ -52,3 +52,27 @@ def make_case(seed):
 def test_random_shapes(ctx, seed):
     ids, tg, k, kind = make_case(seed)
     check_topk(ctx, ids, tg, k)
+
+
+def make_edge_case(seed):
+    """Boundary shapes: n at or next to a power of two (plan levels flip there), n < k, q
+    around the small-batch limit (64 / 65) and K6's target-bucket sizes, exact-hit targets
+    (distance 0), ids sorted by key (F2 blocks see one prefix range each)."""
+    rng = np.random.default_rng(10_000 + seed)
+    p = int(rng.integers(0, 22))
+    n = max(1, (1 << p) + int(rng.choice([-1, 0, 1, 3])))
+    q = int(rng.choice([1, 2, 63, 64, 65, 66, 255, 256, 257, int(rng.integers(1, 2049))]))
+    k = int(rng.integers(1, 33))
+    ids = rng.integers(0, 256, size=(n, 20), dtype=np.uint8)
+    if seed % 3 == 1:   # sorted by the full key
+        ids = ids[np.lexsort(ids.T[::-1])]
+    tg = rng.integers(0, 256, size=(q, 20), dtype=np.uint8)
+    hit = rng.random(q) < 0.3
+    tg[hit] = ids[rng.integers(0, n, int(hit.sum()))]   # exact hits
+    return np.ascontiguousarray(ids), np.ascontiguousarray(tg), k
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_edge_shapes(ctx, seed):
+    ids, tg, k = make_edge_case(seed)
+    check_topk(ctx, ids, tg, k)
