@@ -82,10 +82,11 @@ def test_subpartition_with_fewer_than_k_ids(ctx):
     assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
 
 
-@pytest.mark.parametrize("k", [16, 32])
+@pytest.mark.parametrize("k", [1, 3, 16, 32])
 def test_subpartitions_larger_k(ctx, k):
-    """2^26 ids, 2^18 targets (4 prefix sub-partitions, one K6 launch sequence) at k = 16 and
-    32: whole batch == K1 scan, a sample == std::partial_sort(xorCmp)."""
+    """2^26 ids, 2^18 targets (4 prefix sub-partitions, one K6 launch sequence) at k = 1, 3, 16
+    and 32 (k < 4: many empty mark-level subtrees, so the fallback scan's per-target form runs
+    with its split cap): whole batch == K1 scan, a sample == std::partial_sort(xorCmp)."""
     n, q = 1 << 26, 1 << 18
     ctx.gen_ids(2929, n)
     tg = O.gen_ids(2930, q)
