@@ -76,3 +76,46 @@ def make_edge_case(seed):
 def test_edge_shapes(ctx, seed):
     ids, tg, k = make_edge_case(seed)
     check_topk(ctx, ids, tg, k)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_find_closest_random_tables(ctx, seed):
+    """RoutingTable::findClosestNodes (K1r) on random tables: node count, expired fraction,
+    a cluster near myid (deep buckets), count from 1 to 32; every target vs the oracle."""
+    rng = np.random.default_rng(20_000 + seed)
+    myid = rng.integers(0, 256, size=20, dtype=np.uint8)
+    ids = rng.integers(0, 256, size=(int(rng.integers(1, 20001)), 20), dtype=np.uint8)
+    if seed % 2:
+        m = int(rng.integers(1, 10))
+        ids[: ids.shape[0] // 2, :m] = myid[:m]
+    firsts, off, nodes = O.Table(myid).grow(ids).export()
+    good = (rng.random(nodes.shape[0]) >= rng.uniform(0, 0.9)).astype(np.uint8)
+    tg = rng.integers(0, 256, size=(int(rng.integers(1, 300)), 20), dtype=np.uint8)
+    if nodes.shape[0]:
+        tg = np.concatenate([tg, nodes[rng.integers(0, nodes.shape[0], 8)]])
+    count = int(rng.integers(1, 33))
+    got, cnt = ctx.find_closest(firsts, off, nodes, good, tg, count)
+    for qi in range(tg.shape[0]):
+        want = O.find_closest(firsts, off, nodes, good, tg[qi], count)
+        assert cnt[qi] == len(want) and list(got[qi, : cnt[qi]]) == list(want), (seed, qi)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_cached_nodes_random(ctx, seed):
+    """NodeCache::getCachedNodes (a8) on random sorted caches: size, accept fraction, count,
+    targets on and between cached ids; every target vs the oracle."""
+    rng = np.random.default_rng(30_000 + seed)
+    n = int(rng.integers(1, 60001))
+    ids = rng.integers(0, 256, size=(n, 20), dtype=np.uint8)
+    if seed % 3 == 2:
+        ids[: n // 2, :6] = ids[0, :6]
+    s = np.unique(ids, axis=0)   # a std::map: unique keys, sorted
+    acc = (rng.random(s.shape[0]) < rng.uniform(0.05, 1.0)).astype(np.uint8)
+    ctx.set_ids(np.ascontiguousarray(s))
+    tg = np.concatenate([rng.integers(0, 256, size=(int(rng.integers(1, 200)), 20), dtype=np.uint8),
+                         s[rng.integers(0, s.shape[0], 6)], s[:1], s[-1:]])
+    count = int(rng.integers(1, 33))
+    got, cnt = ctx.cached_nodes(tg, count, acc)
+    for qi in range(tg.shape[0]):
+        want = O.cached_nodes(s, acc, tg[qi], count)
+        assert list(got[qi, : cnt[qi]]) == list(want), (seed, qi)
