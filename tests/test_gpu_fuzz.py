@@ -119,3 +119,35 @@ def test_cached_nodes_random(ctx, seed):
     for qi in range(tg.shape[0]):
         want = O.cached_nodes(s, acc, tg[qi], count)
         assert list(got[qi, : cnt[qi]]) == list(want), (seed, qi)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_prefix_shards_random(ctx, seed):
+    """Prefix shards (SURVEY 8(e) routing) of random streams: pbits 1..8, random pval and k;
+    the shard's own targets get the full set's answer in global stream indices, foreign
+    targets the shard's own top-k (K1, K4/K5 and K6 where they apply)."""
+    rng = np.random.default_rng(40_000 + seed)
+    n = int(rng.integers(1000, (1 << 20) + 1))
+    pbits = int(rng.integers(1, 9))
+    pval = int(rng.integers(0, 1 << pbits))
+    k = int(rng.integers(1, 33))
+    sd = 50 + seed
+    ids = O.gen_ids(sd, n)
+    top = lambda a: a[:, 0].astype(np.uint32) >> (8 - pbits)
+    ctx.gen_ids_prefix(sd, n, pbits, pval)
+    shard = ids[top(ids) == pval]
+    assert ctx.num_ids == shard.shape[0]
+    tg = rng.integers(0, 256, size=(int(rng.integers(1, 1500)), 20), dtype=np.uint8)
+    own = tg.copy()
+    own[:, 0] = (own[:, 0] & (0xFF >> pbits)) | (pval << (8 - pbits))
+    if shard.shape[0] >= k:   # the full set's top-k of an own-prefix target lies in the shard
+        want, wcnt = O.topk(ids, own, k)
+        for name, fn in (("scan", ctx.topk), ("index", ctx.index_topk), ("batch", ctx.batch_topk)):
+            got, cnt = fn(own, k)
+            assert np.array_equal(cnt, wcnt) and np.array_equal(got, want), (seed, name)
+    gl = np.nonzero(top(ids) == pval)[0].astype(np.uint32)
+    w2, c2 = O.topk(shard, tg, k)
+    w2 = np.where(w2 == 0xFFFFFFFF, w2, gl[np.minimum(w2, max(gl.size - 1, 0))] if gl.size else w2)
+    for name, fn in (("scan", ctx.topk), ("batch", ctx.batch_topk)):
+        got, cnt = fn(tg, k)
+        assert np.array_equal(cnt, c2) and np.array_equal(got, w2), (seed, name)
