@@ -151,3 +151,47 @@ def test_prefix_shards_random(ctx, seed):
     for name, fn in (("scan", ctx.topk), ("batch", ctx.batch_topk)):
         got, cnt = fn(tg, k)
         assert np.array_equal(cnt, c2) and np.array_equal(got, w2), (seed, name)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_record_shards_merge_random(ctx, seed):
+    """The broadcast route's building block at random shapes: the id set cut into 1..5 range
+    shards at random bounds (one context each, idx_base = the shard's start), every shard
+    answering the whole batch in record form (K6 or K1 alternately), K3 merging the shard
+    records: == one flat top-k of the whole set."""
+    import torch
+    import opendht_amd
+    rng = np.random.default_rng(50_000 + seed)
+    n = int(rng.integers(50, 300_001))
+    q = int(rng.integers(1, 1500))
+    k = int(rng.integers(1, 33))
+    ids = rng.integers(0, 256, size=(n, 20), dtype=np.uint8)
+    if seed % 2:
+        ids[: n // 3, :3] = ids[0, :3]
+    tg = rng.integers(0, 256, size=(q, 20), dtype=np.uint8)
+    nsh = int(rng.integers(1, 6))
+    bounds = [0] + sorted(int(x) for x in rng.integers(0, n + 1, nsh - 1)) + [n]
+    dev = torch.device("cuda", 0)
+    ts = (q + 63) // 64 * 64
+    tp = torch.zeros(5 * ts, dtype=torch.int32, device=dev)
+    L = opendht_amd.lib()
+    tb = torch.from_numpy(tg.reshape(-1)).to(dev)
+    torch.cuda.synchronize()
+    assert L.dhtgpu_pack_dev(tb.data_ptr(), q, tp.data_ptr(), ts, None) == 0
+    torch.cuda.synchronize()
+    rec = torch.empty((nsh, q, k, 6), dtype=torch.int32, device=dev)
+    for s in range(nsh):
+        c = opendht_amd.Context(0)
+        c.set_ids(np.ascontiguousarray(ids[bounds[s]:bounds[s + 1]]))
+        fn = c.batch_topk_dev if (s + seed) % 2 == 0 else c.topk_dev
+        fn(tp.data_ptr(), ts, q, k, None, None, rec[s].data_ptr(), bounds[s], c.stream)
+        torch.cuda.synchronize()
+        c.close()
+    out = torch.empty((q, k), dtype=torch.int32, device=dev)
+    cnt = torch.empty(q, dtype=torch.int32, device=dev)
+    assert L.dhtgpu_merge_dev(rec.data_ptr(), nsh, q, k, tp.data_ptr(), ts, k, out.data_ptr(), cnt.data_ptr(),
+                              None) == 0
+    torch.cuda.synchronize()
+    want, wcnt = O.topk(ids, tg, k)
+    assert np.array_equal(cnt.cpu().numpy().view(np.uint32), wcnt), seed
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want), seed
