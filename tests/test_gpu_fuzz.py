@@ -195,3 +195,21 @@ def test_record_shards_merge_random(ctx, seed):
     want, wcnt = O.topk(ids, tg, k)
     assert np.array_equal(cnt.cpu().numpy().view(np.uint32), wcnt), seed
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want), seed
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_subpartitioned_random(ctx, seed):
+    """Sets past one K6 plan at random shapes (n in (2^24, 2^26], q in [2^14, 2^17], random k):
+    the library sub-partitions them; whole batch == K1 scan, a sample == the oracle."""
+    rng = np.random.default_rng(60_000 + seed)
+    n = int(rng.integers((1 << 24) + 1, (1 << 26) + 1))
+    q = int(rng.integers(1 << 14, (1 << 17) + 1))
+    k = int(rng.integers(1, 33))
+    ctx.gen_ids(700 + seed, n)
+    tg = rng.integers(0, 256, size=(q, 20), dtype=np.uint8)
+    got, cnt = ctx.batch_topk(tg, k)
+    sc, scnt = ctx.topk(tg, k)
+    assert np.array_equal(cnt, scnt) and np.array_equal(got, sc), (seed, n, q, k)
+    rows = np.unique(np.r_[rng.integers(0, q, 6), [0, q - 1]])
+    want, wcnt = O.topk(O.gen_ids(700 + seed, n), tg[rows], k, threads=16)
+    assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
