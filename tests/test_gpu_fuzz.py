@@ -213,3 +213,25 @@ def test_subpartitioned_random(ctx, seed):
     rows = np.unique(np.r_[rng.integers(0, q, 6), [0, q - 1]])
     want, wcnt = O.topk(O.gen_ids(700 + seed, n), tg[rows], k, threads=16)
     assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
+
+
+def test_subpartition_overfull():
+    """2^25 ids (two prefix sub-partitions by the top bit) with 75 % of them moved into
+    sub-partition 0 (~2^24.6 ids: more than one K6 plan serves): the call must still be exact
+    (K6 == K1 scan on the whole batch, a sample == the oracle)."""
+    import opendht_amd
+    n, q, k = 1 << 25, 1 << 17, 8
+    ids = O.gen_ids(8080, n)
+    ids[: 3 * n // 4, 0] &= 0x7F
+    tg = O.gen_ids(8081, q)
+    c = opendht_amd.Context(0)
+    try:
+        c.set_ids(ids)
+        got, cnt = c.batch_topk(tg, k)
+        sc, scnt = c.topk(tg, k)
+        assert np.array_equal(cnt, scnt) and np.array_equal(got, sc)
+        rows = np.r_[np.arange(0, q, q // 8), [q - 1]]
+        want, wcnt = O.topk(ids, tg[rows], k, threads=16)
+        assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
+    finally:
+        c.close()
