@@ -235,3 +235,31 @@ def test_subpartition_overfull():
         assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_search_batch_random(ctx, seed):
+    """Crawl-model searches on random networks: size from 20 to 200,000 nodes, dead fraction up
+    to 0.7, clustered ids on odd seeds, random max_rounds; list for list vs the oracle model."""
+    rng = np.random.default_rng(70_000 + seed)
+    n = int(np.exp(rng.uniform(np.log(20), np.log(200_000))))
+    ids = rng.integers(0, 256, size=(n, 20), dtype=np.uint8)
+    if seed % 2:
+        ids[: n // 2, :2] = ids[0, :2]
+    ids = np.unique(ids, axis=0)
+    ids = ids[rng.permutation(ids.shape[0])]
+    n = ids.shape[0]
+    dead = (rng.random(n) < rng.uniform(0, 0.7)).astype(np.uint8) if seed % 4 else None
+    q = int(rng.integers(1, 600))
+    tg = rng.integers(0, 256, size=(q, 20), dtype=np.uint8)
+    hit = rng.random(q) < 0.2
+    tg[hit] = ids[rng.integers(0, n, int(hit.sum()))]
+    sr = rng.integers(0, n, q).astype(np.uint32)
+    rounds = int(rng.choice([1, 3, 8, 64]))
+    ctx.set_ids(np.ascontiguousarray(ids))
+    ctx.net_prepare(dead, table_seed=seed + 1)
+    got = ctx.search_batch(tg, sr, rounds)
+    want = O.search_batch(ids, dead, seed + 1, tg, sr, rounds)
+    for g, w, nm in zip(got, want, ["idx", "flags", "len", "rounds", "queries"]):
+        bad = np.nonzero((g != w).reshape(g.shape[0], -1).any(axis=1))[0]
+        assert bad.size == 0, f"seed {seed} {nm}: {bad.size} searches differ, first {bad[:5]}"
