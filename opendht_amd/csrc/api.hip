@@ -96,6 +96,10 @@ struct dhtgpu_ctx {
     };
     static constexpr int kBatchDepth = 4;
     BatchSlot bslot[kBatchDepth];
+    // fallback-list length of the context's last completed K6 call, written by F4 into mapped
+    // host memory (a hint read without any sync: it sizes the next call's fallback-scan grid)
+    uint32_t* fb_hint = nullptr;
+    uint32_t* fb_hint_dev = nullptr;
     int bnext = 0, blast = 0;
     bool last_small = false;   // the last K6-API call took the small-batch path
     uint64_t last_n = 0;       // ... else its plan: largest sub-partition, planned targets, sub-partitions
@@ -214,6 +218,7 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
     for (auto& b : c->bslot)
         for (DevBuf* d : {&b.ws, &b.out_idx, &b.out_cnt, &b.sws}) d->release();
     c->invalidate_subs();
+    if (c->fb_hint) (void)hipHostFree(c->fb_hint);
     for (DevBuf* b : {&c->stamps, &c->w0s, &c->sview.planes, &c->sview.perm,
                       &c->cache.planes, &c->cache.perm, &c->cache_in, &c->sort_scratch, &c->cache_acc, &c->srch})
         b->release();
@@ -580,6 +585,17 @@ static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hi
         b.desc_sig = 0;
     }
     DHT_TRY(b.ws.ensure(need));
+    if (!c->fb_hint) {
+        void* h = nullptr;
+        DHT_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped));
+        c->fb_hint = static_cast<uint32_t*>(h);
+        *c->fb_hint = 1u;   // unknown: assume a fallback list (full-size grid)
+        void* d = nullptr;
+        DHT_TRY(hipHostGetDevicePointer(&d, h, 0));
+        c->fb_hint_dev = static_cast<uint32_t*>(d);
+    }
+    bc.fb_hint = c->fb_hint;
+    bc.fb_hint_dev = c->fb_hint_dev;
     if (b.zeroed < head) DHT_TRY(hipMemsetAsync(b.ws.p, 0, head, s));
     b.zeroed = 0;   // re-established below once every launch went through
     if (bc.dbg & 256) {

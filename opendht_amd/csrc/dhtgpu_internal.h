@@ -122,6 +122,8 @@ struct BatchCall {
     int num_cus;
     uint32_t dbg;                          // DHTGPU_DBG experiment switches (0 in production)
     uint32_t f2_seg;                       // F2 sparse-mode segment override in ids (0: the plan's)
+    const volatile uint32_t* fb_hint;      // nullable: the slot's last fallback-list length (mapped host memory)
+    uint32_t* fb_hint_dev;                 // its device address (F4 writes it)
     unsigned long long* stamps;            // dbg & 256: phase stamps [2 * 8192 * 16]
     hipEvent_t* ev;                        // nullable: 8 events around F1..F4
 };
