@@ -37,20 +37,68 @@ Beside the headline (`value`) the line carries, measured in the same run:
                   splits it into prefix sub-partitions) -- its w0 planes (537 MB) exceed L3
   cfg4 / cfg5     classification of 10^8 ids; iterative searches over 5*10^7 nodes
   cfg3 (N > 1)    BASELINE cfg 3 itself over the ranks: 10^9 ids, 2^20 targets, both routes
-  cpu_baseline    the oracle port on the host cores (rank 0, N = 1), 1 core and 16 threads
+  cpu_baseline    the oracle port on the host cores (rank 0, N = 1): every host CPU and 1 core;
+                  cfg 1 (findClosestNodes on an onNewNode-grown table), cfg 2 (partial_sort),
+                  cfg 4 (findBucket + commonBits), getCachedNodes
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import bisect
 import ctypes
 import json
 import os
 import platform
+import socket
 import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+
+def launcher_cmd(gpus, argv):
+    """`python bench.py --gpus N` (N > 1) started as ONE process: the command that runs it as N
+    ranks, one per GPU (torch.distributed.run, 127.0.0.1 rendezvous on a free port).  Built and
+    started before anything touches the GPU (this process never initialises HIP)."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def maybe_launch(argv):
+    """--gpus N > 1 without a torch.distributed environment: start the N-rank job as a child
+    process and return its exit code (None: this process is a rank, or N == 1).  --dry-run
+    prints what would run (the launcher command, or this rank's identity) and exits;
+    --dry-run-ranks starts the N ranks for real and each prints its identity (no GPU)."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    pre.add_argument("--dry-run", action="store_true")
+    pre.add_argument("--dry-run-ranks", action="store_true")
+    a, _ = pre.parse_known_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if a.gpus > 1 and env_world is None:
+        cmd = launcher_cmd(a.gpus, argv)
+        if a.dry_run and not a.dry_run_ranks:
+            print(json.dumps({"mode": "launcher", "gpus": a.gpus, "cmd": cmd,
+                              "env": {k: os.environ.get(k) for k in ("HSA_ENABLE_IPC_MODE_LEGACY",)}}))
+            return 0
+        print(f"[bench] --gpus {a.gpus}: launching {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+        return subprocess.call(cmd)
+    if a.dry_run or a.dry_run_ranks:
+        print(json.dumps({"mode": "rank" if env_world is not None else "single", "gpus": a.gpus,
+                          "world_size": int(env_world or 1), "rank": int(os.environ.get("RANK", "0")),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}))
+        return 0
+    return None
+
+
+if __name__ == "__main__":
+    _rc = maybe_launch(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
 # Hardware queues: HIP's default (4 per process, shared round-robin by the streams) is kept.
 # Measured: 8 queues leave the cfg-2 step unchanged (40.6-41.0 vs 40.8-40.9 us) and make the
 # sub-partitioned cfg-3 shard 1.7x slower (0.60 vs 0.35 ms per call with two calls in flight).
@@ -77,12 +125,16 @@ HBM_PEAK_GBS = 8000.0
 # 64-bit lane; both fractions are reported (the packed prefilter is an algorithmic win).
 OPS_PER_PAIR = 1.0
 SURVEY_OPS_PER_PAIR = 3.0
-PMC_FILE = "profiles/r02/pmc_traffic.json"
+PMC_FILE = "profiles/r03/pmc_traffic.json"
 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); N > 1 outside torch.distributed.run re-launches itself under it")
+    ap.add_argument("--dry-run", action="store_true", help="print the launch plan and exit (no GPU)")
+    ap.add_argument("--dry-run-ranks", action="store_true",
+                    help="launch the ranks for real; each prints its identity and exits (no GPU)")
     ap.add_argument("--steps", type=int, default=1000)   # ~40 ms timed: steady state, not ramp-up
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--n", type=int, default=1 << 24, help="node ids (per GPU with weak scaling)")
@@ -105,8 +157,10 @@ def parse():
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="prefix route only: run rank --simulate-rank of a world of this size on one GPU")
     ap.add_argument("--simulate-rank", type=int, default=0)
-    ap.add_argument("--cpu-targets", type=int, default=256, help="cpu_baseline sample (targets, 16 threads)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-targets", type=int, default=256, help="cpu_baseline sample (targets, all host threads)")
+    ap.add_argument("--cpu-threads", type=int, default=usable_cpus(),
+                    help="cpu_baseline threads (default: every CPU this process may use -- its affinity set capped "
+                         "by the cgroup CPU quota; the single-core figures are reported too)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra legs (small batch, cfg 1/3/4/5)")
     ap.add_argument("--no-scan", action="store_true", help="skip the reference K1 scan measurement")
@@ -153,6 +207,31 @@ def cpu_model():
     except OSError:
         pass
     return platform.processor() or "unknown"
+
+
+def usable_cpus():
+    """CPUs this process can keep busy: its affinity set, capped by the cgroup CPU quota (a GPU
+    box's job gets 16 CPUs of time on a 256-CPU host: 256 threads there only time-slice)."""
+    sh = cpu_share()
+    n = sh.get("affinity_cpus") or os.cpu_count() or 1
+    q = sh.get("cgroup_cpu_quota")
+    return max(1, min(n, int(q + 0.5))) if q else n
+
+
+def cpu_share():
+    """The CPUs this process may actually run on: its affinity set and the cgroup CPU quota
+    (a GPU box shares the host; os.cpu_count() reports the whole machine)."""
+    out = {}
+    try:
+        out["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        out["cgroup_cpu_quota"] = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return out
 
 
 class EvSets:
@@ -203,30 +282,58 @@ def k6_kernels(ms, n, q, k, surv):
             "k_f3_answer": (ms[2], 8 * surv + q * (8 + 16 + 4 * k + 4)), "k_f4_fallback": (ms[3], 0)}
 
 
-def synthetic_table(myid, depth, per_bucket, rng):
-    """A RoutingTable-shaped snapshot (src/routing_table.cpp: contiguous lexicographic buckets
-    split along myid's path, each holding per_bucket nodes): the sibling subtree of myid at
-    every level < depth, plus myid's own depth-`depth` subtree, sorted by Bucket::first."""
+def grow_table(myid, ids):
+    """The RoutingTable a node with id `myid` holds after learning `ids` in order: onNewNode
+    (src/routing_table.cpp:204-262) with every node good -- insert into findBucket's bucket
+    (:153-166) while it holds < TARGET_NODES = 8, else split it (:169-200, depth :100-107) if it
+    contains myid and retry, else drop the node.  Node order inside a bucket follows the
+    reference's std::list splices (emplace_front on insert, splice-to-front on split).  The
+    bench's workload generator (host logic on the input side); returns the snapshot the C ABI
+    takes: bucket firsts (nb, 20), bucket offsets (nb + 1), node ids (m, 20)."""
     me = int.from_bytes(bytes(myid), "big")
-    ranges = []
-    for lvl in range(depth + 1):
-        if lvl < depth:
-            bit = (me >> (159 - lvl)) & 1
-            prefix = ((me >> (160 - lvl)) << 1 | (1 - bit)) if lvl else (1 - bit)
-            plen = lvl + 1
-        else:
-            prefix, plen = me >> (160 - depth), depth
-        ranges.append((prefix << (160 - plen), plen))
-    ranges.sort()
-    firsts, ids, off = [], [], [0]
-    for first, plen in ranges:
-        firsts.append(first.to_bytes(20, "big"))
-        for _ in range(per_bucket):
-            low = int.from_bytes(rng.bytes(20), "big") & ((1 << (160 - plen)) - 1)
-            ids.append((first | low).to_bytes(20, "big"))
-        off.append(len(ids))
-    as_u8 = lambda v: np.frombuffer(b"".join(v), dtype=np.uint8).reshape(-1, 20).copy()
-    return as_u8(firsts), np.array(off, np.uint32), as_u8(ids)
+    firsts, nodes = [0], [[]]
+    lowbit = lambda x: 160 - (x & -x).bit_length() if x else -1      # infohash.h:132-143
+    for row in ids:
+        x = int.from_bytes(bytes(row), "big")
+        while True:
+            b = bisect.bisect_right(firsts, x) - 1
+            if x in nodes[b]:
+                break
+            if len(nodes[b]) < 8:
+                nodes[b].insert(0, x)
+                break
+            nxt = firsts[b + 1] if b + 1 < len(firsts) else None
+            if not (firsts[b] <= me and (nxt is None or me < nxt)):
+                break                                   # not my bucket: the node is cached away
+            bit = max(lowbit(firsts[b]), lowbit(nxt) if nxt is not None else -1) + 1
+            if bit >= 160:
+                break
+            firsts.insert(b + 1, firsts[b] | (1 << (159 - bit)))
+            moved, nodes[b] = nodes[b], []
+            nodes.insert(b + 1, [])
+            for v in moved:                              # splice each to the front of its bucket
+                nodes[bisect.bisect_right(firsts, v) - 1].insert(0, v)
+    off = np.zeros(len(firsts) + 1, np.uint32)
+    off[1:] = np.cumsum([len(v) for v in nodes])
+    to_u8 = lambda vals: np.frombuffer(b"".join(v.to_bytes(20, "big") for v in vals) or b"",
+                                       dtype=np.uint8).reshape(-1, 20).copy()
+    return to_u8(firsts), off, to_u8([v for bn in nodes for v in bn])
+
+
+def cfg1_table(seed):
+    """BASELINE cfg 1's table: 10,000 random ids learned by one node."""
+    rng = np.random.default_rng(seed)
+    myid = np.frombuffer(rng.bytes(20), dtype=np.uint8).copy()
+    ids = np.frombuffer(rng.bytes(20 * 10000), dtype=np.uint8).reshape(-1, 20)
+    return (myid,) + grow_table(myid, ids)
+
+
+def cfg4_firsts(seed):
+    """The bucket firsts of a table grown from 10^5 random ids (SURVEY 8(d) cfg 4)."""
+    rng = np.random.default_rng(seed)
+    myid = np.frombuffer(rng.bytes(20), dtype=np.uint8).copy()
+    firsts, _, _ = grow_table(myid, np.frombuffer(rng.bytes(20 * 100000), dtype=np.uint8).reshape(-1, 20))
+    return myid, firsts
 
 
 def l3_evict(buf):
@@ -264,6 +371,10 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if use_dist and not a.rehearse_one_gpu:
+        world = dist.get_world_size()          # the RCCL communicator's own count
+    if world != a.gpus and not a.rehearse_one_gpu:
+        progress(f"note: --gpus {a.gpus} but the process group has {world} ranks; n_gpus reports {world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     tstream = torch.cuda.Stream(dev)              # every kernel and event of the bench runs here
@@ -405,6 +516,20 @@ def main():
                 "contract_floor_ms": (n_local * 20 + q_local * 20 + q_local * a.k * 4) / HBM_PEAK_GBS / 1e6}
         extra.update({"survivors": surv, "survivor_frac": surv / max(n_local, 1), "fallback_targets": n_fb,
                       "wave_path_targets": n_slow})
+        if use_dist:
+            # aggregate over the ranks: every rank's F2 bytes / the slowest rank's F2 time, against
+            # world x the one-GPU peak (each rank streams its own shard from its own HBM)
+            agg = torch.tensor([float(dom_bytes), float(step_bytes)], dtype=torch.float64, device=dev)
+            slow = torch.tensor([dom_ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(agg, op=dist.ReduceOp.SUM)
+            dist.all_reduce(slow, op=dist.ReduceOp.MAX)
+            ab, sb, sm = float(agg[0].item()), float(agg[1].item()), float(slow.item())
+            roof["aggregate"] = {"ranks": world, "alg_bytes_all_ranks": ab, "slowest_rank_kernel_ms": sm,
+                                 "achieved": ab / (sm * 1e-3) / 1e9, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                                 "frac": ab / (sm * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
+                                 "step_frac": sb / (ms_per_step * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
+                                 "how": "sum of the ranks' F2 algorithmic bytes / the slowest rank's F2 time / "
+                                        "(ranks x 8 TB/s); step_frac: all four kernels' bytes over the timed step"}
         # the same kernel with the Infinity Cache evicted before every call (HBM-bound figure)
         ebuf = torch.zeros(128 << 20, dtype=torch.int32, device=dev)
         cold = EvSets(8, tstream)
@@ -493,6 +618,7 @@ def main():
             "value": (a.q_total if not a.simulate_world else q_local) / (ms_per_step * 1e-3),
             "unit": "queries/s",
             "n_gpus": world,
+            "dist_world_size": dist.get_world_size() if use_dist else 1,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": ms_per_step,
@@ -550,8 +676,8 @@ def small_batch_leg(ctx, tp, ts, n, k, stream, tstream, dev):
     """Q = 1 / 8 / 32 / 64 targets over the same id set: latency per call and the bytes the call
     has to stream (4 B/id of the w0 plane; SURVEY's contract counts 20 B/id).  The library's
     batch entry point takes the small-batch path (KS: S1 one pass over w0, S2 one workgroup per
-    target prefix, F4 the K1 scan for short subtrees -- an empty list here) for q <= 64; K1 is
-    the plain scan beside it."""
+    target prefix beside the scan roles that answer short subtrees -- none here) for q <= 64; K1
+    is the plain scan beside it."""
     out = {}
     oi = torch.empty((64, k), dtype=torch.int32, device=dev)
     oc = torch.empty(64, dtype=torch.int32, device=dev)
@@ -568,7 +694,7 @@ def small_batch_leg(ctx, tp, ts, n, k, stream, tstream, dev):
         ev.arm(ctx)
         ctx.batch_topk_dev(tp.data_ptr(), ts, q, k, oi.data_ptr(), oc.data_ptr(), None, 0, stream)
         kms = ev.mean_ms()
-        row["kernels_ms"] = {"k_s1_filter": kms[1], "k_s2_answer": kms[2], "k_f4 (fallback scan, empty)": kms[3]}
+        row["kernels_ms"] = {"k_s1_filter": kms[1], "k_s2_answer (prefix answers + fallback scan roles)": kms[2]}
         row["s1_frac"] = 4 * n / (kms[1] * 1e-3) / 1e9 / HBM_PEAK_GBS
         out[f"q{q}"] = row
     out["note"] = ("id set L3-resident (the cfg-2 set); w0_frac = the 4 B/id w0 stream over the whole call's "
@@ -580,11 +706,9 @@ def find_closest_leg(ctx, a, dev):
     """RoutingTable::findClosestNodes (dhtgpu_find_closest, K1r) on a cfg-1-shaped table: one
     target per call (the reference's call pattern; host pointers, PCIe included) and one
     65,536-target batch."""
-    rng = np.random.default_rng(a.seed)
-    myid = np.frombuffer(rng.bytes(20), dtype=np.uint8).copy()
-    firsts, off, nodes = synthetic_table(myid, 11, 8, rng)
+    myid, firsts, off, nodes = cfg1_table(a.seed)
     good = np.ones(nodes.shape[0], np.uint8)
-    tg = np.frombuffer(rng.bytes(20 * 65536), dtype=np.uint8).reshape(-1, 20).copy()
+    tg = np.frombuffer(np.random.default_rng(a.seed + 1).bytes(20 * 65536), dtype=np.uint8).reshape(-1, 20).copy()
     ctx.find_closest(firsts, off, nodes, good, tg[:1], 8)
     t0 = time.perf_counter()
     for i in range(200):
@@ -595,7 +719,7 @@ def find_closest_leg(ctx, a, dev):
     for _ in range(5):
         ctx.find_closest(firsts, off, nodes, good, tg, 8)
     batch = (time.perf_counter() - t0) / 5
-    return {"table": f"{firsts.shape[0]} buckets, {nodes.shape[0]} nodes (synthetic, RoutingTable shape)",
+    return {"table": f"{firsts.shape[0]} buckets, {nodes.shape[0]} nodes: onNewNode-grown from 10,000 random ids (cfg 1)",
             "single_target_us": single * 1e6, "batch_65536_ms": batch * 1e3, "batch_qps": 65536 / batch,
             "note": "host API per call: snapshot + targets uploaded, results downloaded (PCIe included)"}
 
@@ -669,11 +793,9 @@ def cfg3_shard_leg(a, L, dev, stream, tstream):
 
 def cfg4_leg(a, L, dev, stream, tstream):
     """BASELINE cfg 4: findBucket + commonBits classification of 10^8 ids vs a local id (K2),
-    bucket firsts of a table grown from ~10^5 ids; 21 B/id algorithmic (20 in + 1 out)."""
+    bucket firsts of a table grown by onNewNode from 10^5 ids; 21 B/id algorithmic (20 in + 1 out)."""
     n = 100_000_000
-    rng = np.random.default_rng(a.seed + 5)
-    myid = np.frombuffer(rng.bytes(20), dtype=np.uint8).copy()
-    firsts, _, _ = synthetic_table(myid, 14, 1, rng)
+    myid, firsts = cfg4_firsts(a.seed + 5)
     c = opendht_amd.Context(dev.index)
     try:
         c.gen_ids(a.seed + 6, n)
@@ -834,8 +956,9 @@ def cfg3_multi_leg(a, L, dev, stream, tstream, world, rank):
 
 def cpu_baseline(O, ids, tg, a):
     """Oracle port on the host cores (rank 0, N = 1): std::partial_sort(xorCmp) over the cfg-2
-    set on a bounded target sample at 16 threads and on 1 core, plus the reference's own
-    RoutingTable::findClosestNodes call pattern (cfg 1) and NodeCache::getCachedNodes."""
+    set on a bounded target sample at --cpu-threads (default: every host CPU) and on 1 core,
+    plus the reference's own RoutingTable::findClosestNodes call pattern (cfg 1), the cfg-4
+    findBucket + commonBits loop and NodeCache::getCachedNodes."""
     t0 = time.perf_counter()
     want, _ = O.topk(ids, tg, a.k, threads=a.cpu_threads)
     dt = time.perf_counter() - t0
@@ -846,8 +969,16 @@ def cpu_baseline(O, ids, tg, a):
     cb = {"value": tg.shape[0] / dt, "unit": "queries/s", "cores": a.cpu_threads, "kind": "port",
           "sample": f"{tg.shape[0]} targets x {ids.shape[0]} ids, k={a.k}, std::partial_sort(xorCmp) per target, "
                     f"{a.cpu_threads} threads, {dt:.2f} s wall",
-          "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "compiler": "g++ -O2 (the reference's Release)",
+          "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), **cpu_share(),
+          "compiler": "g++ -O2 (the reference's Release)",
           "one_core": {"value": m1 / dt1, "unit": "queries/s", "sample": f"{m1} targets, {dt1:.2f} s"}}
+    if cb["host_cpus"] and cb["host_cpus"] > a.cpu_threads:
+        # the job may use a.cpu_threads CPUs of the host's host_cpus (cgroup quota): the whole
+        # host's rate is not measurable here; a linear scaling in cores is its upper bound
+        cb["whole_host_upper_bound"] = {
+            "value": cb["value"] * cb["host_cpus"] / a.cpu_threads, "unit": "queries/s", "cores": cb["host_cpus"],
+            "basis": f"measured {a.cpu_threads}-CPU rate x {cb['host_cpus']}/{a.cpu_threads} (linear in cores: an upper "
+                     f"bound -- std::partial_sort over the 335 MB set is memory-bound at a few threads, SURVEY 8(d))"}
     # the same port built with g++ -O3 -march=native on this host
     try:
         with O.native():
@@ -862,12 +993,15 @@ def cpu_baseline(O, ids, tg, a):
                                  "same_results": bool(np.array_equal(got_n, want))}
     except (OSError, subprocess.CalledProcessError) as e:
         cb["O3_march_native"] = {"error": str(e)[:200]}
-    # cfg 1: findClosestNodes per target over a RoutingTable-shaped snapshot
+    # cfg 1: findClosestNodes per target over the onNewNode-grown 10k-id table; the oracle grows
+    # the same table from the same ids (its restated onNewNode) and must agree
+    myid, firsts, off, nodes = cfg1_table(a.seed)
     rng = np.random.default_rng(a.seed)
-    myid = np.frombuffer(rng.bytes(20), dtype=np.uint8).copy()
-    firsts, off, nodes = synthetic_table(myid, 11, 8, rng)
+    rng.bytes(20)
+    of, oo, on = O.Table(myid).grow(np.frombuffer(rng.bytes(20 * 10000), dtype=np.uint8).reshape(-1, 20)).export()
+    same_table = bool(np.array_equal(of, firsts) and np.array_equal(oo, off) and np.array_equal(on, nodes))
     good = np.ones(nodes.shape[0], np.uint8)
-    tq = np.frombuffer(rng.bytes(20 * 1_000_000), dtype=np.uint8).reshape(-1, 20).copy()
+    tq = np.frombuffer(np.random.default_rng(a.seed + 1).bytes(20 * 1_000_000), dtype=np.uint8).reshape(-1, 20).copy()
     fc = {}
     for th in (1, a.cpu_threads):
         O.find_closest_batch(firsts, off, nodes, good, tq[:1000], 8, threads=th)
@@ -875,8 +1009,24 @@ def cpu_baseline(O, ids, tg, a):
         O.find_closest_batch(firsts, off, nodes, good, tq, 8, threads=th)
         d = time.perf_counter() - t0
         fc[f"threads_{th}"] = {"queries_per_s": tq.shape[0] / d, "us_per_query_per_core": d * th / tq.shape[0] * 1e6}
-    cb["cfg1_find_closest"] = {"table": f"{firsts.shape[0]} buckets, {nodes.shape[0]} nodes", "targets": tq.shape[0],
-                               **fc, "kind": "port (RoutingTable::findClosestNodes restated over a flat snapshot)"}
+    cb["cfg1_find_closest"] = {"table": f"{firsts.shape[0]} buckets, {nodes.shape[0]} nodes, onNewNode-grown from "
+                                        f"10,000 ids", "table_equals_oracle_onNewNode": same_table,
+                               "targets": tq.shape[0], **fc,
+                               "kind": "port (RoutingTable::findClosestNodes, src/routing_table.cpp:110-150, restated "
+                                       "over the table snapshot)"}
+    # cfg 4: findBucket + commonBits per id (src/routing_table.cpp:153-166, infohash.h:154-176)
+    m4, f4 = cfg4_firsts(a.seed + 5)
+    ids4 = O.gen_ids(a.seed + 6, 20_000_000)
+    c4 = {}
+    for th, n4 in ((1, 2_000_000), (a.cpu_threads, ids4.shape[0])):
+        O.classify(f4, m4, ids4[:100_000], threads=th)
+        t0 = time.perf_counter()
+        O.classify(f4, m4, ids4[:n4], threads=th)
+        d = time.perf_counter() - t0
+        c4[f"threads_{th}"] = {"ids_per_s": n4 / d, "ns_per_id_per_core": d * th / n4 * 1e9, "ids": n4}
+    cb["cfg4_classify"] = {"table": f"{f4.shape[0]} buckets (onNewNode-grown from 10^5 ids)", **c4,
+                           "kind": "port (findBucket linear walk + commonBits, per id)"}
+    del ids4
     # NodeCache::getCachedNodes over a 10^6-node cache
     cache = O.gen_ids(a.seed + 9, 1_000_000)
     cache = cache[np.lexsort(cache.T[::-1])]

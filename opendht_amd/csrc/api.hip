@@ -91,6 +91,7 @@ struct dhtgpu_ctx {
         size_t zeroed = 0;      // leading workspace bytes known zero (the last call's clean head)
         uint64_t desc_sig = 0;  // sub-partition descriptors held by the workspace (launch_batch_topk)
         bool sclean = false;
+        uint32_t spar = 0;      // small-batch path: the counter set its next call uses
         hipEvent_t done = nullptr;
         hipStream_t last = nullptr;
     };
@@ -130,6 +131,7 @@ struct dhtgpu_ctx {
     // diagnostics (DHTGPU_DBG, read once at creation; phase stamps per context)
     uint32_t dbg = 0;
     uint32_t f2_seg = 0;          // DHTGPU_F2SEG: F2 sparse-mode segment override (ids; 0 = plan's)
+    int32_t f3_spec = -1;         // DHTGPU_F3SPEC: F3 speculative slots per set (-1 = plan's, 0 = exact gather)
     hipEvent_t next_ev[8] = {};   // dhtgpu_batch_events: the next K6 call records its kernels here
     bool has_next_ev = false;
     DevBuf stamps;
@@ -137,6 +139,7 @@ struct dhtgpu_ctx {
     hipError_t bind() { return hipSetDevice(device); }
     void invalidate_subs() {
         subs_valid = false;
+        if (fb_hint) *fb_hint = 1u;   // a new set or split: the next call's list length is unknown
         for (auto& sp : subs)
             for (DevBuf* b : {&sp.planes, &sp.map, &sp.gmap, &sp.w0s}) b->release();
         subs.clear();
@@ -191,9 +194,21 @@ int dhtgpu_ctx_create(int device, dhtgpu_ctx** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (const char* d = getenv("DHTGPU_DBG")) c->dbg = (uint32_t)atoi(d);
     if (const char* d = getenv("DHTGPU_F2SEG")) c->f2_seg = (uint32_t)atoi(d);
+    if (const char* d = getenv("DHTGPU_F3SPEC")) c->f3_spec = (int32_t)atoi(d);
     if (e == hipSuccess) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+    }
+    if (e == hipSuccess) {   // F4's fallback-list hint: mapped, coherent host memory (F4 stores it system-scope)
+        void* h = nullptr;
+        e = hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) {
+            c->fb_hint = static_cast<uint32_t*>(h);
+            *c->fb_hint = 1u;   // unknown: assume a fallback list (full-size grid)
+            void* d = nullptr;
+            e = hipHostGetDevicePointer(&d, h, 0);
+            c->fb_hint_dev = static_cast<uint32_t*>(d);
+        }
     }
     if (e != hipSuccess) {
         dhtgpu_ctx_destroy(c);
@@ -585,15 +600,6 @@ static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hi
         b.desc_sig = 0;
     }
     DHT_TRY(b.ws.ensure(need));
-    if (!c->fb_hint) {
-        void* h = nullptr;
-        DHT_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped));
-        c->fb_hint = static_cast<uint32_t*>(h);
-        *c->fb_hint = 1u;   // unknown: assume a fallback list (full-size grid)
-        void* d = nullptr;
-        DHT_TRY(hipHostGetDevicePointer(&d, h, 0));
-        c->fb_hint_dev = static_cast<uint32_t*>(d);
-    }
     bc.fb_hint = c->fb_hint;
     bc.fb_hint_dev = c->fb_hint_dev;
     if (b.zeroed < head) DHT_TRY(hipMemsetAsync(b.ws.p, 0, head, s));
@@ -712,6 +718,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     bc.num_cus = c->num_cus;
     bc.dbg = c->dbg;
     bc.f2_seg = c->f2_seg;
+    bc.f3_spec = c->f3_spec;
     bc.ev = ev;
     bc.subs = specs.data();
     bc.nsub = S;
@@ -740,7 +747,10 @@ static int small_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     }
     if (b.sws.cap < small_bytes()) b.sclean = false;
     DHT_TRY(b.sws.ensure(small_bytes()));
-    if (!b.sclean) DHT_TRY(hipMemsetAsync(b.sws.p, 0, small_bytes(), s));
+    if (!b.sclean) {
+        DHT_TRY(hipMemsetAsync(b.sws.p, 0, small_bytes(), s));
+        b.spar = 0;
+    }
     b.sclean = true;   // the kernels leave it zero
     const uint32_t* gidx = c->out_map();
     uint32_t* li = out_idx;
@@ -768,7 +778,8 @@ static int small_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     bc.out_cnt = lc;
     bc.num_cus = c->num_cus;
     bc.ev = ev;
-    DHT_TRY(launch_small_topk(bc, b.sws.p, s));
+    DHT_TRY(launch_small_topk(bc, b.sws.p, b.spar, s));
+    b.spar ^= 1u;
     b.last = s;
     c->last_small = true;
     if (out_rec)
@@ -823,6 +834,7 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     bc.num_cus = c->num_cus;
     bc.dbg = c->dbg;
     bc.f2_seg = c->f2_seg;
+    bc.f3_spec = c->f3_spec;
     bc.ev = ev;
     int r = batch_slot_run(c, si, bc, s, ev);
     if (r) return r;

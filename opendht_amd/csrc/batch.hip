@@ -579,6 +579,8 @@ struct F3Args {
     const SubDesc* subs; uint32_t np_sub;   // sub-partitions, partitions per sub-partition
     uint32_t dbg;
     unsigned long long* stamps;          // dbg & 256: per-block phase timestamps [np][16]
+    uint32_t spec;                       // speculative gather: slots per bucket set loaded with the counts
+                                         // (<= kF3Cap / kSets; 0: counts first, then the exact gather)
 };
 
 // (w0 distance, w1 distance, index) order; words 2..4 are read only when both distances tie
@@ -726,11 +728,12 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     for (uint32_t i = threadIdx.x; i <= nsub; i += kF3Threads) sofs[i] = 0;
     if (threadIdx.x == 0) ntie[0] = ntie[1] = 0;
     // survivors of this partition in each of the kSets bucket sets (F2), its targets (F1), and
-    // -- speculatively, in the same round trip -- the first kSpec slots of every set (entry
+    // -- speculatively, in the same round trip -- the first a.spec slots of every set (entry
     // u * kF3Threads + tid = slot (u & 1) * kF3Threads + tid of set u >> 1) and the first
-    // chunk of targets; slots past a set's count are dropped below
-    constexpr uint32_t kSpec = kF3Cap / kSets;
-    static_assert(kSpec == 2 * kF3Threads && kF3Per == 2 * kSets, "speculative gather layout");
+    // chunk of targets; slots past a set's count are dropped below.  a.spec is the plan's
+    // expected per-set count plus a few sigma (the host sizes it): the slots past it are not
+    // loaded at all, so a partition's speculative bytes follow its survivors
+    static_assert(kF3Cap / kSets == 2 * kF3Threads && kF3Per == 2 * kSets, "speculative gather layout");
     uint32_t ms[kSets];
 #pragma unroll
     for (uint32_t x = 0; x < kSets; ++x) ms[x] = a.pcount[x * np + p];
@@ -739,10 +742,12 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     const uint2 tfirst = tsrc[threadIdx.x < a.tcap ? threadIdx.x : 0u];
     uint2 e[kF3Per];
     const uint2* pb = a.pbuf + (uint64_t)p * kSets * a.pcap;
+    const uint32_t spec = a.spec < a.pcap ? a.spec : a.pcap;
 #pragma unroll
     for (uint32_t u = 0; u < kF3Per; ++u) {
         const uint32_t pos = (u & 1) * kF3Threads + threadIdx.x;
-        e[u] = pb[(u >> 1) * a.pcap + (pos < a.pcap ? pos : 0u)];
+        e[u] = make_uint2(0u, 0u);
+        if (pos < spec) e[u] = pb[(u >> 1) * a.pcap + pos];
     }
     const uint32_t mt = mt0 < a.tcap ? mt0 : a.tcap;
     if (p == 0) {   // spilled targets (foreign, or a full bucket) join the fallback list
@@ -758,14 +763,14 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     }
     sync_lds();   // every thread has read the counts
     // set offsets inside the partition (soff[x] = entries of sets < x); over = a set overflowed;
-    // spec = every set fits its speculative slots
+    // spec_ok = every set fits its speculative slots
     uint32_t soff[kSets + 1];
-    bool over = false, spec = true;
+    bool over = false, spec_ok = true;
     soff[0] = 0;
 #pragma unroll
     for (uint32_t x = 0; x < kSets; ++x) {
         over = over || ms[x] > a.pcap;
-        spec = spec && ms[x] <= kSpec;
+        spec_ok = spec_ok && ms[x] <= spec;
         soff[x + 1] = soff[x] + (ms[x] < a.pcap ? ms[x] : a.pcap);
     }
     const uint32_t m = soff[kSets];
@@ -795,13 +800,14 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     const uint32_t sq_sh = 32 - a.Lq;                            // sub-prefix = bfe(w, 32 - Lq, Lq - b1)
     // valid[u]: slot u holds one of the partition's entries
     uint32_t valid = 0;
-    if (spec) {
+    if (spec_ok) {
 #pragma unroll
         for (uint32_t u = 0; u < kF3Per; ++u)
             valid |= (uint32_t)((u & 1) * kF3Threads + threadIdx.x < ms[u >> 1]) << u;
     } else {
-        // a set past its speculative slots (not on uniform ids): gather the partition
-        // exactly, entry j from set x (soff[x] <= j < soff[x + 1]) at slot j - soff[x]
+        // a set past its speculative slots (rare with the planned spec; always with spec 0):
+        // gather the partition exactly, entry j from set x (soff[x] <= j < soff[x + 1]) at slot
+        // j - soff[x] -- only the m entries are loaded
 #pragma unroll
         for (uint32_t u = 0; u < kF3Per; ++u) {
             const uint32_t j = u * kF3Threads + threadIdx.x;
@@ -809,7 +815,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
 #pragma unroll
             for (uint32_t y = 1; y < kSets; ++y)
                 if (j >= soff[y]) { x = y; base = soff[y]; }
-            e[u] = pb[x * a.pcap + (j < m ? j - base : 0u)];
+            if (j < m) e[u] = pb[x * a.pcap + j - base];
             valid |= (uint32_t)(j < m) << u;
         }
     }
@@ -1106,6 +1112,74 @@ __device__ void fb_merge(const F3Args& a, const FbArgs& f, uint32_t g, uint32_t 
     }
 }
 
+// The fallback list's K1 scan (a.fb_list[0, cnt)): roles of target groups x id-range splits over
+// f.nfb workgroups, this one being workgroup `blk` of them (k_f4, and KS's scan-role workgroups)
+template <int K>
+__device__ __forceinline__ void fb_list_scan(const F3Args& a, const FbArgs& f, uint32_t cnt, uint32_t blk, uint32_t* lds,
+                             uint32_t* last) {
+    const uint32_t wv = threadIdx.x >> 6;
+    // Sub-partitioned call with a short list (on uniform ids: the rare target whose level-Lm
+    // subtree holds < k ids): every target is its own group and scans only its own
+    // sub-partition -- which holds its top-k when it holds >= k ids -- over S splits (a scan of
+    // the whole set cost a single target ~3 ms at 2^28 ids).  Up to one target per
+    // sub-partition: past that, one scan of the whole set for all of them reads less.  (One
+    // scan_run call site for both forms: a second inlined copy doubled this kernel's VGPRs.)
+    const bool single = a.np_sub != f.np_ties && cnt <= min(kFbSingle, f.np_ties / a.np_sub);
+    const uint32_t gsize = single ? 1u : kFbGroup;
+    const uint32_t groups = (cnt + gsize - 1) / gsize;
+    // splits: S * k candidates fit the merge buffer, and one list head per lane (S <= 64; at
+    // k < 4 the buffer alone allowed up to 256 splits, whose lists past lane 63 were dropped)
+    const uint32_t smax = kFbCands / a.k < 64u ? kFbCands / a.k : 64u;
+    uint32_t S = f.nfb / groups;
+    S = S < 1 ? 1u : S > smax ? smax : S;
+    if (!single) {
+        const uint64_t ntiles = (a.n + scan::TILE - 1) / scan::TILE;
+        if ((uint64_t)S > ntiles) S = ntiles ? (uint32_t)ntiles : 1u;
+        const uint64_t sl = (ntiles ? (ntiles + S - 1) / S : 1) * scan::TILE;
+        if (ntiles) S = (uint32_t)((a.n + sl - 1) / sl);
+    }
+    const uint32_t roles = groups * S;
+    for (uint32_t role = blk; role < roles; role += f.nfb) {
+        const uint32_t g = role / S, sp = role - g * S;
+        F3Args as = a;   // single: the target's sub-partition (or the whole set)
+        if (single) {
+            const uint32_t sb = __builtin_amdgcn_readfirstlane((uint32_t)a.fb_sub[g]);
+            if (sb != 255u) {
+                const SubDesc d = a.subs[sb];
+                if (d.n >= a.k) {
+                    as.planes = d.planes;
+                    as.stride = d.stride;
+                    as.n = d.n;
+                    as.gidx = d.gidx;
+                    as.base = d.base;
+                }
+            }
+        }
+        const uint64_t nt = (as.n + scan::TILE - 1) / scan::TILE;
+        const uint64_t split_len = (nt ? (nt + S - 1) / S : 1) * scan::TILE;
+        const uint64_t lo = (uint64_t)sp * split_len < as.n ? (uint64_t)sp * split_len : as.n;
+        const uint64_t hi = lo + split_len < as.n ? lo + split_len : as.n;
+        // split lists at record slot (g * S + sp) * kFbGroup + target-in-group (fb_merge's layout)
+        const uint64_t rb = single ? ((uint64_t)g * S + sp) * kFbGroup - g
+                                   : (uint64_t)g * kFbGroup * (S - 1) + (uint64_t)sp * kFbGroup;
+        const scan::ScanOut o{as.out_idx, as.out_cnt, as.gidx, as.base, S > 1 ? f.rec : nullptr, rb, 0u};
+        const uint32_t qb = single ? (wv == 0 ? g : g + 1) : g * kFbGroup + wv * kScanTargets;
+        scan::scan_run<K, kScanTargets>(lds, as.planes, as.stride, lo, hi, as.tp, as.ts, as.fb_list, qb,
+                                        single ? g + 1 : cnt, as.k, o);
+        if (S == 1) continue;
+        // hand-off: every wave's sc1 record stores drained, then one agent-scope add per block;
+        // the block whose add completes the group merges it (its waves load after the barrier)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) *last = atomicAdd(f.done + g, 1u) == S - 1 ? 1u : 0u;
+        __syncthreads();
+        if (!*last) continue;
+        fb_merge(as, f, g, S, cnt, lds, gsize);
+        if (threadIdx.x == 0) f.done[g] = 0;   // all-zero again for the next call
+        __syncthreads();                       // lds is reused by this block's next role
+    }
+}
+
 template <int K>
 __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[scan::lds_words<kScanTargets>()];
@@ -1151,74 +1225,17 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
             if (threadIdx.x < 64 && mine && myc) a.tie_cnt[pj] = 0;   // all-zero again for the next call
         }
     }
-    if (f.hint && blockIdx.x == 0 && threadIdx.x == 0) *f.hint = a.ctr[0];   // sizes a later call's grid
+    if (f.hint && blockIdx.x == 0 && threadIdx.x == 0)   // sizes a later call's grid (mapped host memory)
+        __hip_atomic_store(f.hint, a.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t cnt = a.ctr[0];
     if (cnt == 0) return;
-    // Sub-partitioned call with a short list (on uniform ids: the rare target whose level-Lm
-    // subtree holds < k ids): every target is its own group and scans only its own
-    // sub-partition -- which holds its top-k when it holds >= k ids -- over S splits (a scan of
-    // the whole set cost a single target ~3 ms at 2^28 ids).  Up to one target per
-    // sub-partition: past that, one scan of the whole set for all of them reads less.  (One
-    // scan_run call site for both forms: a second inlined copy doubled this kernel's VGPRs.)
-    const bool single = a.np_sub != f.np_ties && cnt <= min(kFbSingle, f.np_ties / a.np_sub);
-    const uint32_t gsize = single ? 1u : kFbGroup;
-    const uint32_t groups = (cnt + gsize - 1) / gsize;
-    // splits: S * k candidates fit the merge buffer, and one list head per lane (S <= 64; at
-    // k < 4 the buffer alone allowed up to 256 splits, whose lists past lane 63 were dropped)
-    const uint32_t smax = kFbCands / a.k < 64u ? kFbCands / a.k : 64u;
-    uint32_t S = f.nfb / groups;
-    S = S < 1 ? 1u : S > smax ? smax : S;
-    if (!single) {
-        const uint64_t ntiles = (a.n + scan::TILE - 1) / scan::TILE;
-        if ((uint64_t)S > ntiles) S = ntiles ? (uint32_t)ntiles : 1u;
-        const uint64_t sl = (ntiles ? (ntiles + S - 1) / S : 1) * scan::TILE;
-        if (ntiles) S = (uint32_t)((a.n + sl - 1) / sl);
-    }
-    const uint32_t roles = groups * S;
-    for (uint32_t role = blockIdx.x; role < roles; role += f.nfb) {
-        const uint32_t g = role / S, sp = role - g * S;
-        F3Args as = a;   // single: the target's sub-partition (or the whole set)
-        if (single) {
-            const uint32_t sb = __builtin_amdgcn_readfirstlane((uint32_t)a.fb_sub[g]);
-            if (sb != 255u) {
-                const SubDesc d = a.subs[sb];
-                if (d.n >= a.k) {
-                    as.planes = d.planes;
-                    as.stride = d.stride;
-                    as.n = d.n;
-                    as.gidx = d.gidx;
-                    as.base = d.base;
-                }
-            }
-        }
-        const uint64_t nt = (as.n + scan::TILE - 1) / scan::TILE;
-        const uint64_t split_len = (nt ? (nt + S - 1) / S : 1) * scan::TILE;
-        const uint64_t lo = (uint64_t)sp * split_len < as.n ? (uint64_t)sp * split_len : as.n;
-        const uint64_t hi = lo + split_len < as.n ? lo + split_len : as.n;
-        // split lists at record slot (g * S + sp) * kFbGroup + target-in-group (fb_merge's layout)
-        const uint64_t rb = single ? ((uint64_t)g * S + sp) * kFbGroup - g
-                                   : (uint64_t)g * kFbGroup * (S - 1) + (uint64_t)sp * kFbGroup;
-        const scan::ScanOut o{as.out_idx, as.out_cnt, as.gidx, as.base, S > 1 ? f.rec : nullptr, rb, 0u};
-        const uint32_t qb = single ? (wv == 0 ? g : g + 1) : g * kFbGroup + wv * kScanTargets;
-        scan::scan_run<K, kScanTargets>(lds, as.planes, as.stride, lo, hi, as.tp, as.ts, as.fb_list, qb,
-                                        single ? g + 1 : cnt, as.k, o);
-        if (S == 1) continue;
-        // hand-off: every wave's sc1 record stores drained, then one agent-scope add per block;
-        // the block whose add completes the group merges it (its waves load after the barrier)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) last = atomicAdd(f.done + g, 1u) == S - 1 ? 1u : 0u;
-        __syncthreads();
-        if (!last) continue;
-        fb_merge(as, f, g, S, cnt, lds, gsize);
-        if (threadIdx.x == 0) f.done[g] = 0;   // all-zero again for the next call
-        __syncthreads();                       // lds is reused by this block's next role
-    }
+    fb_list_scan<K>(a, f, cnt, blockIdx.x, lds, &last);
 }
 
 struct BatchPlan {
     uint32_t Lm, b1, Lq, nwords, nblk1, nblk2, stage, sparse, tcap;
     uint32_t scap;   // survivors per (bucket set, partition)
+    uint32_t spec;   // F3's speculative slots per set (mean + 5 sigma of one set's share)
     bool fits;   // partitions' survivors fit the F3 stage on uniform ids
     uint64_t per_blk;
 };
@@ -1278,6 +1295,12 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
         const double mean = sub * f * mu, var = sub * f * (1.0 - f) * mu * mu + sub * f * mu;
         const double cap = mean + 8.0 * std::sqrt(var) + 64.0;
         P.scap = cap >= (double)kF3Cap ? kF3Cap : ((uint32_t)cap + 63u) & ~63u;
+        // F3 loads this many slots per set with the counts (one round trip); a partition with a
+        // set past it (about 1 in 10^5 per set at 5 sigma) takes the exact second gather.  A fixed
+        // 512 fetched 2x the survivor bytes at cfg 2 and 5x at the cfg-3 shard (PMC, round 2)
+        const double sp = mean + 5.0 * std::sqrt(var) + 32.0;
+        const uint32_t half = kF3Cap / kSets;
+        P.spec = sp >= (double)half ? half : ((uint32_t)sp + 63u) & ~63u;
     }
     // F3 sorts by up to 1 bit below the mark level (finer candidate ranges), <= 4096 bins
     P.Lq = P.Lm + 1 < 32 ? P.Lm + 1 : 32;
@@ -1704,7 +1727,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     // the base arguments are the whole set's: F4's scan (fallback targets) runs over all its ids
     F3Args a{pbuf, pcount, P.scap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, c.planes, c.stride,
              c.n, c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, fb_sub, pstat, tie_hdr, tie_cand, tie_cnt,
-             d_desc, np, dbg, stamps};
+             d_desc, np, dbg, stamps, c.f3_spec < 0 ? P.spec : (uint32_t)c.f3_spec};
     size_t l3 = f3_lds(P);
     if (dbg & 4096) l3 = l3 > 81920 ? l3 : 81920;   // experiment: 2 F3 blocks per CU
     if (dbg & 8192) l3 = l3 > 54000 ? l3 : 54000;   // experiment: 3 F3 blocks per CU
@@ -1750,27 +1773,34 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
 // little else.  S1 streams w0 once on every CU: each id's top hb = min(16, Ls) bits are tested
 // against an LDS bitmap of the targets' (at most 64 set bits of 2^16), and the rare hits are
 // matched exactly against the sorted distinct level-Ls prefixes of the targets; a match is
-// appended to that prefix's candidate bucket (one returning atomic on its counter).  S2: one
-// workgroup per distinct prefix answers the prefix's targets from its bucket -- every id of
-// sub(t, Ls), complete, so the exact top-k when it holds >= k ids (the candidates' full-key
-// order, f3_wave_answer) -- or, when the bucket is short of k ids or overflowed, hands its
-// targets to the K1 scan over all ids (K6's F4 pass, which exits at once on an empty list).
-// S2 re-zeroes the counters.  Prefix shards stream their shifted word-0 plane, as K6 does.
+// appended, with its word 1 (loaded after the stream, with the append), to that prefix's
+// candidate bucket.  S2, one launch: one workgroup per distinct prefix answers the prefix's
+// targets from its bucket -- every id of sub(t, Ls), complete, so the exact top-k when it holds
+// >= k ids (the candidates' (w0, w1) distance order in registers, the full key only on a double
+// tie) -- and kSmallFbBlocks scan-role workgroups beside them read the final bucket counts (S1
+// has completed), list the targets whose bucket is short of k ids or overflowed, and answer
+// them with the K1 scan over all ids (F4's list scan); on uniform ids the list is empty and the
+// role workgroups exit after one round trip (round 2 launched a separate F4 for it: an empty
+// kernel of ~4 µs on every call).  The bucket counters come in two sets used by alternate calls:
+// S2's workgroups read this call's while S2 zeroes the other's for the next call.  Prefix
+// shards stream their shifted word-0 plane, as K6 does.
 namespace {
 constexpr uint32_t kSmallQ = 64;
 constexpr uint32_t kSmallCap = 512;                   // candidates per prefix bucket
 constexpr uint32_t kS1Queue = 512;                    // matched ids queued in LDS per block
-constexpr uint32_t kSmallFbBlocks = 32;               // K1 fallback scan workgroups
+constexpr uint32_t kSmallFbBlocks = 32;               // K1 fallback scan workgroups (S2's scan roles)
 constexpr int kS2Threads = scan::WAVES * 64;
+static_assert(kSmallCap <= (uint32_t)kS2Threads, "one bucket slot per S2 thread");
 
 struct SmallArgs {
     const uint32_t* w0; uint64_t n; uint64_t per_blk; uint32_t lim;
+    const uint32_t* w1;         // the ids' word-1 plane (unshifted): carried with every candidate
     const uint32_t* tp; uint64_t ts; uint32_t q, shift, Ls;
-    uint32_t* cnt;      // [kSmallQ] bucket fill per distinct prefix (all-zero between calls)
-    uint2* cand;        // [kSmallQ][kSmallCap] {shifted w0, index}
-    uint32_t* tab;      // [kSmallQ + 1] the sorted distinct prefixes (S1 block 0), their number last
-    uint32_t* fb;       // [kSmallQ] targets for the K1 scan; fb_cnt[0] their number (S1 zeroes it)
-    uint32_t* fb_cnt;
+    uint32_t* cnt;              // [kSmallQ] this call's bucket fills (all-zero before S1)
+    uint32_t* cnt_next;         // [kSmallQ] the next call's (S2 zeroes them)
+    uint4* cand;                // [kSmallQ][kSmallCap] {shifted w0, index, word 1, 0}
+    uint32_t* tab;              // [kSmallQ + 1] the sorted distinct prefixes (S1 block 0), their number last
+    uint32_t* fb;               // [kSmallFbBlocks][kSmallQ] each scan role's copy of the fallback list
 };
 
 // target qi's word 0 as the streamed plane holds it (shifted for a prefix shard)
@@ -1821,10 +1851,7 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
         if (lane == 0) ntab_s = (uint32_t)__popcll(fm);
         if (blockIdx.x == 0) {
             if (first) a.tab[rank] = pre;
-            if (lane == 0) {
-                a.tab[kSmallQ] = (uint32_t)__popcll(fm);
-                a.fb_cnt[0] = 0;
-            }
+            if (lane == 0) a.tab[kSmallQ] = (uint32_t)__popcll(fm);
         }
     }
     __syncthreads();
@@ -1842,7 +1869,7 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
             hitq[qi] = make_uint4(w, j, slot, 0u);
         } else {
             const uint32_t pos = atomicAdd(a.cnt + slot, 1u);
-            if (pos < kSmallCap) a.cand[slot * kSmallCap + pos] = make_uint2(w, j);
+            if (pos < kSmallCap) a.cand[slot * kSmallCap + pos] = make_uint4(w, j, a.w1[j], 0u);
         }
     };
     const uint32_t h_off = 32 - hb, tid4 = 4 * threadIdx.x;
@@ -1878,49 +1905,139 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
         }
     }
     __syncthreads();
+    // the queue to the buckets: word 1 and the slot reservation in one round trip
     const uint32_t nq = nhit < kS1Queue ? nhit : kS1Queue;
     for (uint32_t i = threadIdx.x; i < nq; i += NT) {
         const uint4 e = hitq[i];
+        const uint32_t w1 = a.w1[e.y];
         const uint32_t pos = atomicAdd(a.cnt + e.z, 1u);
-        if (pos < kSmallCap) a.cand[e.z * kSmallCap + pos] = make_uint2(e.x, e.y);
+        if (pos < kSmallCap) a.cand[e.z * kSmallCap + pos] = make_uint4(e.x, e.y, w1, 0u);
     }
 }
 
-__global__ __launch_bounds__(kS2Threads) void k_s2_answer(F3Args a, SmallArgs sa) {
-    __shared__ uint2 S[kSmallCap];      // the bucket
-    __shared__ uint32_t tl[kSmallQ];
-    __shared__ uint32_t ntl_s;
-    const uint32_t s = blockIdx.x;
+// exact top-`want` of target qi (word 0 as streamed: t0; all five words: t) from the c
+// candidates S[0, c) of one bucket, {w0, index, w1}: order by (w0 distance, w1 distance), the
+// full key (planes) only on a double tie.  c <= 64: one candidate per lane, its rank counted
+// against all of them; else a lane-distributed running list over chunks of 64.
+__device__ void ks_answer(const F3Args& a, const uint4* S, uint32_t c, uint32_t qi, uint32_t t0, const uint32_t* t,
+                          uint32_t want, uint32_t lane) {
+    uint32_t* orow = a.out_idx + (uint64_t)qi * a.k;
+    if (c <= 64) {
+        const bool act = lane < c;
+        const uint4 me = S[act ? lane : 0u];
+        const uint32_t md = act ? me.x ^ t0 : DHT_NONE, m1 = act ? me.z ^ t[1] : DHT_NONE;
+        uint32_t rank = 0;
+        for (uint32_t o = 0; o < c; ++o) {
+            const uint32_t xd = __builtin_amdgcn_readlane((int)md, (int)o);
+            const uint32_t x1 = __builtin_amdgcn_readlane((int)m1, (int)o);
+            const uint32_t xi = __builtin_amdgcn_readlane((int)me.y, (int)o);
+            if (xd < md || (xd == md && x1 < m1)) ++rank;
+            else if (xd == md && x1 == m1 && act && o != lane && id_less(xd, xi, md, me.y, a.planes, a.stride, t)) ++rank;
+        }
+        if (act && rank < want) orow[rank] = map_out(me.y, a.gidx, a.base);
+    } else {
+        uint32_t ed = DHT_NONE, e1 = DHT_NONE, ei = DHT_NONE, cnt = 0;
+        for (uint32_t c0 = 0; c0 < c; c0 += 64) {
+            const bool v = c0 + lane < c;
+            const uint4 x = v ? S[c0 + lane] : make_uint4(0u, DHT_NONE, 0u, 0u);
+            const uint32_t xd = x.x ^ t0, xi = x.y, x1 = v ? x.z ^ t[1] : DHT_NONE;
+            uint32_t wd = cnt == want ? __builtin_amdgcn_readlane((int)ed, want - 1) : DHT_NONE;
+            uint32_t w1 = cnt == want ? __builtin_amdgcn_readlane((int)e1, want - 1) : DHT_NONE;
+            uint32_t wi = cnt == want ? __builtin_amdgcn_readlane((int)ei, want - 1) : DHT_NONE;
+            uint64_t cm = __ballot(v && (cnt < want || key2_less(xd, x1, xi, wd, w1, wi, a.planes, a.stride, t)));
+            while (cm) {
+                const uint32_t l = (uint32_t)__ffsll((long long)cm) - 1;
+                cm &= cm - 1;
+                const uint32_t cd = __builtin_amdgcn_readlane((int)xd, l), c1 = __builtin_amdgcn_readlane((int)x1, l);
+                const uint32_t ci = __builtin_amdgcn_readlane((int)xi, l);
+                if (cnt == want && !key2_less(cd, c1, ci, wd, w1, wi, a.planes, a.stride, t)) continue;
+                const bool closer = lane < cnt && key2_less(ed, e1, ei, cd, c1, ci, a.planes, a.stride, t);
+                const uint32_t pos = (uint32_t)__popcll(__ballot(closer));
+                const uint32_t ud = __shfl_up(ed, 1), u1 = __shfl_up(e1, 1), ui = __shfl_up(ei, 1);
+                if (lane == pos) { ed = cd; e1 = c1; ei = ci; }
+                else if (lane > pos) { ed = ud; e1 = u1; ei = ui; }
+                cnt = cnt + 1 < want ? cnt + 1 : want;
+                wd = cnt == want ? __builtin_amdgcn_readlane((int)ed, want - 1) : DHT_NONE;
+                w1 = cnt == want ? __builtin_amdgcn_readlane((int)e1, want - 1) : DHT_NONE;
+                wi = cnt == want ? __builtin_amdgcn_readlane((int)ei, want - 1) : DHT_NONE;
+            }
+        }
+        if (lane < want) orow[lane] = map_out(ei, a.gidx, a.base);
+    }
+    if (lane >= want && lane < a.k) orow[lane] = DHT_NONE;
+    if (lane == 0) a.out_cnt[qi] = want;
+}
+
+// S2: workgroups [0, q) answer the distinct prefixes (workgroup s: prefix s, if s < ntab), the
+// kSmallFbBlocks after them are the fallback list's scan roles
+template <int K>
+__global__ __launch_bounds__(kS2Threads) void k_s2_answer(F3Args a, SmallArgs sa, FbArgs f) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[scan::lds_words<kScanTargets>()];
+    __shared__ uint32_t misc[4];
+    __shared__ uint32_t s2_last;
+    static_assert(scan::lds_words<kScanTargets>() >= 4 * kSmallCap + kSmallQ * (1 + DHT_W), "S2 LDS image");
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-    // one round trip: the table, the bucket's count, the targets' words and (speculatively)
-    // the bucket's first kS2Threads slots
+    const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
+    if (blockIdx.x == 0 && threadIdx.x < kSmallQ) sa.cnt_next[threadIdx.x] = 0;   // the next call's counters
+    if (blockIdx.x >= sa.q) {
+        // ---- scan role r: the fallback list, from the final bucket counts (one round trip) ----
+        const uint32_t r = blockIdx.x - sa.q;
+        uint32_t* list = sa.fb + r * kSmallQ;   // this role's own copy (every role builds the same)
+        if (threadIdx.x < 64) {
+            const uint32_t ntab = sa.tab[kSmallQ];
+            const uint32_t tb = sa.tab[lane], cb = sa.cnt[lane];
+            const uint32_t pre = lane < sa.q ? top_bits(small_tw0(sa, lane), sa.Ls) : DHT_NONE;
+            const bool short_b = lane < ntab && (cb < want || cb > kSmallCap);
+            bool mine = false;   // my target's prefix is one of the short buckets
+            for (uint64_t m = __ballot(short_b); m; m &= m - 1) {
+                const uint32_t b = (uint32_t)__ffsll((long long)m) - 1;
+                mine = mine || pre == (uint32_t)__builtin_amdgcn_readlane((int)tb, (int)b);
+            }
+            mine = mine && lane < sa.q;
+            const uint64_t lm = __ballot(mine);
+            if (mine) list[__popcll(lm & ((1ull << lane) - 1ull))] = lane;
+            if (lane == 0) misc[0] = (uint32_t)__popcll(lm);
+        }
+        __syncthreads();   // wave 0's list stores are visible to the workgroup
+        const uint32_t nfl = __builtin_amdgcn_readfirstlane(misc[0]);
+        if (!nfl) return;   // uniform ids: nothing to scan (block-uniform)
+        F3Args as = a;
+        as.fb_list = list;
+        fb_list_scan<K>(as, f, nfl, r, lds, &s2_last);
+        return;
+    }
+    // ---- prefix workgroup s: one round trip for the table, the count, the targets' words and
+    // the bucket (one slot per thread) ----
+    const uint32_t s = blockIdx.x;
+    uint4* S = reinterpret_cast<uint4*>(lds);
+    uint32_t* tl = lds + 4 * kSmallCap;   // this prefix's targets
+    uint32_t* tw = tl + kSmallQ;          // [DHT_W][kSmallQ] target words
     const uint32_t ntab = sa.tab[kSmallQ];
     const uint32_t pre_s = sa.tab[s < kSmallQ ? s : 0u];
     const uint32_t c = sa.cnt[s < kSmallQ ? s : 0u];
-    const uint32_t tw = threadIdx.x < 64 && lane < sa.q ? small_tw0(sa, lane) : 0u;
-    static_assert(kSmallCap == kS2Threads, "one speculative bucket slot per thread");
-    const uint2 e = sa.cand[(s < kSmallQ ? s : 0u) * kSmallCap + threadIdx.x];
+    const uint32_t t0s = threadIdx.x < 64 && lane < sa.q ? small_tw0(sa, lane) : 0u;
+    const uint4 e = sa.cand[(s < kSmallQ ? s : 0u) * kSmallCap + (threadIdx.x < kSmallCap ? threadIdx.x : 0u)];
+    const uint32_t tj = threadIdx.x / kSmallQ, tq = threadIdx.x % kSmallQ;
+    const uint32_t twv = tj < DHT_W && tq < sa.q ? sa.tp[(uint64_t)tj * sa.ts + tq] : 0u;
     if (s >= ntab) return;   // block-uniform
     if (threadIdx.x < 64) {   // this prefix's targets
-        const bool v = lane < sa.q && top_bits(tw, sa.Ls) == pre_s;
+        const bool v = lane < sa.q && top_bits(t0s, sa.Ls) == pre_s;
         const uint64_t m = __ballot(v);
         if (v) tl[__popcll(m & ((1ull << lane) - 1ull))] = lane;
-        if (lane == 0) ntl_s = (uint32_t)__popcll(m);
+        if (lane == 0) misc[0] = (uint32_t)__popcll(m);
     }
-    if (threadIdx.x < c) S[threadIdx.x] = e;
+    if (threadIdx.x < c && threadIdx.x < kSmallCap) S[threadIdx.x] = e;
+    if (tj < DHT_W) tw[tj * kSmallQ + tq] = twv;
     __syncthreads();
-    if (threadIdx.x == 0) sa.cnt[s] = 0;   // all-zero again (only this workgroup reads bucket s)
-    const uint32_t ntl = __builtin_amdgcn_readfirstlane(ntl_s);
-    const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
-    if (c >= want && c <= kSmallCap) {
-        for (uint32_t i = wv; i < ntl; i += scan::WAVES) {
-            const uint32_t qi = __builtin_amdgcn_readfirstlane(tl[i]);
-            f3_wave_answer(a, S, 0, c, qi, __builtin_amdgcn_readfirstlane(small_tw0(sa, qi)), want, lane);
-        }
-    } else if (threadIdx.x == 0) {
-        // sub(t, Ls) short of k ids (or the bucket overflowed): the K1 scan over all ids
-        const uint32_t b = atomicAdd(sa.fb_cnt, ntl);
-        for (uint32_t i = 0; i < ntl; ++i) sa.fb[b + i] = tl[i];
+    if (c < want || c > kSmallCap) return;   // the scan roles answer this prefix's targets
+    const uint32_t ntl = misc[0];
+    for (uint32_t i = wv; i < ntl; i += scan::WAVES) {
+        const uint32_t qi = __builtin_amdgcn_readfirstlane(tl[i]);
+        uint32_t t[DHT_W];
+#pragma unroll
+        for (int j = 0; j < DHT_W; ++j) t[j] = __builtin_amdgcn_readfirstlane(tw[j * kSmallQ + qi]);
+        const uint32_t t0 = sa.shift ? (t[0] << sa.shift) | (t[1] >> (32 - sa.shift)) : t[0];
+        ks_answer(a, S, c, qi, t0, t, want, lane);
     }
 }
 
@@ -1933,30 +2050,32 @@ bool small_supported(uint64_t n, uint32_t q, uint32_t k) {
     return q >= 1 && q <= kSmallQ && k >= 1 && k <= DHTGPU_MAX_K_DEV && n >= 1 && n < (1ull << 31);
 }
 
-// cnt | tab | fb | fb_cnt | F4 scratch (list_scan_bytes(32): done counters first) | cand
+// cnt[2][kSmallQ] | tab | fb[kSmallFbBlocks][kSmallQ] | F4 scratch (list_scan_bytes(32): done
+// counters first) | cand
 size_t small_bytes() {
-    return al256((size_t)kSmallQ * 4) + al256((size_t)(kSmallQ + 1) * 4) + al256((size_t)kSmallQ * 4) + 256 +
-           list_scan_bytes(DHTGPU_MAX_K_DEV) + (size_t)kSmallQ * kSmallCap * 8;
+    return al256((size_t)2 * kSmallQ * 4) + al256((size_t)(kSmallQ + 1) * 4) + al256((size_t)kSmallFbBlocks * kSmallQ * 4) +
+           list_scan_bytes(DHTGPU_MAX_K_DEV) + (size_t)kSmallQ * kSmallCap * 16;
 }
 
-hipError_t launch_small_topk(const BatchCall& c, void* sws, hipStream_t s) {
+hipError_t launch_small_topk(const BatchCall& c, void* sws, uint32_t parity, hipStream_t s) {
     uint8_t* w = static_cast<uint8_t*>(sws);
     SmallArgs a{};
-    a.cnt = reinterpret_cast<uint32_t*>(w);
-    a.tab = reinterpret_cast<uint32_t*>(w + al256((size_t)kSmallQ * 4));
-    uint8_t* x = w + al256((size_t)kSmallQ * 4) + al256((size_t)(kSmallQ + 1) * 4);
+    a.cnt = reinterpret_cast<uint32_t*>(w) + (parity & 1u) * kSmallQ;
+    a.cnt_next = reinterpret_cast<uint32_t*>(w) + ((parity & 1u) ^ 1u) * kSmallQ;
+    uint8_t* x = w + al256((size_t)2 * kSmallQ * 4);
+    a.tab = reinterpret_cast<uint32_t*>(x);
+    x += al256((size_t)(kSmallQ + 1) * 4);
     a.fb = reinterpret_cast<uint32_t*>(x);
-    x += al256((size_t)kSmallQ * 4);
-    a.fb_cnt = reinterpret_cast<uint32_t*>(x);
-    x += 256;
+    x += al256((size_t)kSmallFbBlocks * kSmallQ * 4);
     void* fb_scratch = x;
     x += list_scan_bytes(DHTGPU_MAX_K_DEV);
-    a.cand = reinterpret_cast<uint2*>(x);
+    a.cand = reinterpret_cast<uint4*>(x);
     const uint64_t n = c.n;
     // level: the deepest with >= 4k ids per subtree on uniform ids (K6's rule), at most 31
     a.Ls = 0;
     while (a.Ls < 31 && (n >> (a.Ls + 1)) >= 4ull * c.k) ++a.Ls;
     a.w0 = c.w0s ? c.w0s : c.planes;
+    a.w1 = c.planes + c.stride;
     a.n = n;
     const uint64_t lim = (c.w0s ? c.stride : 5 * c.stride) - 4;
     a.lim = (uint32_t)(lim < 0xFFFFFFF0ull ? lim : 0xFFFFFFF0ull);
@@ -1994,18 +2113,17 @@ hipError_t launch_small_topk(const BatchCall& c, void* sws, hipStream_t s) {
         (void)hipEventRecord(ev[1], s);
     }
     go(1, k_s1_filter<nt>, dim3(nblk), dim3(nt), 0, a);
-    go(2, k_s2_answer, dim3(c.q), dim3(kS2Threads), 0, f, a);
-    // the K1 scan for the listed targets (K6's F4 pass; an empty list exits at once)
-    f.ctr = a.fb_cnt;
-    f.fb_list = a.fb;
-    // a smaller grid than K6's: the list holds at most 64 targets (one scan group) and is
-    // empty on all but strongly clustered id sets, where the dispatch of an empty grid is the cost
+    // S2: the prefix workgroups and the fallback list's scan roles in one launch
     const FbArgs fa{reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(fb_scratch) + al256((size_t)kFbBlocks * 4)),
-                    static_cast<uint32_t*>(fb_scratch), kSmallFbBlocks, 0u};
-    const dim3 g4(kSmallFbBlocks), b4(kF4Threads);
-    if (c.k <= 8) go(3, k_f4<8>, g4, b4, 0, f, fa);
-    else if (c.k <= 16) go(3, k_f4<16>, g4, b4, 0, f, fa);
-    else go(3, k_f4<32>, g4, b4, 0, f, fa);
+                    static_cast<uint32_t*>(fb_scratch), kSmallFbBlocks, 0u, nullptr};
+    const dim3 g2(c.q + kSmallFbBlocks), b2(kS2Threads);
+    if (c.k <= 8) go(2, k_s2_answer<8>, g2, b2, 0, f, a, fa);
+    else if (c.k <= 16) go(2, k_s2_answer<16>, g2, b2, 0, f, a, fa);
+    else go(2, k_s2_answer<32>, g2, b2, 0, f, a, fa);
+    if (ev) {   // no separate fallback kernel: an empty pair
+        (void)hipEventRecord(ev[6], s);
+        (void)hipEventRecord(ev[7], s);
+    }
     return hipGetLastError();
 }
 

@@ -122,6 +122,7 @@ struct BatchCall {
     int num_cus;
     uint32_t dbg;                          // DHTGPU_DBG experiment switches (0 in production)
     uint32_t f2_seg;                       // F2 sparse-mode segment override in ids (0: the plan's)
+    int32_t f3_spec;                       // F3 speculative slots per bucket set (< 0: the plan's; 0: exact gather)
     const volatile uint32_t* fb_hint;      // nullable: the slot's last fallback-list length (mapped host memory)
     uint32_t* fb_hint_dev;                 // its device address (F4 writes it)
     unsigned long long* stamps;            // dbg & 256: phase stamps [2 * 8192 * 16]
@@ -131,10 +132,11 @@ struct BatchCall {
 hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty);
 // KS (batch.hip): batches of at most 64 targets -- one pass over word 0 and one workgroup per
 // distinct target prefix (K6's results).  sws: small_bytes(), zero before its first use (left
-// zero); ev (nullable) gets S1 as F2's pair and S2 as F3's, F1 / F4 pairs empty.
+// zero); parity: alternates between consecutive calls on one workspace (two counter sets);
+// ev (nullable) gets S1 as F2's pair and S2 as F3's, F1 / F4 pairs empty.
 bool small_supported(uint64_t n, uint32_t q, uint32_t k);
 size_t small_bytes();
-hipError_t launch_small_topk(const BatchCall& c, void* sws, hipStream_t s);
+hipError_t launch_small_topk(const BatchCall& c, void* sws, uint32_t parity, hipStream_t s);
 
 // sort.hip: lexicographic sort of an id set (stable LSD radix over the 160-bit keys).
 // out_planes (out_stride >= n) = the ids in ascending InfoHash order, perm[j] = the input index

@@ -20,6 +20,8 @@
 #include "dhtgpu_dev.h"
 #include "dhtgpu_internal.h"
 
+#include <mutex>
+
 namespace dhtgpu {
 namespace {
 
@@ -496,6 +498,9 @@ static void index_layout(void* ws, uint64_t n, uint32_t B, uint2*& pairs, uint32
     (void)B;
 }
 
+constexpr int kIdxMaxDevices = 64;
+std::once_flag g_idx_attr_once[kIdxMaxDevices];
+
 hipError_t launch_index_build(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t B, void* ws,
                               hipStream_t s, hipEvent_t* ev) {
     (void)stride;
@@ -510,12 +515,15 @@ hipError_t launch_index_build(const uint32_t* planes, uint64_t stride, uint64_t 
     uint32_t* H = reinterpret_cast<uint32_t*>(tmp + n);
     uint32_t* pcount = H + np * (nblk ? nblk : 1);
     uint32_t* pstart = pcount + np;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_p2_buckets, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
-        (void)hipFuncSetAttribute((const void*)k_p1_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
-        attr_set = true;
-    }
+    // hipFuncSetAttribute applies to the device current at the call: once per device, from
+    // whichever thread gets there first (a plain static flag raced between threads and skipped
+    // every device after the first)
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kIdxMaxDevices)
+        std::call_once(g_idx_attr_once[dev], [] {
+            (void)hipFuncSetAttribute((const void*)k_p2_buckets, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
+            (void)hipFuncSetAttribute((const void*)k_p1_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
+        });
     if (ev) (void)hipEventRecord(ev[0], s);
     if (n) {
         k_p0_hist<<<nblk, kBlk, np * 4, s>>>(planes, n, b1, nblk, p1_tile(n), H);

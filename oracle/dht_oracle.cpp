@@ -301,6 +301,22 @@ void orc_classify(uint32_t nb, const uint8_t* firsts20, const uint8_t* myid20,
     }
 }
 
+/* orc_classify over `threads` contiguous id ranges (the cfg-4 CPU baseline at every host core):
+ * the same findBucket + commonBits per id, one 161-bin histogram per thread, summed. */
+void orc_classify_mt(uint32_t nb, const uint8_t* firsts20, const uint8_t* myid20,
+                     const uint8_t* ids20, uint64_t n, uint8_t* out_bucket, uint64_t* hist161, int threads) {
+    if (threads < 1) threads = 1;
+    std::vector<uint64_t> h((size_t)threads * 161, 0);
+    parallel_for((uint64_t)threads, threads, [&](uint64_t t) {
+        const uint64_t lo = n * t / threads, hi = n * (t + 1) / threads;
+        orc_classify(nb, firsts20, myid20, ids20 + 20 * lo, hi - lo, out_bucket + lo, h.data() + 161 * t);
+    });
+    for (unsigned i = 0; i <= 8 * HASH_LEN; i++) {
+        hist161[i] = 0;
+        for (int t = 0; t < threads; t++) hist161[i] += h[161 * (size_t)t + i];
+    }
+}
+
 /* NodeCache::getCachedNodes, src/node_cache.cpp:42-74. END plays the role of c.cend(). */
 uint32_t orc_cached_nodes(const uint8_t* sorted_ids20, uint64_t n, const uint8_t* accept,
                           const uint8_t* target20, uint32_t count, uint32_t* out_idx) {

@@ -102,6 +102,10 @@ uint32_t orc_buffer_nodes(const uint8_t* ids20, const uint8_t* tail, uint32_t al
 int orc_deserialize_node(const uint8_t* rec, uint32_t af, const uint8_t* myid20, uint32_t from_af,
                          const uint8_t* from_addr, uint8_t* out_tail);
 
+/* orc_classify split over `threads` contiguous id ranges (cfg-4 CPU baseline). */
+void orc_classify_mt(uint32_t nb, const uint8_t* firsts20, const uint8_t* myid20,
+                     const uint8_t* ids20, uint64_t n, uint8_t* out_bucket, uint64_t* hist161, int threads);
+
 /* Crawl-replay model (crawl_oracle.cpp header comment): one iterative search per target
  * over an n-node network with implicit k-bucket routing tables.  Outputs the final
  * SearchNode list (64 slots: index, flags bit0 asked / bit1 replied / bit2 bad), its

@@ -85,6 +85,7 @@ def _load(path):
     L.orc_find_closest.argtypes = [ctypes.c_uint32, u8p, u32p, u8p, u8p, u8p, ctypes.c_uint32, u32p]
     L.orc_find_closest.restype = ctypes.c_uint32
     L.orc_classify.argtypes = [ctypes.c_uint32, u8p, u8p, u8p, ctypes.c_uint64, u8p, u64p]
+    L.orc_classify_mt.argtypes = [ctypes.c_uint32, u8p, u8p, u8p, ctypes.c_uint64, u8p, u64p, ctypes.c_int]
     L.orc_search_insert.argtypes = [u8p, u8p, u8p, ctypes.c_uint32, ctypes.c_uint32, u32p, u8p, u32p, u8p, u64p,
                                     u32p, u8p, u8p, ctypes.c_int]
     L.orc_find_closest_batch.argtypes = [ctypes.c_uint32, u8p, u32p, u8p, u8p, u8p, ctypes.c_uint32,
@@ -132,14 +133,21 @@ def cmp(a, b):
     return lib().orc_cmp(_p(a, u8p), _p(b, u8p))
 
 
-def topk(ids, targets, k, threads=os.cpu_count() or 1):
+def default_threads():
+    """Worker threads when the caller names none: the host's CPUs, at most 16 (a GPU box's CPU
+    share; os.cpu_count() there reports the whole machine).  An explicit count is used as given
+    (bench.py's cpu_baseline runs at every host CPU)."""
+    return min(os.cpu_count() or 1, 16)
+
+
+def topk(ids, targets, k, threads=None):
     ids = np.ascontiguousarray(ids, dtype=np.uint8)
     targets = np.ascontiguousarray(targets, dtype=np.uint8)
     q = targets.shape[0]
     out = np.empty((q, k), dtype=np.uint32)
     cnt = np.empty(q, dtype=np.uint32)
     lib().orc_topk(_p(ids, u8p), ids.shape[0], _p(targets, u8p), q, k, _p(out, u32p), _p(cnt, u32p),
-                   min(threads, 16))
+                   int(threads or default_threads()))
     return out, cnt
 
 
@@ -242,15 +250,20 @@ def search_insert(node_ids, node_state, targets, lists, flags, lens, expired, in
     return lists, flags, lens, expired, added[: node.size]
 
 
-def classify(firsts, myid, ids):
+def classify(firsts, myid, ids, threads=1):
+    """findBucket + commonBits per id (src/routing_table.cpp:153-166, infohash.h:154-176)."""
     firsts = np.ascontiguousarray(firsts, dtype=np.uint8)
     ids = np.ascontiguousarray(ids, dtype=np.uint8)
     myid = np.ascontiguousarray(myid, dtype=np.uint8)
     n = ids.shape[0]
     out = np.empty(max(n, 1), dtype=np.uint8)
     hist = np.zeros(161, dtype=np.uint64)
-    lib().orc_classify(firsts.shape[0], _p(firsts, u8p), _p(myid, u8p), _p(ids, u8p), n,
-                       _p(out, u8p), _p(hist, u64p))
+    if threads > 1:
+        lib().orc_classify_mt(firsts.shape[0], _p(firsts, u8p), _p(myid, u8p), _p(ids, u8p), n,
+                              _p(out, u8p), _p(hist, u64p), threads)
+    else:
+        lib().orc_classify(firsts.shape[0], _p(firsts, u8p), _p(myid, u8p), _p(ids, u8p), n,
+                           _p(out, u8p), _p(hist, u64p))
     return out[:n].copy(), hist
 
 
@@ -287,7 +300,7 @@ def deserialize_node(rec, af, myid, from_af, from_addr):
     return st, out
 
 
-def search_batch(ids, dead, table_seed, targets, searchers, max_rounds=64, threads=os.cpu_count() or 1):
+def search_batch(ids, dead, table_seed, targets, searchers, max_rounds=64, threads=None):
     """Crawl-replay model (oracle/crawl_oracle.cpp): (idx, flags, len, rounds, queries)."""
     ids = np.ascontiguousarray(ids, dtype=np.uint8)
     targets = np.ascontiguousarray(targets, dtype=np.uint8)
@@ -299,7 +312,7 @@ def search_batch(ids, dead, table_seed, targets, searchers, max_rounds=64, threa
     ln, rd, qs = (np.empty(q, np.uint32) for _ in range(3))
     lib().orc_search_batch(_p(ids, u8p), ids.shape[0], _p(d, u8p) if d is not None else None, table_seed,
                            _p(targets, u8p), _p(sr, u32p), q, max_rounds, _p(idx, u32p), _p(fl, u8p),
-                           _p(ln, u32p), _p(rd, u32p), _p(qs, u32p), min(threads, 16))
+                           _p(ln, u32p), _p(rd, u32p), _p(qs, u32p), int(threads or default_threads()))
     return idx, fl, ln, rd, qs
 
 

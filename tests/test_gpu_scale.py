@@ -216,6 +216,50 @@ def test_two_contexts_two_threads():
     assert not errors, errors
 
 
+_TWO_THREAD_INDEX = r"""
+import sys, threading
+import numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + "/tests")
+import opendht_amd, oracle as O
+ids = [O.gen_ids(6150 + i, 300_000) for i in range(2)]
+tgs = [O.gen_ids(6160 + i, 3000) for i in range(2)]
+want = [O.topk(ids[i], tgs[i], 8, threads=8) for i in range(2)]
+sr = (np.arange(500, dtype=np.uint64) * 7919 % 300_000).astype(np.uint32)
+crawl_want = [O.search_batch(ids[i], None, 9 + i, tgs[i][:500], sr, threads=8) for i in range(2)]
+errors, go = [], threading.Barrier(2)
+def worker(i):
+    try:
+        with opendht_amd.Context(0) as c:
+            c.set_ids(ids[i])
+            go.wait()                      # both threads reach the first K4/K5 launch together
+            for _ in range(6):
+                got = c.index_topk(tgs[i], 8)
+                if not (np.array_equal(got[0], want[i][0]) and np.array_equal(got[1], want[i][1])):
+                    errors.append(("index", i)); return
+            c.net_prepare(None, table_seed=9 + i)   # builds its order with the K4 index kernels
+            got = c.search_batch(tgs[i][:500], sr)
+            if not all(np.array_equal(g, w) for g, w in zip(got, crawl_want[i])):
+                errors.append(("crawl", i))
+    except Exception as e:
+        errors.append(repr(e))
+th = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+[t.start() for t in th]; [t.join(timeout=90) for t in th]
+print("ERRORS", errors); sys.exit(1 if errors or any(t.is_alive() for t in th) else 0)
+"""
+
+
+def test_index_two_threads_fresh_process():
+    """K4/K5 (index_topk) and the crawl network's order (net_prepare, built with the K4 kernels)
+    driven from two host threads in a FRESH process, so both threads hit the first launch -- and
+    the per-device once-only LDS attribute setup -- together (a plain static
+    flag there raced).  Both threads' answers == the oracle."""
+    import subprocess
+    import sys
+    root = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _TWO_THREAD_INDEX, root], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_batches_over_three_streams(ctx):
     """Nine calls issued back to back over three streams without a synchronisation between them
     (the bench's --inflight 3: each stream keeps its own workspace slot), then the same batches
