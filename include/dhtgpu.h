@@ -30,7 +30,10 @@
  * Threading (mirrors the reference, src/dhtrunner.cpp:115-150): one context per
  * thread, or external locking; every host-pointer call is synchronous.
  * The *_dev entry points take device pointers and a hipStream_t (void*), are
- * stream-ordered and do not synchronise (for batch/bench/multi-GPU use).
+ * stream-ordered and do not synchronise (for batch/bench/multi-GPU use).  A stream passed
+ * to a context must outlive it: a later call that moves a workspace slot to another stream
+ * records an event on the slot's previous stream, and dhtgpu_ctx_destroy synchronises the
+ * streams the slots last used.
  */
 #ifndef DHTGPU_H
 #define DHTGPU_H

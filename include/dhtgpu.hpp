@@ -23,13 +23,22 @@
  * Behaviour: results are identical to the reference (same nodes, same order).  On a
  * device error the helpers throw dhtgpu::Error; they never return different nodes.
  * The caller (single dht_thread, src/dhtrunner.cpp:115-150) owns the Context.
+ *
+ * Dispatch: a device call costs a fixed ~90 µs (snapshot + PCIe + launches) against
+ * ~0.13 µs per findClosestNodes on one CPU core (bench.py find_closest / cpu_baseline), so
+ * the helpers answer on the host -- the same walk as the reference body -- below
+ * Context::min_device_batch targets (default kMinDeviceBatch = 1024, above the measured
+ * crossover of ~740) and only larger batches go to the device.  A single call is therefore
+ * as fast as the reference's own (tests/cpp/adapter_check.cpp reports both).
  */
 #ifndef DHTGPU_HPP
 #define DHTGPU_HPP
 
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
+#include <iterator>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -54,6 +63,9 @@ inline void check(int code, const char* what) {
     if (code != DHTGPU_OK) throw Error(code, what);
 }
 
+/* Batches below this many targets are answered on the host (see Dispatch above). */
+static const size_t kMinDeviceBatch = 1024;
+
 /* RAII owner of one device context. */
 class Context {
 public:
@@ -62,6 +74,7 @@ public:
     Context(const Context&) = delete;
     Context& operator=(const Context&) = delete;
     dhtgpu_ctx* get() const { return ctx_; }
+    size_t min_device_batch = kMinDeviceBatch;   // smallest batch sent to the device
     uint64_t cache_version_ = 0;   // NodeCache mirror: version and size of the last upload
     size_t cache_size_ = 0;
 private:
@@ -73,6 +86,75 @@ template <class H>
 inline void put_id(std::vector<uint8_t>& out, const H& h) {
     const uint8_t* p = h.data();
     out.insert(out.end(), p, p + DHTGPU_HASH_LEN);
+}
+
+/* InfoHash::xorCmp(a, b) < 0 for target t (include/opendht/infohash.h:179-194): at the first
+ * byte where a and b differ, the one whose byte XOR t's is smaller is closer. */
+inline bool xor_closer(const uint8_t* t, const uint8_t* a, const uint8_t* b) {
+    for (unsigned i = 0; i < DHTGPU_HASH_LEN; ++i)
+        if (a[i] != b[i]) return (uint8_t)(a[i] ^ t[i]) < (uint8_t)(b[i] ^ t[i]);
+    return false;
+}
+
+/* The reference's findClosestNodes walk on the host (src/routing_table.cpp:110-150): the
+ * target's bucket (findBucket, :153-166: the last whose first <= id), then one bucket on each
+ * side per round until `count` good nodes are held, each inserted in xorCmp order. */
+template <class Table, class HashT, class TimePoint, class NodePtr>
+void find_closest_host(const Table& table, const HashT& id, TimePoint now, size_t count, std::vector<NodePtr>& nodes) {
+    nodes.clear();
+    const auto begin = table.begin(), end = table.end();
+    if (begin == end) return;
+    const uint8_t* t = id.data();
+    auto b = begin;
+    for (;;) {
+        auto nx = std::next(b);
+        if (nx == end || std::memcmp(t, nx->first.data(), DHTGPU_HASH_LEN) < 0) break;
+        b = nx;
+    }
+    auto insert_bucket = [&](const decltype(*begin)& bk) {
+        for (const auto& n : bk.nodes) {
+            if (!n->isGood(now)) continue;
+            auto here = std::find_if(nodes.begin(), nodes.end(), [&](const NodePtr& o) {
+                return xor_closer(t, n->id.data(), o->id.data());
+            });
+            nodes.insert(here, n);
+        }
+    };
+    auto itn = b;
+    auto itp = b == begin ? end : std::prev(b);
+    while (nodes.size() < count && (itn != end || itp != end)) {
+        if (itn != end) { insert_bucket(*itn); ++itn; }
+        if (itp != end) { insert_bucket(*itp); itp = itp == begin ? end : std::prev(itp); }
+    }
+    if (nodes.size() > count) nodes.resize(count);
+}
+
+/* The reference's getCachedNodes walk on the host (src/node_cache.cpp:42-74): out of
+ * lower_bound(id), each step takes the XOR-closer of the two neighbours; accepted = lock()
+ * succeeds && !isExpired() && !isClient().  O(log N + visited) -- no pass over the map. */
+template <class NodeMap, class HashT>
+std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>>
+cached_nodes_host(const NodeMap& c, const HashT& id, size_t count) {
+    std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>> res;
+    const uint8_t* t = id.data();
+    auto it_n = c.lower_bound(id);
+    auto it_p = it_n;
+    const auto end = c.cend();
+    auto dec = [&](decltype(it_p)& it) {   // cbegin() -> cend(), else prev()
+        auto ret = it;
+        it = it == c.cbegin() ? end : std::prev(it);
+        return ret;
+    };
+    if (!c.empty()) dec(it_p);
+    while (res.size() < count && (it_n != end || it_p != end)) {
+        decltype(it_n) it;
+        if (it_p == end) it = it_n++;
+        else if (it_n == end) it = dec(it_p);
+        else it = xor_closer(t, it_p->first.data(), it_n->first.data()) ? dec(it_p) : it_n++;
+        if (auto n = it->second.lock())
+            if (!n->isExpired() && !n->isClient()) res.push_back(n);
+    }
+    return res;
 }
 }  // namespace detail
 
@@ -108,7 +190,10 @@ findClosestNodesBatch(Context& ctx, const Table& table, const HashT* targets, si
     typedef typename TableSnapshot<Table, TimePoint>::NodePtr NodePtr;
     std::vector<std::vector<NodePtr>> res(q);
     if (q == 0 || count == 0) return res;
-    if (count > DHTGPU_MAX_K) throw Error(DHTGPU_EINVAL, "findClosestNodes count > DHTGPU_MAX_K");
+    if (q < ctx.min_device_batch || count > DHTGPU_MAX_K) {   // the host walk (Dispatch)
+        for (size_t i = 0; i < q; ++i) detail::find_closest_host(table, targets[i], now, count, res[i]);
+        return res;
+    }
     TableSnapshot<Table, TimePoint> snap(table, now);
     std::vector<uint8_t> t;
     t.reserve(q * DHTGPU_HASH_LEN);
@@ -126,10 +211,16 @@ findClosestNodesBatch(Context& ctx, const Table& table, const HashT* targets, si
     return res;
 }
 
-/* Drop-in for RoutingTable::findClosestNodes(id, now, count). */
+/* Drop-in for RoutingTable::findClosestNodes(id, now, count): one target is always below
+ * the device threshold, so this is the host walk (the reference's cost, no snapshot). */
 template <class Table, class HashT, class TimePoint>
 std::vector<typename TableSnapshot<Table, TimePoint>::NodePtr>
 findClosestNodes(Context& ctx, const Table& table, const HashT& id, TimePoint now, size_t count = 8) {
+    if (ctx.min_device_batch > 1) {
+        std::vector<typename TableSnapshot<Table, TimePoint>::NodePtr> res;
+        detail::find_closest_host(table, id, now, count, res);
+        return res;
+    }
     return std::move(findClosestNodesBatch(ctx, table, &id, 1, now, count)[0]);
 }
 
@@ -170,15 +261,35 @@ void getCachedNodesRaw(Context& ctx, const NodeMap& map, const HashT* targets, s
     for (size_t i = 0; i < q; ++i) out[i].assign(idx.begin() + i * count, idx.begin() + i * count + cnt[i]);
 }
 
-/* Drop-in for NodeCache::getCachedNodes(id, af, count). */
+/* NodeCache::getCachedNodes for a batch of targets.  The device path walks the map once per
+ * batch (the accept mask is evaluated at call time, as the reference does per visited entry),
+ * so it is taken only when the batch is large against the map (q >= min_device_batch and
+ * q >= map.size() / 8: the walk then costs less than 8 entries per target); otherwise each
+ * target takes the host walk, O(log N + count). */
+template <class NodeMap, class HashT>
+std::vector<std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>>>
+getCachedNodesBatch(Context& ctx, const NodeMap& map, const HashT* targets, size_t q, size_t count,
+                    uint64_t version = 0) {
+    std::vector<std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>>> res(q);
+    if (q == 0 || count == 0) return res;
+    if (q < ctx.min_device_batch || q < map.size() / 8 || count > DHTGPU_MAX_K) {
+        for (size_t i = 0; i < q; ++i) res[i] = detail::cached_nodes_host(map, targets[i], count);
+        return res;
+    }
+    std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>> locked;
+    std::vector<std::vector<uint32_t>> out;
+    getCachedNodesRaw(ctx, map, targets, q, count, locked, out, version);
+    for (size_t i = 0; i < q; ++i)
+        for (uint32_t j : out[i]) res[i].push_back(locked[j]);
+    return res;
+}
+
+/* Drop-in for NodeCache::getCachedNodes(id, af, count): one target -- the host walk, as fast
+ * as the reference body (no pass over the map, nothing uploaded). */
 template <class NodeMap, class HashT>
 std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>>
 getCachedNodes(Context& ctx, const NodeMap& map, const HashT& id, size_t count, uint64_t version = 0) {
-    std::vector<std::shared_ptr<typename NodeMap::mapped_type::element_type>> locked, res;
-    std::vector<std::vector<uint32_t>> out;
-    getCachedNodesRaw(ctx, map, &id, 1, count, locked, out, version);
-    for (uint32_t i : out[0]) res.push_back(locked[i]);
-    return res;
+    return std::move(getCachedNodesBatch(ctx, map, &id, 1, count, version)[0]);
 }
 
 /* Flat exact k-NN over a fixed id set kept resident in HBM (the batched

@@ -49,6 +49,14 @@ def test_cpp_adapter_header_compiles(tmp_path):
     assert subprocess.check_output([exe], text=True).strip() == "built"
 
 
+def test_cpp_adapter_host_walks(tmp_path):
+    """The adapter's host walks -- what a single findClosestNodes / getCachedNodes runs below the
+    device threshold -- give the oracle's nodes in the oracle's order (no GPU needed)."""
+    exe = build_adapter_check(str(tmp_path / "adapter_check"))
+    out = subprocess.run([exe, "--host"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and "0 mismatches" in out.stdout, out.stdout + out.stderr
+
+
 def build_adapter_check(exe):
     src = os.path.join(ROOT, "tests", "cpp", "adapter_check.cpp")
     libdir = os.path.dirname(opendht_amd.LIB_PATH)
