@@ -115,7 +115,7 @@ from opendht_amd import sharding  # noqa: E402
 
 METRIC = "queries/sec, k=8 XOR-NN over 16M 160-bit IDs; % HBM roofline at 1/2/4/8 GPUs"
 # int32 VALU peak: a wave64 integer VALU op issues every 4 cycles per SIMD on gfx950
-# (16 lanes/clk/SIMD): 1024 SIMDs x 16 x 2.4 GHz = 39.3 T lane-ops/s; tools/valu_peak
+# (16 lanes/clk/SIMD): 1024 SIMDs x 16 x 2.4 GHz = 39.3 T lane-ops/s; tools/experiments/valu_peak
 # measures 40.1 T on the box (profiles/r01_valu_peak.log).
 VALU_PEAK_TOPS = 1024 * 16 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0

@@ -1521,7 +1521,7 @@ WsLayout ws_layout(const BatchPlan& P, uint32_t nsub, uint32_t q, uint32_t k) {
 // turns -- one round of workgroups however large the set; when not even one ring turn fits, no
 // workgroup gets more ids than that bound.
 uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, uint32_t q_plan, int num_cus,
-                        SubDesc* d, uint32_t* seg) {
+                        SubDesc* d, uint32_t* seg, bool no_seg = false) {
     const double f = 1.0 - std::exp(-(double)q_plan / (double)(1ull << P.Lm));
     uint64_t pb_cap = 1ull << 40;   // dense mode: no cap
     if (P.sparse) {
@@ -1534,7 +1534,7 @@ uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, 
     }
     *seg = 0xFFFFFFFFu;
     constexpr uint64_t turn = (uint64_t)kRing * kF2Sub;
-    if (P.sparse && pb_cap >= turn) {
+    if (P.sparse && pb_cap >= turn && !no_seg) {   // (no_seg: more workgroups instead, in whole rounds)
         *seg = (uint32_t)std::min<uint64_t>(pb_cap / turn * turn, 0x80000000ull);
         pb_cap = 1ull << 40;
     }
@@ -1658,7 +1658,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     // (steady-state calls upload nothing)
     SubDesc hd[kMaxSubs];
     uint32_t seg = 0;
-    const uint32_t nblk2 = deal_f2_blocks(P, subs, nsub, c.q_plan, c.num_cus, hd, &seg);
+    const uint32_t nblk2 = deal_f2_blocks(P, subs, nsub, c.q_plan, c.num_cus, hd, &seg, c.f2_noseg != 0);
     if (c.f2_seg && P.sparse && seg != 0xFFFFFFFFu) {   // experiment: segments of whole ring turns
         constexpr uint32_t turn = kRing * kF2Sub;
         seg = std::max<uint32_t>(turn, c.f2_seg / turn * turn);

@@ -94,13 +94,17 @@ __global__ __launch_bounds__(256) void k_find_closest(
 }
 
 // ---------------------------------------------------------------------------------
-// K2.  HBM-streaming: each thread classifies 4 consecutive ids (5 x 16-B plane loads,
-// one 4-B bucket store).  Bucket firsts live in LDS; findBucket is a branch-light
-// binary search.  commonBits is a clz over the first nonzero xor word; the heavy
-// low bins (cb < 8 hold 255/256 of uniform ids) are counted with wave ballots, the
-// rest with LDS atomics, then one global atomic per bin per workgroup.
+// K2.  HBM-streaming: each thread classifies 4 consecutive ids per step (5 x 16-B plane
+// loads, one 4-B bucket store), with the next step's 5 loads issued before this step's
+// work (two steps in flight per lane).  The grid is a whole number of workgroups per CU
+// (kClsPerCu, all resident at once: no second round of workgroups at the end).  Bucket
+// firsts live in LDS; findBucket is a branch-light binary search.  commonBits is a clz
+// over the first nonzero xor word; the heavy low bins (cb < 8 hold 255/256 of uniform ids)
+// are counted with wave ballots, the rest with LDS atomics, then one global atomic per bin
+// per workgroup.
 // ---------------------------------------------------------------------------------
 constexpr int kClsBlock = 256;
+constexpr int kClsPerCu = 4;
 
 __global__ __launch_bounds__(kClsBlock) void k_classify(
     const uint32_t* __restrict__ planes, uint64_t stride, uint64_t n, uint32_t nb,
@@ -108,23 +112,27 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
     uint32_t m4, uint8_t* __restrict__ out_bucket, unsigned long long* __restrict__ hist) {
     __shared__ uint32_t sf[DHT_W * 256];
     __shared__ uint32_t sh[161];
+    const uint64_t n4 = (n + 3) / 4;
+    const uint64_t G = (uint64_t)gridDim.x * kClsBlock;
+    uint64_t g = (uint64_t)blockIdx.x * kClsBlock + threadIdx.x;
+    // the first step's loads ahead of the setup
+    uint4 v[DHT_W];
+#pragma unroll
+    for (int w = 0; w < DHT_W; ++w)
+        v[w] = g < n4 ? reinterpret_cast<const uint4*>(planes + (uint64_t)w * stride)[g] : make_uint4(0u, 0u, 0u, 0u);
     for (uint32_t i = threadIdx.x; i < DHT_W * nb; i += kClsBlock) sf[i] = fp[i];
     for (uint32_t i = threadIdx.x; i < 161; i += kClsBlock) sh[i] = 0;
     __syncthreads();
     const uint32_t my[DHT_W] = {m0, m1, m2, m3, m4};
     const uint32_t lane = lane_id();
     uint32_t low[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-
-    const uint64_t n4 = (n + 3) / 4;
-    for (uint64_t g = (uint64_t)blockIdx.x * kClsBlock + threadIdx.x;
-         g - threadIdx.x < n4;   // keep whole waves in the loop for the ballots
-         g += (uint64_t)gridDim.x * kClsBlock) {
+    for (; g - threadIdx.x < n4; g += G) {   // block-uniform: whole waves stay in the loop for the ballots
         const bool active = g < n4;
-        uint4 v[DHT_W];
-        if (active) {
+        const uint64_t gn = g + G;
+        uint4 nx[DHT_W];
 #pragma unroll
-            for (int w = 0; w < DHT_W; ++w) v[w] = reinterpret_cast<const uint4*>(planes + (uint64_t)w * stride)[g];
-        }
+        for (int w = 0; w < DHT_W; ++w)
+            nx[w] = gn < n4 ? reinterpret_cast<const uint4*>(planes + (uint64_t)w * stride)[gn] : make_uint4(0u, 0u, 0u, 0u);
         uint32_t packed = 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -157,6 +165,8 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
                     if (4 * g + e < n) out_bucket[4 * g + e] = (uint8_t)(packed >> (8 * e));
             }
         }
+#pragma unroll
+        for (int w = 0; w < DHT_W; ++w) v[w] = nx[w];
     }
     if (lane == 0) {
 #pragma unroll
@@ -248,8 +258,11 @@ hipError_t launch_classify(const uint32_t* planes, uint64_t stride, uint64_t n, 
                            unsigned long long* hist, hipStream_t s) {
     if (!n) return hipSuccess;
     const uint64_t n4 = (n + 3) / 4;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     uint64_t grid = (n4 + kClsBlock - 1) / kClsBlock;
-    if (grid > 256 * 8) grid = 256 * 8;
+    const uint64_t full = (uint64_t)(cus > 0 ? cus : 256) * kClsPerCu;
+    if (grid > full) grid = full;
     k_classify<<<(uint32_t)grid, kClsBlock, 0, s>>>(planes, stride, n, nb, fp, myid[0], myid[1],
                                                     myid[2], myid[3], myid[4], out_bucket, hist);
     return hipGetLastError();

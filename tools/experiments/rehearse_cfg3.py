@@ -3,12 +3,12 @@ prefix routes) on ONE GPU as a world of 1 over RCCL, so that the code path the d
 multi-GPU run takes (sub-partitioned K6 in record mode, all-gather, K3 merge; prefix shards)
 is exercised end to end before that run.  Also re-checks the merged results of the broadcast
 route on a target sample against the library's own K1 scan over the same ids.
-usage: python tools/rehearse_cfg3.py"""
+usage: python tools/experiments/rehearse_cfg3.py"""
 import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29533")
