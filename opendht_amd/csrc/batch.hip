@@ -581,6 +581,7 @@ struct F3Args {
     unsigned long long* stamps;          // dbg & 256: per-block phase timestamps [np][16]
     uint32_t spec;                       // speculative gather: slots per bucket set loaded with the counts
                                          // (<= kF3Cap / kSets; 0: counts first, then the exact gather)
+    uint32_t cap;                        // LDS stage entries (the plan's, <= kF3Cap)
 };
 
 // (w0 distance, w1 distance, index) order; words 2..4 are read only when both distances tie
@@ -721,7 +722,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     uint32_t* slow = wsum + 17;               // [kF3Threads + 1] slow-path target slots, count last
     uint32_t* ntie = slow + kF3Threads + 1;   // [0] deferred-tie slots taken, [1] wave-path targets (stat)
     uint2* S = reinterpret_cast<uint2*>(sh + f3_words(nsub));
-    uint2* T = S + kF3Cap;
+    uint2* T = S + a.cap;
     // the bitmap is no longer read in this call: clear this block's share of its sub-partition's
     for (uint32_t i = pl + a.np_sub * threadIdx.x; i < a.nwords; i += a.np_sub * kF3Threads)
         a.bitmap[sub * a.nwords + i] = 0;
@@ -785,7 +786,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     constexpr uint32_t NWV = kF3Threads / 64;
     if (Diag && (a.dbg & 32)) return;
-    if (m > kF3Cap || over) {
+    if (m > a.cap || over) {
         // strongly clustered ids: this partition's targets take the exact brute-force path
         if (threadIdx.x == 0) ntie[2] = atomicAdd(a.ctr, mt);   // one reservation for the block
         sync_lds();
@@ -973,7 +974,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                         a.out_cnt[qi] = want;
                     } else {
 #pragma unroll
-                        for (int r = 0; r < K; ++r) res[r] = (uint32_t)r < want ? S[ok[r] & (kF3Cap - 1)].y : 0u;
+                        for (int r = 0; r < K; ++r) res[r] = (uint32_t)r < want ? S[ok[r] < a.cap ? ok[r] : 0u].y : 0u;
                         if (a.gidx) {
 #pragma unroll
                             for (int r = 0; r < K; ++r) res[r] = a.gidx[res[r]];
@@ -1234,6 +1235,7 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
 
 struct BatchPlan {
     uint32_t Lm, b1, Lq, nwords, nblk1, nblk2, stage, sparse, tcap;
+    uint32_t f3cap;  // F3's LDS stage entries (kF3Cap, or the 6-sigma bound when that buys a 4th workgroup per CU)
     uint32_t scap;   // survivors per (bucket set, partition)
     uint32_t spec;   // F3's speculative slots per set (mean + 5 sigma of one set's share)
     bool fits;   // partitions' survivors fit the F3 stage on uniform ids
@@ -1282,10 +1284,12 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     // stage (an overflowing partition sends its targets to the brute force); plans that
     // cannot are refused (batch_supported), e.g. n >> 2^24 with its 256-id subtrees.
     P.fits = false;
+    double need = (double)kF3Cap;   // the partition bound the plan was accepted with
     for (;; ++b1) {
         const double sub = (double)(1ull << (P.Lm - b1)), mu = (double)n / (double)(1ull << P.Lm);
         const double mean = sub * f * mu, var = sub * f * (1.0 - f) * mu * mu + sub * f * mu;
-        if (mean + 6.0 * std::sqrt(var) + 64.0 <= (double)kF3Cap) { P.fits = true; break; }
+        need = mean + 6.0 * std::sqrt(var) + 64.0;
+        if (need <= (double)kF3Cap) { P.fits = true; break; }
         if (b1 >= 13 || b1 >= P.Lm) break;
     }
     P.b1 = b1;
@@ -1305,6 +1309,23 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     // F3 sorts by up to 1 bit below the mark level (finer candidate ranges), <= 4096 bins
     P.Lq = P.Lm + 1 < 32 ? P.Lm + 1 : 32;
     while (P.Lq > P.Lm && P.Lq - P.b1 > 12) --P.Lq;
+    // F3's LDS: four workgroups per CU (40 KB each) where the plan allows -- sort one bit less
+    // finely, and stage the plan's own 6-sigma bound instead of kF3Cap entries (a partition past
+    // it sends its targets to the exact fallback, as one past kF3Cap always did).  The cfg-3
+    // shard's plan (b1 = 8, 4096 sort bins: 52 KB) ran three per CU, 2.7 rounds of 2,048 blocks.
+    P.f3cap = kF3Cap;
+    auto lds3 = [&](uint32_t Lq, uint32_t cap) {
+        return (size_t)f3_words(1u << (Lq - P.b1)) * 4 + (size_t)(cap + kF3Threads) * 8;
+    };
+    constexpr size_t kF3Lds4 = kLdsMax / 4;
+    if (P.fits && lds3(P.Lq, P.f3cap) > kF3Lds4) {
+        const uint32_t cap6 = std::min<uint32_t>(kF3Cap, ((uint32_t)need + 63u) & ~63u);
+        for (uint32_t lq = P.Lq; lq >= P.Lm && lq > P.b1; --lq) {
+            if (lds3(lq, kF3Cap) <= kF3Lds4) { P.Lq = lq; break; }
+            if (lds3(lq, cap6) <= kF3Lds4) { P.Lq = lq; P.f3cap = cap6; break; }
+            if (lq == P.Lm) break;
+        }
+    }
     P.nwords = P.Lm >= 5 ? (1u << (P.Lm - 5)) : 1u;
     P.nblk1 = (q + kF1Threads - 1) / kF1Threads;
     // target buckets: mean + 6 sigma + 64 (uniform targets); overflow spills to F4
@@ -1342,7 +1363,7 @@ size_t f2_lds(const BatchPlan& P) {
 
 size_t f3_lds(const BatchPlan& P) {
     const uint32_t nsub = 1u << (P.Lq - P.b1);
-    return (size_t)f3_words(nsub) * 4 + (size_t)(kF3Cap + kF3Threads) * 8;
+    return (size_t)f3_words(nsub) * 4 + (size_t)(P.f3cap + kF3Threads) * 8;
 }
 
 // DHTGPU_DBG=256: per-block phase profiles of F2 and F3 from their s_memrealtime stamps
@@ -1727,7 +1748,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     // the base arguments are the whole set's: F4's scan (fallback targets) runs over all its ids
     F3Args a{pbuf, pcount, P.scap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, c.planes, c.stride,
              c.n, c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, fb_sub, pstat, tie_hdr, tie_cand, tie_cnt,
-             d_desc, np, dbg, stamps, c.f3_spec < 0 ? P.spec : (uint32_t)c.f3_spec};
+             d_desc, np, dbg, stamps, c.f3_spec < 0 ? P.spec : (uint32_t)c.f3_spec, P.f3cap};
     size_t l3 = f3_lds(P);
     if (dbg & 4096) l3 = l3 > 81920 ? l3 : 81920;   // experiment: 2 F3 blocks per CU
     if (dbg & 8192) l3 = l3 > 54000 ? l3 : 54000;   // experiment: 3 F3 blocks per CU

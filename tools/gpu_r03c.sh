@@ -2,6 +2,8 @@
 # (DHTGPU_F2NOSEG=1: more workgroups in whole rounds instead), KS timings.
 set -o pipefail
 OUT=gpurun_out/r03c; mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_scale.py tests/test_gpu_fuzz.py tests/test_gpu_parity.py::test_k6_cfg2_full_batch_vs_oracle > $OUT/t0.log 2>&1 || { tail -30 $OUT/t0.log; exit 1; }
+tail -1 $OUT/t0.log
 timeout -k 10 120 python tools/classify_probe.py > $OUT/k2.log 2>&1 || { cat $OUT/k2.log; exit 1; }
 cat $OUT/k2.log
 timeout -k 10 200 python tools/batch_probe.py --reps 10 --n 134217728 --q 131072 > $OUT/cfg3_seg.log 2>&1 || exit 1
