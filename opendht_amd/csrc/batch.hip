@@ -595,12 +595,10 @@ __device__ __forceinline__ bool key2_less(uint32_t da, uint32_t a1, uint32_t ia,
 // exact answer for one target from <= 64 candidates, one per lane (lane < mm): its rank is
 // the number of candidates strictly closer by (w0, w1) distance (full key on a double tie).
 // Word 1 and the target are loaded unconditionally (clamped), in one round trip.
-__device__ void wave_rank_answer(const F3Args& a, uint2 me, uint32_t mm, uint32_t qi, uint32_t t0, uint32_t want,
-                                 uint32_t lane) {
+// (the ranking itself, once word 1 of this lane's candidate and the target's words are loaded)
+__device__ void wave_rank_loaded(const F3Args& a, uint2 me, uint32_t mm, uint32_t qi, uint32_t t0, uint32_t want,
+                                 uint32_t lane, uint32_t w1, const uint32_t* t) {
     const bool act = lane < mm;
-    const uint32_t w1 = a.planes[a.stride + (act ? me.y : 0u)];
-    uint32_t t[DHT_W];
-    load_target(a.tp, a.ts, qi, t);
     const uint32_t md = me.x ^ t0;
     const uint32_t m1 = act ? w1 ^ t[1] : DHT_NONE;
     uint32_t rank = 0;
@@ -615,6 +613,14 @@ __device__ void wave_rank_answer(const F3Args& a, uint2 me, uint32_t mm, uint32_
     if (act && rank < want) orow[rank] = map_out(me.y, a.gidx, a.base);
     if (lane >= want && lane < a.k) orow[lane] = DHT_NONE;
     if (lane == 0) a.out_cnt[qi] = want;
+}
+
+__device__ void wave_rank_answer(const F3Args& a, uint2 me, uint32_t mm, uint32_t qi, uint32_t t0, uint32_t want,
+                                 uint32_t lane) {
+    const uint32_t w1 = a.planes[a.stride + (lane < mm ? me.y : 0u)];
+    uint32_t t[DHT_W];
+    load_target(a.tp, a.ts, qi, t);
+    wave_rank_loaded(a, me, mm, qi, t0, want, lane, w1, t);
 }
 
 // exact wave-cooperative answer for one target (ties on w0, large subtrees).  Every lane
@@ -1203,23 +1209,46 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
             if (lane >= (uint32_t)o) inc += y;
         }
         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        for (uint32_t t = wv; t < total; t += scan::WAVES) {
-            const uint32_t j = (uint32_t)__popcll(__ballot(inc <= t));   // partition j holds tie t
-            const uint32_t before = j ? (uint32_t)__builtin_amdgcn_readlane((int)inc, (int)j - 1) : 0u;
-            const uint32_t part = blockIdx.x + (j0 + j) * gridDim.x;
-            const uint32_t g = part * kTieSlots + (t - before);
-            const uint4 h = a.tie_hdr[g];
-            const uint2 c = a.tie_cand[(uint64_t)g * 64 + lane];
-            F3Args as = a;   // the partition's sub-partition: tie words and result map
-            if (a.np_sub != f.np_ties) {
-                const SubDesc d = a.subs[__builtin_amdgcn_readfirstlane(part / a.np_sub)];
-                as.planes = d.planes;
-                as.stride = d.stride;
-                as.gidx = d.gidx;
-                as.base = d.base;
+        // two ties per wave in flight: both ties' loads (header, candidates, sub-partition
+        // descriptor; then word 1 and the target) are issued before either is ranked, so a wave
+        // holding two ties pays two round trips, not four (the cfg-3 shard defers ~1.5 per wave)
+        for (uint32_t t = wv; t < total; t += 2 * scan::WAVES) {
+            const bool two = t + scan::WAVES < total;   // wave-uniform
+            uint32_t g[2], part[2];
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                const uint32_t tt = x ? (two ? t + scan::WAVES : t) : t;
+                const uint32_t j = (uint32_t)__popcll(__ballot(inc <= tt));   // partition j holds tie tt
+                const uint32_t before = j ? (uint32_t)__builtin_amdgcn_readlane((int)inc, (int)j - 1) : 0u;
+                part[x] = blockIdx.x + (j0 + j) * gridDim.x;
+                g[x] = part[x] * kTieSlots + (tt - before);
             }
-            wave_rank_answer(as, c, __builtin_amdgcn_readfirstlane(h.z), __builtin_amdgcn_readfirstlane(h.x),
-                             __builtin_amdgcn_readfirstlane(h.y), want, lane);
+            uint4 h[2];
+            uint2 c[2];
+            F3Args as[2] = {a, a};   // each partition's sub-partition: tie words and result map
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                h[x] = a.tie_hdr[g[x]];
+                c[x] = a.tie_cand[(uint64_t)g[x] * 64 + lane];
+                if (a.np_sub != f.np_ties) {
+                    const SubDesc d = a.subs[__builtin_amdgcn_readfirstlane(part[x] / a.np_sub)];
+                    as[x].planes = d.planes;
+                    as[x].stride = d.stride;
+                    as[x].gidx = d.gidx;
+                    as[x].base = d.base;
+                }
+            }
+            uint32_t mm[2], qi[2], t0[2], w1[2], tw[2][DHT_W];
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                mm[x] = __builtin_amdgcn_readfirstlane(h[x].z);
+                qi[x] = __builtin_amdgcn_readfirstlane(h[x].x);
+                t0[x] = __builtin_amdgcn_readfirstlane(h[x].y);
+                w1[x] = as[x].planes[as[x].stride + (lane < mm[x] ? c[x].y : 0u)];
+                load_target(a.tp, a.ts, qi[x], tw[x]);
+            }
+            wave_rank_loaded(as[0], c[0], mm[0], qi[0], t0[0], want, lane, w1[0], tw[0]);
+            if (two) wave_rank_loaded(as[1], c[1], mm[1], qi[1], t0[1], want, lane, w1[1], tw[1]);
         }
         if (total) {   // block-uniform: every wave has read the counts before they are cleared
             __syncthreads();
@@ -1237,7 +1266,7 @@ struct BatchPlan {
     uint32_t Lm, b1, Lq, nwords, nblk1, nblk2, stage, sparse, tcap;
     uint32_t f3cap;  // F3's LDS stage entries (kF3Cap, or the 6-sigma bound when that buys a 4th workgroup per CU)
     uint32_t scap;   // survivors per (bucket set, partition)
-    uint32_t spec;   // F3's speculative slots per set (mean + 5 sigma of one set's share)
+    uint32_t spec;   // F3's speculative slots per set (0: exact gather after the counts)
     bool fits;   // partitions' survivors fit the F3 stage on uniform ids
     uint64_t per_blk;
 };
@@ -1299,12 +1328,12 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
         const double mean = sub * f * mu, var = sub * f * (1.0 - f) * mu * mu + sub * f * mu;
         const double cap = mean + 8.0 * std::sqrt(var) + 64.0;
         P.scap = cap >= (double)kF3Cap ? kF3Cap : ((uint32_t)cap + 63u) & ~63u;
-        // F3 loads this many slots per set with the counts (one round trip); a partition with a
-        // set past it (about 1 in 10^5 per set at 5 sigma) takes the exact second gather.  A fixed
-        // 512 fetched 2x the survivor bytes at cfg 2 and 5x at the cfg-3 shard (PMC, round 2)
-        const double sp = mean + 5.0 * std::sqrt(var) + 32.0;
-        const uint32_t half = kF3Cap / kSets;
-        P.spec = sp >= (double)half ? half : ((uint32_t)sp + 63u) & ~63u;
+        // F3's speculative gather (slots per set loaded with the counts, one round trip) is off:
+        // the exact gather after the counts fetches the survivors' bytes only (PMC at cfg 2:
+        // 18.5 MB against 19.7 MB algorithmic; the fixed 512 slots of round 2 fetched 40 MB) and
+        // measured no slower (cfg-2 step 37.7-38.1 us against 38.3-38.4 with the planned mean +
+        // 5 sigma, F3 15.4 against 15.8 us).  DHTGPU_F3SPEC sets a slot count for experiments.
+        P.spec = 0;
     }
     // F3 sorts by up to 1 bit below the mark level (finer candidate ranges), <= 4096 bins
     P.Lq = P.Lm + 1 < 32 ? P.Lm + 1 : 32;
@@ -1779,7 +1808,9 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     // context's last completed call listed no target (a hint F4 leaves in mapped host memory;
     // read without a sync, so possibly a call or two old), the full grid otherwise (the
     // fallback scan's parallelism).  Measured at three in flight: step -1.3 µs, latency +1.5.
-    const uint32_t nfb = (c.fb_hint && *c.fb_hint == 0u) ? kFbBlocks / 2 : kFbBlocks;
+    // (a sub-partitioned call fills the chip alone and defers ~1 tie per partition over 2,048+
+    // partitions: the full grid keeps them at about one per wave)
+    const uint32_t nfb = (c.fb_hint && *c.fb_hint == 0u && nsub == 1) ? kFbBlocks / 2 : kFbBlocks;
     const FbArgs fa{fb_rec, fb_done, nfb, NP, c.fb_hint_dev};
     const dim3 g4(nfb), b4(kF4Threads);
     if (k <= 8) go(3, k_f4<8>, g4, b4, 0, a, fa);
