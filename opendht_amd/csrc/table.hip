@@ -141,14 +141,21 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
             uint32_t id[DHT_W];
 #pragma unroll
             for (int w = 0; w < DHT_W; ++w) id[w] = e == 0 ? v[w].x : e == 1 ? v[w].y : e == 2 ? v[w].z : v[w].w;
+            // findBucket by binary search on word 0 of the firsts; words 1..4 only when word 0
+            // ties (a first shares the id's top 32 bits: rare)
             uint32_t j = 0;
             for (uint32_t step = 128; step; step >>= 1) {
                 const uint32_t c = j + step;
                 if (c < nb) {
-                    uint32_t f[DHT_W];
+                    const uint32_t f0 = sf[c];
+                    bool le = f0 < id[0];
+                    if (f0 == id[0]) {
+                        uint32_t f[DHT_W];
 #pragma unroll
-                    for (int w = 0; w < DHT_W; ++w) f[w] = sf[w * nb + c];
-                    if (lex_le(f, id)) j = c;
+                        for (int w = 0; w < DHT_W; ++w) f[w] = sf[w * nb + c];
+                        le = lex_le(f, id);
+                    }
+                    if (le) j = c;
                 }
             }
             packed |= j << (8 * e);
