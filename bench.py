@@ -158,9 +158,9 @@ def parse():
                     help="prefix route only: run rank --simulate-rank of a world of this size on one GPU")
     ap.add_argument("--simulate-rank", type=int, default=0)
     ap.add_argument("--cpu-targets", type=int, default=256, help="cpu_baseline sample (targets, all host threads)")
-    ap.add_argument("--cpu-threads", type=int, default=usable_cpus(),
-                    help="cpu_baseline threads (default: every CPU this process may use -- its affinity set capped "
-                         "by the cgroup CPU quota; the single-core figures are reported too)")
+    ap.add_argument("--cpu-threads", type=int, default=os.cpu_count() or 1,
+                    help="cpu_baseline threads (default: every host CPU, nproc; the rate at the job's cgroup CPU "
+                         "quota and the single-core figures are reported too)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra legs (small batch, cfg 1/3/4/5)")
     ap.add_argument("--no-scan", action="store_true", help="skip the reference K1 scan measurement")
@@ -660,7 +660,7 @@ def main():
                 cb, want = cpu_baseline(O, ids, tg, a)
                 res["cpu_baseline"] = cb
             else:
-                want, _ = O.topk(ids, tg, a.k, threads=a.cpu_threads)
+                want, _ = O.topk(ids, tg, a.k, threads=usable_cpus())
             res["verified_targets"] = int(nv)
             res["verified_exact"] = bool(np.array_equal(got_idx[:nv], want))
             progress("verified")
@@ -782,7 +782,7 @@ def cfg3_shard_leg(a, L, dev, stream, tstream):
             O = oracle()
             rows = np.arange(0, q, q // 16)
             got = outs[(steps - 1) % 2][0].cpu().numpy().view(np.uint32)[rows]
-            want, _ = O.topk(O.gen_ids(a.seed + 3, n), O.gen_ids(a.seed + 4, q)[rows], k, threads=a.cpu_threads)
+            want, _ = O.topk(O.gen_ids(a.seed + 3, n), O.gen_ids(a.seed + 4, q)[rows], k, threads=usable_cpus())
             res["verified_targets"] = int(rows.size)
             res["verified_exact"] = bool(np.array_equal(got, want))
         return res
@@ -972,13 +972,15 @@ def cpu_baseline(O, ids, tg, a):
           "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), **cpu_share(),
           "compiler": "g++ -O2 (the reference's Release)",
           "one_core": {"value": m1 / dt1, "unit": "queries/s", "sample": f"{m1} targets, {dt1:.2f} s"}}
-    if cb["host_cpus"] and cb["host_cpus"] > a.cpu_threads:
-        # the job may use a.cpu_threads CPUs of the host's host_cpus (cgroup quota): the whole
-        # host's rate is not measurable here; a linear scaling in cores is its upper bound
-        cb["whole_host_upper_bound"] = {
-            "value": cb["value"] * cb["host_cpus"] / a.cpu_threads, "unit": "queries/s", "cores": cb["host_cpus"],
-            "basis": f"measured {a.cpu_threads}-CPU rate x {cb['host_cpus']}/{a.cpu_threads} (linear in cores: an upper "
-                     f"bound -- std::partial_sort over the 335 MB set is memory-bound at a few threads, SURVEY 8(d))"}
+    uq = usable_cpus()
+    if uq < a.cpu_threads:
+        # the job's cgroup quota / affinity lets it run uq CPUs at once: nproc threads time-slice
+        # over them, so the same sample at uq threads is reported beside it
+        t0 = time.perf_counter()
+        O.topk(ids, tg, a.k, threads=uq)
+        dq = time.perf_counter() - t0
+        cb["at_cpu_quota"] = {"value": tg.shape[0] / dq, "unit": "queries/s", "cores": uq,
+                              "note": "threads = the CPUs the job may run at once (affinity capped by the cgroup quota)"}
     # the same port built with g++ -O3 -march=native on this host
     try:
         with O.native():
