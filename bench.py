@@ -696,6 +696,8 @@ def small_batch_leg(ctx, tp, ts, n, k, stream, tstream, dev):
         kms = ev.mean_ms()
         row["kernels_ms"] = {"k_s1_filter": kms[1], "k_s2_answer (prefix answers + fallback scan roles)": kms[2]}
         row["s1_frac"] = 4 * n / (kms[1] * 1e-3) / 1e9 / HBM_PEAK_GBS
+        # rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes of tools/small_probe.py (profiles/r03)
+        row["pmc_traffic_bytes_per_launch"] = {kn: pmc_traffic(f"ks:{n}x{q}x{k}", kn) for kn in ("k_s1_filter", "k_s2_answer")}
         out[f"q{q}"] = row
     out["note"] = ("id set L3-resident (the cfg-2 set); w0_frac = the 4 B/id w0 stream over the whole call's "
                    "time; s1_frac = the same bytes over the S1 kernel alone")
@@ -816,7 +818,8 @@ def cfg4_leg(a, L, dev, stream, tstream):
         b = 21 * n
         return {"workload": f"{n} ids vs one local id, {nb} routing buckets", "ms": ms, "ids_per_s": n / (ms * 1e-3),
                 "roofline": {"bound": "hbm", "achieved": b / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "alg_bytes": b},
+                             "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "alg_bytes": b,
+                             "traffic": pmc_traffic(f"cfg4:{n}", "k_classify")},
                 "hist_total": int(hist.sum().item())}
     finally:
         c.close()
