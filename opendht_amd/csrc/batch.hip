@@ -252,8 +252,28 @@ struct F2Args {
 // consecutive addresses of its bucket pbuf[p][...], whose slots one returning global
 // atomic per partition reserved.  A partition that outgrows pcap keeps counting (F3 then
 // sends its targets to the fallback).
+// Narrow stage (kF2Narrow: a workgroup's ids span < 2^16): the stage is two arrays, word 0
+// [a.stage] u32 then the id's offset from the workgroup's first id [a.stage] u16 -- 6 B per
+// entry instead of 8, so F2's LDS leaves room for an F3 workgroup of another batch on its CU.
 constexpr uint32_t kStagePer = (kStage + 1023) / 1024;
-__device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* hist, uint32_t* wsum, uint32_t poff) {
+template <bool Narrow>
+__device__ __forceinline__ uint2 stage_get(const uint2* stage, uint32_t cap, uint32_t ibase, uint32_t j) {
+    if (!Narrow) return stage[j];
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(stage);
+    const uint16_t* si = reinterpret_cast<const uint16_t*>(sw + cap);
+    return make_uint2(sw[j], ibase + si[j]);
+}
+template <bool Narrow>
+__device__ __forceinline__ void stage_put(uint2* stage, uint32_t cap, uint32_t ibase, uint32_t j, uint32_t w, uint32_t i) {
+    if (!Narrow) { stage[j] = make_uint2(w, i); return; }
+    uint32_t* sw = reinterpret_cast<uint32_t*>(stage);
+    uint16_t* si = reinterpret_cast<uint16_t*>(sw + cap);
+    sw[j] = w;
+    si[j] = (uint16_t)(i - ibase);
+}
+template <bool Narrow>
+__device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* hist, uint32_t* wsum, uint32_t poff,
+                         uint32_t ibase) {
     const uint32_t np = 1u << a.b1;
     if (a.dbg & 128) { sync_lds(); return; }
     for (uint32_t i = threadIdx.x; i <= np; i += kF2Threads) hist[i] = 0;
@@ -264,7 +284,7 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
     for (uint32_t r = 0; r < kStagePer; ++r) {
         const uint32_t j = r * kF2Threads + threadIdx.x;
         if (j < cnt) {
-            e[r] = stage[j];
+            e[r] = stage_get<Narrow>(stage, a.stage, ibase, j);
             rk[r] = atomicAdd(hist + top_bits(e[r].x, a.b1), 1u);
         }
     }
@@ -284,7 +304,7 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
 #pragma unroll
     for (uint32_t r = 0; r < kStagePer; ++r) {
         const uint32_t j = r * kF2Threads + threadIdx.x;
-        if (j < cnt) stage[hist[top_bits(e[r].x, a.b1)] + rk[r]] = e[r];
+        if (j < cnt) stage_put<Narrow>(stage, a.stage, ibase, hist[top_bits(e[r].x, a.b1)] + rk[r], e[r].x, e[r].y);
     }
     // wsum is free again: reuse the stage-local starts to turn reservations into deltas
     // (bucket offset of stage position j = res[p] - start[p] + j)
@@ -304,7 +324,7 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
     F2_STAMP(4);
     if (!(a.dbg & 2)) {
         for (uint32_t j = threadIdx.x; j < cnt; j += kF2Threads) {
-            const uint2 x = stage[j];
+            const uint2 x = stage_get<Narrow>(stage, a.stage, ibase, j);
             const uint32_t p = top_bits(x.x, a.b1);
             const uint32_t pos = hist[p] + j;
             if (pos < a.pcap) a.pbuf[(uint64_t)((poff + p) * kSets + set) * a.pcap + pos] = x;
@@ -344,13 +364,16 @@ __device__ __forceinline__ uint4 f2_load1(__amdgpu_buffer_rsrc_t rs, uint32_t lo
 // VGPRs, the whole register file at 16 waves per CU, where kF2Sparse needs 68 and leaves
 // room for the other stream's F1 / F4 waves); kF2Stream is the streaming-only
 // ablation (DHTGPU_DBG & 64).
-constexpr uint32_t kF2Dense = 0, kF2Sparse = 1, kF2Stream = 2, kF2Seg = 3;
+// kF2Narrow is kF2Sparse over the 6-B narrow stage (a workgroup's range < 2^16 ids).
+constexpr uint32_t kF2Dense = 0, kF2Sparse = 1, kF2Stream = 2, kF2Seg = 3, kF2Narrow = 4;
 
 // Subs: several sub-partitions (descriptors read from memory, ring through buffer loads); the
 // one-set instantiation takes its descriptor from the kernel arguments and streams with plain
 // global loads
 template <uint32_t Mode, bool Subs>
 __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
+    constexpr bool Narrow = Mode == kF2Narrow;
+    constexpr bool Sparse = Mode == kF2Sparse || Mode == kF2Seg || Narrow;
     extern __shared__ uint32_t sh[];   // (32 spare) | misc[8] | bm[nwords] | hist[np + 1] | wsum[17] | lost[np/32 + 1] | stage
     const uint32_t np = 1u << a.b1;
     uint32_t* misc = sh + 28;
@@ -419,7 +442,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
         if (Mode == kF2Seg && c0 != lo && (c0 - lo) % a.seg == 0) {
             // segment boundary (block-uniform): flush while the ring's next loads are in flight
             sync_lds();
-            f2_flush(a, misc[0] < a.stage ? misc[0] : a.stage, stage, hist, wsum, poff);
+            f2_flush<false>(a, misc[0] < a.stage ? misc[0] : a.stage, stage, hist, wsum, poff, 0u);
             if (threadIdx.x == 0) misc[0] = 0;
             sync_lds();
         }
@@ -430,7 +453,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                 cnt += ring[r].x ^ ring[r].y ^ ring[r].z ^ ring[r].w;
             } else if (sb < hi) {   // block-uniform
                 if (Mode == kF2Dense && cnt > a.stage - kF2Sub) {
-                    f2_flush(a, cnt, stage, hist, wsum, poff);
+                    f2_flush<false>(a, cnt, stage, hist, wsum, poff, 0u);
                     cnt = 0;
                 }
                 const uint32_t j0 = sb + 4 * threadIdx.x;
@@ -467,7 +490,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                         if (sv[f]) {
                             const uint32_t at = __builtin_amdgcn_mbcnt_hi(
                                 (uint32_t)(bal[f] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[f], pos));
-                            stage[at] = make_uint2(v4[f], j0 + f);
+                            stage_put<Narrow>(stage, a.stage, lo, at, v4[f], j0 + f);
                         }
                         pos += (uint32_t)__popcll(bal[f]);
                     }
@@ -482,7 +505,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                             const uint32_t at = __builtin_amdgcn_mbcnt_hi(
                                 (uint32_t)(bal[f] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[f], pos));
                             if (at < a.stage) {
-                                stage[at] = make_uint2(v4[f], j0 + f);
+                                stage_put<Narrow>(stage, a.stage, lo, at, v4[f], j0 + f);
                             } else {
                                 const uint32_t p = top_bits(v4[f], a.b1);
                                 atomicOr(lost + (p >> 5), 1u << (p & 31));
@@ -500,13 +523,13 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
         }
     }
     if (Mode == kF2Stream) { if (cnt == 0x12345678u) a.ctr[4] = cnt; return; }
-    if (Mode == kF2Sparse || Mode == kF2Seg) {
+    if (Sparse) {
         sync_lds();
         cnt = misc[0] < a.stage ? misc[0] : a.stage;
     }
     F2_STAMP(2);
-    if (cnt) f2_flush(a, cnt, stage, hist, wsum, poff);
-    if (Mode == kF2Sparse || Mode == kF2Seg) {   // partitions that lost entries: count past any stage (F3 -> fallback)
+    if (cnt) f2_flush<Narrow>(a, cnt, stage, hist, wsum, poff, lo);
+    if (Sparse) {   // partitions that lost entries: count past any stage (F3 -> fallback)
         for (uint32_t i = threadIdx.x; i <= np / 32; i += kF2Threads) {
             uint32_t m = lost[i];
             while (m) {
@@ -1264,6 +1287,7 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
 
 struct BatchPlan {
     uint32_t Lm, b1, Lq, nwords, nblk1, nblk2, stage, sparse, tcap;
+    uint32_t nstage; // F2's narrow stage entries (6 B each; 0: none) -- F2 then leaves room for an F3 workgroup
     uint32_t f3cap;  // F3's LDS stage entries (kF3Cap, or the 6-sigma bound when that buys a 4th workgroup per CU)
     uint32_t scap;   // survivors per (bucket set, partition)
     uint32_t spec;   // F3's speculative slots per set (0: exact gather after the counts)
@@ -1347,8 +1371,8 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
         return (size_t)f3_words(1u << (Lq - P.b1)) * 4 + (size_t)(cap + kF3Threads) * 8;
     };
     constexpr size_t kF3Lds4 = kLdsMax / 4;
+    const uint32_t cap6 = std::min<uint32_t>(kF3Cap, ((uint32_t)need + 63u) & ~63u);
     if (P.fits && lds3(P.Lq, P.f3cap) > kF3Lds4) {
-        const uint32_t cap6 = std::min<uint32_t>(kF3Cap, ((uint32_t)need + 63u) & ~63u);
         for (uint32_t lq = P.Lq; lq >= P.Lm && lq > P.b1; --lq) {
             if (lds3(lq, kF3Cap) <= kF3Lds4) { P.Lq = lq; break; }
             if (lds3(lq, cap6) <= kF3Lds4) { P.Lq = lq; P.f3cap = cap6; break; }
@@ -1383,11 +1407,32 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
         }
         if (pb == kF2Step) break;
     }
+    // F2's narrow stage (6 B per entry: ranges < 2^16 ids, the cfg-2 shape): sized so that F2
+    // plus one F3 workgroup fit a CU's LDS -- the F2 of one batch in flight and the F3 of another
+    // then share CUs instead of waiting for each other's workgroups to drain.  F3 stages its
+    // plan's own 6-sigma bound where that is what makes the pair fit (a partition past it sends
+    // its targets to the exact fallback, as one past kF3Cap does).  1 KB of margin per kernel
+    // for the LDS allocation granule.
+    P.nstage = 0;
+    if (P.sparse && P.per_blk <= 65536) {
+        const double mean = (double)P.per_blk * f, sd = std::sqrt(mean * (1.0 - f));
+        const double need2 = mean + 8.0 * sd + 256.0;
+        for (int pass = 0; pass < 2 && !P.nstage; ++pass) {
+            if (pass == 1) {
+                if (!P.fits || cap6 >= P.f3cap) break;
+                P.f3cap = cap6;
+            }
+            const size_t f3l = (lds3(P.Lq, P.f3cap) + 1023) & ~(size_t)1023;
+            if (fixed + f3l + 1024 >= kLdsMax) continue;
+            const size_t room6 = (kLdsMax - f3l - fixed - 1024) / 6;
+            if ((double)room6 >= need2) P.nstage = (uint32_t)std::min<size_t>(room6, kStage) & ~1u;
+        }
+    }
     return P;
 }
 
-size_t f2_lds(const BatchPlan& P) {
-    return (size_t)f2_fixed_words(P.nwords, 1u << P.b1) * 4 + (size_t)P.stage * 8;
+size_t f2_lds(const BatchPlan& P, bool narrow = false) {
+    return (size_t)f2_fixed_words(P.nwords, 1u << P.b1) * 4 + (narrow ? (size_t)P.nstage * 6 : (size_t)P.stage * 8);
 }
 
 size_t f3_lds(const BatchPlan& P) {
@@ -1504,6 +1549,7 @@ void set_lds_attributes() {
                         (const void*)k_f2_filter<kF2Stream, false>, (const void*)k_f2_filter<kF2Seg, false>,
                         (const void*)k_f2_filter<kF2Dense, true>, (const void*)k_f2_filter<kF2Sparse, true>,
                         (const void*)k_f2_filter<kF2Stream, true>, (const void*)k_f2_filter<kF2Seg, true>,
+                        (const void*)k_f2_filter<kF2Narrow, false>, (const void*)k_f2_filter<kF2Narrow, true>,
                         (const void*)k_f3_answer<8, false, true, false>,  (const void*)k_f3_answer<16, false, true, false>,
                         (const void*)k_f3_answer<32, false, true, false>, (const void*)k_f3_answer<8, true, true, false>,
                         (const void*)k_f3_answer<16, true, true, false>,  (const void*)k_f3_answer<32, true, true, false>,
@@ -1716,6 +1762,16 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     bool seg_used = false;   // some workgroup's range spans more than one segment
     for (uint32_t i = 0; i < nsub; ++i) seg_used = seg_used || (hd[i].nblk && hd[i].per_blk > seg);
     if (nblk2 > kMaxF2Blocks) return hipErrorInvalidValue;
+    // the narrow stage: every workgroup's range under 2^16 ids and its survivors (mean + 8 sigma
+    // + 256 on uniform ids) within the narrow stage; no segments
+    bool narrow = P.nstage && P.sparse && !seg_used && !c.f2_wide && !(dbg & 64);
+    {
+        const double f = 1.0 - std::exp(-(double)c.q_plan / (double)(1ull << P.Lm));
+        for (uint32_t i = 0; i < nsub && narrow; ++i) {
+            const double mean = (double)hd[i].per_blk * f, sd = std::sqrt(mean * (1.0 - f));
+            if (hd[i].nblk && (hd[i].per_blk > 65536 || mean + 8.0 * sd + 256.0 > (double)P.nstage)) narrow = false;
+        }
+    }
     if (NP > 8192 || nblk2 > 8192) dbg &= ~256u;   // phase stamps hold 8192 workgroups per kernel
     if (nsub > 1) {
         uint64_t sig = 1469598103934665603ull;
@@ -1750,16 +1806,17 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
                     bitmap, tcount, tbuf, P.tcap, ctr, tspill};
     go(0, k_f1_targets, dim3((q + kF1Threads - 1) / kF1Threads), dim3(kF1Threads), 0, a1);
     if (nblk2) {
-        F2Args a2{d_desc, d_blk, hd[0], nsub, NP, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, P.scap, ctr, P.stage, dbg, P.sparse, seg,
-                  stamps ? stamps + 8192 * 16 : nullptr};
+        F2Args a2{d_desc, d_blk, hd[0], nsub, NP, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, P.scap, ctr,
+                  narrow ? P.nstage : P.stage, dbg, P.sparse, seg, stamps ? stamps + 8192 * 16 : nullptr};
         const dim3 g2(nblk2), b2(kF2Threads);
-        const size_t l2 = f2_lds(P);
+        const size_t l2 = f2_lds(P, narrow);
 #define F2_GO(MM)                                                    \
     do {                                                             \
         if (nsub > 1) go(1, k_f2_filter<MM, true>, g2, b2, l2, a2);  \
         else go(1, k_f2_filter<MM, false>, g2, b2, l2, a2);          \
     } while (0)
         if (dbg & 64) F2_GO(kF2Stream);
+        else if (narrow) F2_GO(kF2Narrow);
         else if (P.sparse && seg_used) F2_GO(kF2Seg);
         else if (P.sparse) F2_GO(kF2Sparse);
         else F2_GO(kF2Dense);

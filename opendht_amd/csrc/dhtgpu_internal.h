@@ -124,6 +124,7 @@ struct BatchCall {
     uint32_t f2_seg;                       // F2 sparse-mode segment override in ids (0: the plan's)
     int32_t f3_spec;                       // F3 speculative slots per bucket set (< 0: the plan's; 0: exact gather)
     uint32_t f2_noseg;                     // experiment: never segment F2's ranges (more workgroups, whole rounds)
+    uint32_t f2_wide;                      // experiment: F2's 8-B stage where the 6-B narrow one fits
     const volatile uint32_t* fb_hint;      // nullable: the slot's last fallback-list length (mapped host memory)
     uint32_t* fb_hint_dev;                 // its device address (F4 writes it)
     unsigned long long* stamps;            // dbg & 256: phase stamps [2 * 8192 * 16]
