@@ -20,7 +20,8 @@ import numpy as np
 
 __all__ = ["Context", "DhtGpuError", "NONE", "MAX_K", "lib", "LIB_PATH", "id_words"]
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdhtgpu.so")
+# DHTGPU_LIB: another build of the same library (A/B experiments, tools/gpu_ab_lib.sh)
+LIB_PATH = os.environ.get("DHTGPU_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdhtgpu.so")
 NONE = 0xFFFFFFFF
 MAX_K = 32
 # status codes (include/dhtgpu.h)
