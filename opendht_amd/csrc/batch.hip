@@ -216,7 +216,7 @@ __global__ __launch_bounds__(kF1Threads) void k_f1_targets(F1Args a) {
 
 // ---- F2: stream w0, keep ids in marked subtrees, partition them ----------------------
 // Persistent: one workgroup per CU, each owning a contiguous id range streamed through
-// a ring of kRing 16-B loads per lane (128 KB in flight per CU).  Survivors are appended
+// a ring of kF2Ring 16-B loads per lane (64 KB in flight per CU).  Survivors are appended
 // to an LDS stage; when the stage could overflow (and at the end) it is flushed into the
 // partition-major survivor buckets pbuf[p][...] (see f2_flush).
 constexpr int kF2Threads = 1024;
@@ -336,7 +336,11 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
 // Loads are unconditional 16-B loads (no data-dependent branches, so every load of the
 // ring stays in flight): addresses past the id range are clamped into the plane
 // allocation and their words are masked by the caller's range test.
-constexpr uint32_t kRing = 8;
+constexpr uint32_t kRing = 8;     // S1's ring (two 512-thread workgroups per CU: 64 KB each)
+// F2's ring: 4 sub-steps = 64 KB in flight per CU.  A pure 64 MB stream by one 1024-thread
+// workgroup per CU (tools/experiments/stream_probe.hip, profiles/r03/experiments) takes
+// 13.4 us with 8 (128 KB in flight), 11.7 us with 4: the deeper ring only queues longer
+constexpr uint32_t kF2Ring = 4;
 // The ring loads are buffer loads through a descriptor based at the workgroup's first id
 // (f2_rsrc): the plane pointers come from sub-partition descriptors in memory, whose address
 // space the compiler cannot infer -- plain loads through them are FLAT loads, which also count
@@ -418,15 +422,15 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     } else {
         for (uint32_t i = threadIdx.x; i < a.nwords; i += kF2Threads) bm[i] = bsrc[i];
     }
-    // ring of kRing sub-steps (one 16-B load per lane each) in flight: 128 KB per CU.
+    // ring of kF2Ring sub-steps (one 16-B load per lane each) in flight: 64 KB per CU.
     // Loads past the block's range are clamped to its last 16 B (cache hits, masked).
     // (the ring's first loads take most of this phase's ~4 µs: all CUs start their streams at
     // once; the 64 KB bitmap copy alone is ~1 µs)
     const uint32_t lim = min(d.lim, ((hi + 3u) & ~3u) - 4u);
     const __amdgpu_buffer_rsrc_t rs = f2_rsrc(w0, lo, lim);
-    uint4 ring[kRing];
+    uint4 ring[kF2Ring];
 #pragma unroll
-    for (uint32_t r = 0; r < kRing; ++r)
+    for (uint32_t r = 0; r < kF2Ring; ++r)
         ring[r] = Subs ? f2_load1(rs, lo, lo + r * kF2Sub, lim) : f2_load1g(w0, lo + r * kF2Sub, lim);
     if (threadIdx.x < 3) misc[threadIdx.x] = 0;
     for (uint32_t i = threadIdx.x; i <= np / 32; i += kF2Threads) lost[i] = 0;
@@ -438,7 +442,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     // (before its barrier), when every read of its previous use (sub-step s - 2) is complete.
     // Sparse mode: one counter misc[0] for the whole block, read after the final barrier.
     uint32_t cnt = 0, s3 = 0;
-    for (uint32_t c0 = lo; c0 < hi; c0 += kRing * kF2Sub) {
+    for (uint32_t c0 = lo; c0 < hi; c0 += kF2Ring * kF2Sub) {
         if (Mode == kF2Seg && c0 != lo && (c0 - lo) % a.seg == 0) {
             // segment boundary (block-uniform): flush while the ring's next loads are in flight
             sync_lds();
@@ -447,7 +451,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
             sync_lds();
         }
 #pragma unroll
-        for (uint32_t r = 0; r < kRing; ++r) {
+        for (uint32_t r = 0; r < kF2Ring; ++r) {
             const uint32_t sb = c0 + r * kF2Sub;
             if (Mode == kF2Stream) {
                 cnt += ring[r].x ^ ring[r].y ^ ring[r].z ^ ring[r].w;
@@ -519,7 +523,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                     cnt += misc[s3 == 0 ? 2u : s3 - 1];
                 }
             }
-            ring[r] = Subs ? f2_load1(rs, lo, sb + kRing * kF2Sub, lim) : f2_load1g(w0, sb + kRing * kF2Sub, lim);
+            ring[r] = Subs ? f2_load1(rs, lo, sb + kF2Ring * kF2Sub, lim) : f2_load1g(w0, sb + kF2Ring * kF2Sub, lim);
         }
     }
     if (Mode == kF2Stream) { if (cnt == 0x12345678u) a.ctr[4] = cnt; return; }
@@ -1629,7 +1633,7 @@ uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, 
         }
     }
     *seg = 0xFFFFFFFFu;
-    constexpr uint64_t turn = (uint64_t)kRing * kF2Sub;
+    constexpr uint64_t turn = (uint64_t)kF2Ring * kF2Sub;
     if (P.sparse && pb_cap >= turn && !no_seg) {   // (no_seg: more workgroups instead, in whole rounds)
         *seg = (uint32_t)std::min<uint64_t>(pb_cap / turn * turn, 0x80000000ull);
         pb_cap = 1ull << 40;
@@ -1756,7 +1760,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     uint32_t seg = 0;
     const uint32_t nblk2 = deal_f2_blocks(P, subs, nsub, c.q_plan, c.num_cus, hd, &seg, c.f2_noseg != 0);
     if (c.f2_seg && P.sparse && seg != 0xFFFFFFFFu) {   // experiment: segments of whole ring turns
-        constexpr uint32_t turn = kRing * kF2Sub;
+        constexpr uint32_t turn = kF2Ring * kF2Sub;
         seg = std::max<uint32_t>(turn, c.f2_seg / turn * turn);
     }
     bool seg_used = false;   // some workgroup's range spans more than one segment
