@@ -216,7 +216,7 @@ __global__ __launch_bounds__(kF1Threads) void k_f1_targets(F1Args a) {
 
 // ---- F2: stream w0, keep ids in marked subtrees, partition them ----------------------
 // Persistent: one workgroup per CU, each owning a contiguous id range streamed through
-// a ring of kF2Ring 16-B loads per lane (64 KB in flight per CU).  Survivors are appended
+// a ring of kF2Ring 16-B loads per lane (32 KB in flight per CU).  Survivors are appended
 // to an LDS stage; when the stage could overflow (and at the end) it is flushed into the
 // partition-major survivor buckets pbuf[p][...] (see f2_flush).
 constexpr int kF2Threads = 1024;
@@ -337,10 +337,11 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
 // ring stays in flight): addresses past the id range are clamped into the plane
 // allocation and their words are masked by the caller's range test.
 constexpr uint32_t kRing = 8;     // S1's ring (two 512-thread workgroups per CU: 64 KB each)
-// F2's ring: 4 sub-steps = 64 KB in flight per CU.  A pure 64 MB stream by one 1024-thread
+// F2's ring: 2 sub-steps = 32 KB in flight per CU.  A pure 64 MB stream by one 1024-thread
 // workgroup per CU (tools/experiments/stream_probe.hip, profiles/r03/experiments) takes
-// 13.4 us with 8 (128 KB in flight), 11.7 us with 4: the deeper ring only queues longer
-constexpr uint32_t kF2Ring = 4;
+// 13.3 us with 8 (128 KB in flight), 11.7 with 4, 11.1 with 3, 10.3 with 2: a deeper ring only
+// queues longer.  F2 at cfg 2: 21.9 us with 4, 21.3 with 3, 20.7 with 2 (round 2: 8, 24.1 us)
+constexpr uint32_t kF2Ring = 2;
 // The ring loads are buffer loads through a descriptor based at the workgroup's first id
 // (f2_rsrc): the plane pointers come from sub-partition descriptors in memory, whose address
 // space the compiler cannot infer -- plain loads through them are FLAT loads, which also count
@@ -422,7 +423,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     } else {
         for (uint32_t i = threadIdx.x; i < a.nwords; i += kF2Threads) bm[i] = bsrc[i];
     }
-    // ring of kF2Ring sub-steps (one 16-B load per lane each) in flight: 64 KB per CU.
+    // ring of kF2Ring sub-steps (one 16-B load per lane each) in flight: 32 KB per CU.
     // Loads past the block's range are clamped to its last 16 B (cache hits, masked).
     // (the ring's first loads take most of this phase's ~4 µs: all CUs start their streams at
     // once; the 64 KB bitmap copy alone is ~1 µs)

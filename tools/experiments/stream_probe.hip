@@ -90,6 +90,11 @@ int main() {
         printf("plane %llu MB, %d CUs\n", (unsigned long long)(bytes >> 20), cus);
         ring_case<1024, 8>(p, n16, out, cus, 1);
         ring_case<1024, 4>(p, n16, out, cus, 1);
+        ring_case<1024, 3>(p, n16, out, cus, 1);
+        ring_case<1024, 2>(p, n16, out, cus, 1);
+        ring_case<512, 4>(p, n16, out, cus, 1);
+        ring_case<512, 8>(p, n16, out, cus, 1);
+        ring_case<768, 4>(p, n16, out, cus, 1);
         ring_case<1024, 16>(p, n16, out, cus, 1);
         ring_case<512, 8>(p, n16, out, cus, 2);
         ring_case<512, 4>(p, n16, out, cus, 2);
