@@ -88,9 +88,12 @@ def maybe_launch(argv):
         print(f"[bench] --gpus {a.gpus}: launching {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
         return subprocess.call(cmd)
     if a.dry_run or a.dry_run_ranks:
-        print(json.dumps({"mode": "rank" if env_world is not None else "single", "gpus": a.gpus,
-                          "world_size": int(env_world or 1), "rank": int(os.environ.get("RANK", "0")),
-                          "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}))
+        # one write of line + newline: the ranks share the launcher's stdout pipe, and a write
+        # under PIPE_BUF bytes is atomic there (print's separate newline write could interleave)
+        line = json.dumps({"mode": "rank" if env_world is not None else "single", "gpus": a.gpus,
+                           "world_size": int(env_world or 1), "rank": int(os.environ.get("RANK", "0")),
+                           "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}) + "\n"
+        os.write(sys.stdout.fileno(), line.encode())
         return 0
     return None
 
