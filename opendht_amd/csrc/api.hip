@@ -2,6 +2,7 @@
 // stream; converts between the boundary's 20-byte big-endian ids and the device
 // word-plane layout; never throws across the ABI.
 #include <hip/hip_runtime.h>
+#include <cstdio>
 
 #include <algorithm>
 #include <cstring>
@@ -42,10 +43,19 @@ int map_err(hipError_t e) {
     return DHTGPU_EDEVICE;
 }
 
-#define DHT_TRY(expr)                                 \
-    do {                                              \
-        hipError_t _e = (expr);                       \
-        if (_e != hipSuccess) return map_err(_e);     \
+// DHTGPU_VERBOSE: name the failing HIP call on stderr (diagnostics; read once)
+bool verbose() {
+    static const bool v = getenv("DHTGPU_VERBOSE") != nullptr;
+    return v;
+}
+
+#define DHT_TRY(expr)                                                                                  \
+    do {                                                                                               \
+        hipError_t _e = (expr);                                                                        \
+        if (_e != hipSuccess) {                                                                        \
+            if (verbose()) fprintf(stderr, "dhtgpu: %s at %s:%d: %s\n", hipGetErrorString(_e), __FILE__, __LINE__, #expr); \
+            return map_err(_e);                                                                        \
+        }                                                                                              \
     } while (0)
 
 uint32_t pad_q(uint32_t q) { return (q + 63) & ~63u; }

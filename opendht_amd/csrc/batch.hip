@@ -1787,6 +1787,13 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         mix(hd, nsub * sizeof(SubDesc));
         mix(&nsub, 4);
         mix(&nblk2, 4);   // (seg travels in the kernel arguments)
+        // where the tables live: their offsets depend on k and q (the layout puts them after
+        // the k-sized fallback records), so a call with another k on the same workspace must
+        // upload them again
+        const uint8_t* wd = reinterpret_cast<const uint8_t*>(d_desc);
+        const uint8_t* wb = d_blk;
+        mix(&wd, sizeof wd);
+        mix(&wb, sizeof wb);
         if (sig == 0) sig = 1;
         if (!c.desc_sig || *c.desc_sig != sig) {
             std::vector<uint8_t> bs(nblk2);

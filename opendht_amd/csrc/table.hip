@@ -96,15 +96,24 @@ __global__ __launch_bounds__(256) void k_find_closest(
 // ---------------------------------------------------------------------------------
 // K2.  HBM-streaming: each thread classifies 4 consecutive ids per step (5 x 16-B plane
 // loads, one 4-B bucket store), with the next step's 5 loads issued before this step's
-// work (two steps in flight per lane).  The grid is a whole number of workgroups per CU
-// (kClsPerCu, all resident at once: no second round of workgroups at the end).  Bucket
+// work (two steps in flight per lane).  The grid is kClsPerCu = 32 workgroups per CU (four
+// rounds of the eight that are resident at once): shorter grid-stride ranges per workgroup
+// end together (measured, profiles/r03/experiments/k2_shapes.txt: 4 per CU 0.468 ms, 8 0.48,
+// 16 0.44, 32 0.42-0.43, 64 without the look-ahead 0.43 ms).  Bucket
 // firsts live in LDS; findBucket is a branch-light binary search.  commonBits is a clz
 // over the first nonzero xor word; the heavy low bins (cb < 8 hold 255/256 of uniform ids)
 // are counted with wave ballots, the rest with LDS atomics, then one global atomic per bin
 // per workgroup.
 // ---------------------------------------------------------------------------------
 constexpr int kClsBlock = 256;
-constexpr int kClsPerCu = 4;
+#ifndef DHT_K2_PERCU
+#define DHT_K2_PERCU 32
+#endif
+#ifndef DHT_K2_AHEAD
+#define DHT_K2_AHEAD 1
+#endif
+constexpr int kClsPerCu = DHT_K2_PERCU;
+constexpr bool kClsAhead = DHT_K2_AHEAD != 0;   // the next step's loads issued before this step's work
 
 __global__ __launch_bounds__(kClsBlock) void k_classify(
     const uint32_t* __restrict__ planes, uint64_t stride, uint64_t n, uint32_t nb,
@@ -130,9 +139,11 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
         const bool active = g < n4;
         const uint64_t gn = g + G;
         uint4 nx[DHT_W];
+        if (kClsAhead) {
 #pragma unroll
-        for (int w = 0; w < DHT_W; ++w)
-            nx[w] = gn < n4 ? reinterpret_cast<const uint4*>(planes + (uint64_t)w * stride)[gn] : make_uint4(0u, 0u, 0u, 0u);
+            for (int w = 0; w < DHT_W; ++w)
+                nx[w] = gn < n4 ? reinterpret_cast<const uint4*>(planes + (uint64_t)w * stride)[gn] : make_uint4(0u, 0u, 0u, 0u);
+        }
         uint32_t packed = 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -172,8 +183,14 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
                     if (4 * g + e < n) out_bucket[4 * g + e] = (uint8_t)(packed >> (8 * e));
             }
         }
+        if (kClsAhead) {
 #pragma unroll
-        for (int w = 0; w < DHT_W; ++w) v[w] = nx[w];
+            for (int w = 0; w < DHT_W; ++w) v[w] = nx[w];
+        } else {
+#pragma unroll
+            for (int w = 0; w < DHT_W; ++w)
+                v[w] = gn < n4 ? reinterpret_cast<const uint4*>(planes + (uint64_t)w * stride)[gn] : make_uint4(0u, 0u, 0u, 0u);
+        }
     }
     if (lane == 0) {
 #pragma unroll

@@ -82,6 +82,26 @@ def test_subpartition_with_fewer_than_k_ids(ctx):
     assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
 
 
+def test_subpartitions_k_sequence_fresh_context():
+    """Sub-partition descriptor tables after a change of k on the same workspace: their offsets
+    in the workspace move with k (they sit after the k-sized fallback records), and a call that
+    reused the cached table signature without re-uploading read stale descriptors (a fault, once
+    the workspace was large enough not to be reallocated).  k = 32 first (the largest workspace),
+    then smaller k on the same context: every call == K1 scan."""
+    import opendht_amd
+    n, q = 1 << 25, 1 << 18   # q large enough that one plan cannot serve: 2 sub-partitions
+    c = opendht_amd.Context(0)
+    try:
+        c.gen_ids(3131, n)
+        tg = O.gen_ids(3132, q)
+        for k in (32, 1, 3, 8, 16, 3):
+            got, cnt = c.batch_topk(tg, k)
+            sc, scnt = c.topk(tg, k)
+            assert np.array_equal(cnt, scnt) and np.array_equal(got, sc), k
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("k", [1, 3, 16, 32])
 def test_subpartitions_larger_k(ctx, k):
     """2^26 ids, 2^18 targets (4 prefix sub-partitions, one K6 launch sequence) at k = 1, 3, 16
