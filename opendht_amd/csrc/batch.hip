@@ -2007,6 +2007,10 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
                     const uint32_t h = __builtin_amdgcn_ubfe(v4[f], h_off, hb);
                     hit[f] = ((b16[h >> 5] >> (h & 31)) & 1u) && tid4 + f < rem;
                 }
+#ifdef DHT_S1_MEASURE_NOFILTER
+                if (v4[0] == 0x12345678u && v4[1] == 0x9abcdef0u) nhit = hit[0];   // measurement build: stream only
+                if (false)
+#endif
                 if (__ballot(hit[0] || hit[1] || hit[2] || hit[3])) {   // rare
 #pragma unroll
                     for (uint32_t f = 0; f < 4; ++f) {
@@ -2026,6 +2030,9 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
         }
     }
     __syncthreads();
+#ifdef DHT_S1_MEASURE_NOTAIL
+    return;   // measurement build: no queue flush (results incomplete)
+#endif
     // the queue to the buckets: word 1 and the slot reservation in one round trip
     const uint32_t nq = nhit < kS1Queue ? nhit : kS1Queue;
     for (uint32_t i = threadIdx.x; i < nq; i += NT) {
