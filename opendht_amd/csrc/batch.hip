@@ -1930,7 +1930,14 @@ __device__ __forceinline__ uint32_t small_tw0(const SmallArgs& a, uint32_t qi) {
     return a.shift ? (w << a.shift) | (a.tp[a.ts + qi] >> (32 - a.shift)) : w;
 }
 
-template <int NT>
+// NQ > 0 (q <= NQ targets, so at most NQ distinct prefixes): an id's level-Ls prefix is compared
+// in registers with the NQ sorted prefixes (wave-uniform, unused slots past any prefix) and the
+// match is its bucket slot -- one v_bfe + NQ compares per id instead of the LDS bitmap read and
+// the binary search of a hit.  The filter cost 2.4 us of S1 at q = 1 over the bare stream
+// (profiles/r03/experiments/s1_measure.txt); NQ = 1 (q = 1): S1 13.0 -> 11.8 us.  NQ = 8 for
+// q <= 8 measured slower than the bitmap (20.3 against 13.9 us at q = 8): q > 1 takes NQ = 0,
+// the bitmap.
+template <int NT, int NQ>
 __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
     constexpr uint32_t kS1Sub = 4 * NT;
     __shared__ uint32_t b16[2048];      // 2^16 bits: the targets' top hb prefix bits
@@ -1994,6 +2001,10 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
         }
     };
     const uint32_t h_off = 32 - hb, tid4 = 4 * threadIdx.x;
+    uint32_t tq[NQ > 0 ? NQ : 1];
+#pragma unroll
+    for (int i = 0; i < (NQ > 0 ? NQ : 1); ++i)
+        tq[i] = (uint32_t)i < ntab ? __builtin_amdgcn_readfirstlane(tab[i]) : DHT_NONE;   // prefixes < 2^31
     for (uint32_t c0 = lo; c0 < hi; c0 += kRing * kS1Sub) {
 #pragma unroll
         for (uint32_t r = 0; r < kRing; ++r) {
@@ -2001,6 +2012,24 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
             if (sb < hi) {   // block-uniform
                 const uint32_t v4[4] = {ring[r].x, ring[r].y, ring[r].z, ring[r].w};
                 const uint32_t rem = hi - sb;
+                if (NQ > 0) {
+                    uint32_t m[4];
+#pragma unroll
+                    for (uint32_t f = 0; f < 4; ++f) {
+                        const uint32_t pre = top_bits(v4[f], a.Ls);
+                        m[f] = 0;
+#pragma unroll
+                        for (int i = 0; i < NQ; ++i) m[f] |= (uint32_t)(pre == tq[i]) << i;
+                        m[f] = tid4 + f < rem ? m[f] : 0u;
+                    }
+                    if (__ballot((m[0] | m[1] | m[2] | m[3]) != 0)) {   // rare
+#pragma unroll
+                        for (uint32_t f = 0; f < 4; ++f)
+                            if (m[f]) emit(v4[f], sb + tid4 + f, (uint32_t)__ffs(m[f]) - 1);
+                    }
+                    ring[r] = load(sb + kRing * kS1Sub);
+                    continue;
+                }
                 bool hit[4];
 #pragma unroll
                 for (uint32_t f = 0; f < 4; ++f) {
@@ -2240,7 +2269,8 @@ hipError_t launch_small_topk(const BatchCall& c, void* sws, uint32_t parity, hip
         (void)hipEventRecord(ev[0], s);
         (void)hipEventRecord(ev[1], s);
     }
-    go(1, k_s1_filter<nt>, dim3(nblk), dim3(nt), 0, a);
+    if (c.q == 1) go(1, k_s1_filter<nt, 1>, dim3(nblk), dim3(nt), 0, a);
+    else go(1, k_s1_filter<nt, 0>, dim3(nblk), dim3(nt), 0, a);
     // S2: the prefix workgroups and the fallback list's scan roles in one launch
     const FbArgs fa{reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(fb_scratch) + al256((size_t)kFbBlocks * 4)),
                     static_cast<uint32_t*>(fb_scratch), kSmallFbBlocks, 0u, nullptr};

@@ -667,10 +667,11 @@ def test_table_stats_lowbit_depth(ctx):
 
 @pytest.mark.parametrize("n", [1, 7, 9, 100, 5000, 70001])
 @pytest.mark.parametrize("k", [1, 8, 14, 32])
-@pytest.mark.parametrize("q", [1, 13, 64])
+@pytest.mark.parametrize("q", [1, 5, 8, 13, 64])
 def test_small_batch_path(ctx, n, k, q):
     """Batches of <= 64 targets take the small-batch path (one pass over word 0 + one
-    workgroup per target prefix, the K1 scan for short subtrees): bit-exact like K6."""
+    workgroup per target prefix, the K1 scan for short subtrees): bit-exact like K6.  q = 1 and
+    q <= 8 run S1's register prefix check, q > 8 its LDS bitmap."""
     ids = O.gen_ids(3000 + n, n)
     tg = O.gen_ids(3100 + q, q)
     ctx.set_ids(ids)
@@ -681,10 +682,11 @@ def test_small_batch_path(ctx, n, k, q):
     assert bad.size == 0, f"{bad.size} targets differ, first {bad[:5]}"
 
 
-def test_small_batch_clusters_duplicates_fallback(ctx):
+@pytest.mark.parametrize("rows", [slice(0, 64), slice(0, 8), slice(14, 15), slice(8, 16), slice(40, 41)])
+def test_small_batch_clusters_duplicates_fallback(ctx, rows):
     """Small batches over clustered ids (w0 ties, buckets past their capacity, subtrees short
     of k ids: the K1 fallback), targets sharing a prefix (one bucket, several targets) and
-    duplicated ids."""
+    duplicated ids; the whole batch and sub-batches of 8 and 1 (S1's register prefix check)."""
     ids = O.gen_ids(51, 40000)
     ids[:20000, :4] = ids[0, :4]          # 20,000 ids in one 32-bit prefix: bucket overflow
     ids[:5000, 4:8] = ids[0, 4:8]
@@ -696,6 +698,7 @@ def test_small_batch_clusters_duplicates_fallback(ctx):
     tg[14:20, :3] = 0
     tg[20:30] = tg[30:40]                 # repeated targets
     tg[40:45] = ids[30000:30005]          # targets that are (duplicated) members
+    tg = np.ascontiguousarray(tg[rows])
     ctx.set_ids(ids)
     for k in (8, 32):
         want, wcnt = O.topk(ids, tg, k)
