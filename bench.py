@@ -453,9 +453,18 @@ def main():
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
+    # diagnostic: the same window on the GPU's clock (first kernel enqueued .. last stream done),
+    # against which the host wall below adds the launch of the first step and the wake-up of
+    # the final synchronize
+    w_beg, w_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    w_beg.record(streams[0])
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+    t_enq = time.perf_counter() - t0   # host time to enqueue the K steps (diagnostic)
+    for st_ in streams[1:]:
+        streams[0].wait_stream(st_)
+    w_end.record(streams[0])
     torch.cuda.synchronize()
     if use_dist:
         dist.barrier()
@@ -625,6 +634,8 @@ def main():
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": ms_per_step,
+            "host_enqueue_ms_per_step": t_enq * 1e3 / a.steps,   # rank 0's host time to enqueue a step
+            "gpu_window_ms_per_step": w_beg.elapsed_time(w_end) / a.steps,   # rank 0, GPU clock (diagnostic)
             "higher_is_better": True,
             "scaling": scaling,
             "vs_baseline": None,

@@ -144,6 +144,7 @@ struct dhtgpu_ctx {
     int32_t f3_spec = -1;         // DHTGPU_F3SPEC: F3 speculative slots per set (-1 = plan's, 0 = exact gather)
     uint32_t f2_noseg = 0;        // DHTGPU_F2NOSEG: F2 ranges never segmented (more workgroups instead)
     uint32_t f2_wide = 0;         // DHTGPU_F2WIDE: F2's 8-B stage even where the narrow one fits (A/B)
+    uint32_t f4_quiet = 0;        // DHTGPU_F4QUIET: F4's grid after an empty fallback list (A/B; 0 = the default)
     hipEvent_t next_ev[8] = {};   // dhtgpu_batch_events: the next K6 call records its kernels here
     bool has_next_ev = false;
     DevBuf stamps;
@@ -209,6 +210,7 @@ int dhtgpu_ctx_create(int device, dhtgpu_ctx** out) {
     if (const char* d = getenv("DHTGPU_F3SPEC")) c->f3_spec = (int32_t)atoi(d);
     if (const char* d = getenv("DHTGPU_F2NOSEG")) c->f2_noseg = (uint32_t)atoi(d);
     if (const char* d = getenv("DHTGPU_F2WIDE")) c->f2_wide = (uint32_t)atoi(d);
+    if (const char* d = getenv("DHTGPU_F4QUIET")) c->f4_quiet = (uint32_t)atoi(d);
     if (e == hipSuccess) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
@@ -735,6 +737,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     bc.f3_spec = c->f3_spec;
     bc.f2_noseg = c->f2_noseg;
     bc.f2_wide = c->f2_wide;
+    bc.f4_quiet = c->f4_quiet;
     bc.ev = ev;
     bc.subs = specs.data();
     bc.nsub = S;
@@ -853,6 +856,7 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     bc.f3_spec = c->f3_spec;
     bc.f2_noseg = c->f2_noseg;
     bc.f2_wide = c->f2_wide;
+    bc.f4_quiet = c->f4_quiet;
     bc.ev = ev;
     int r = batch_slot_run(c, si, bc, s, ev);
     if (r) return r;

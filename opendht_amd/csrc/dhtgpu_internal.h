@@ -125,6 +125,7 @@ struct BatchCall {
     int32_t f3_spec;                       // F3 speculative slots per bucket set (< 0: the plan's; 0: exact gather)
     uint32_t f2_noseg;                     // experiment: never segment F2's ranges (more workgroups, whole rounds)
     uint32_t f2_wide;                      // experiment: F2's 8-B stage where the 6-B narrow one fits
+    uint32_t f4_quiet;                     // experiment: F4's grid after an empty list (0: kFbBlocks / 2)
     const volatile uint32_t* fb_hint;      // nullable: the slot's last fallback-list length (mapped host memory)
     uint32_t* fb_hint_dev;                 // its device address (F4 writes it)
     unsigned long long* stamps;            // dbg & 256: phase stamps [2 * 8192 * 16]
