@@ -706,10 +706,11 @@ def test_small_batch_clusters_duplicates_fallback(ctx, rows):
         assert np.array_equal(cnt, wcnt) and np.array_equal(got, want), k
 
 
+@pytest.mark.parametrize("q", [40, 1])
 @pytest.mark.parametrize("pbits,pval", [(1, 1), (3, 5)])
-def test_small_batch_prefix_shard(ctx, pbits, pval):
+def test_small_batch_prefix_shard(ctx, pbits, pval, q):
     """Small batches on a prefix shard (the shifted word-0 plane), own and foreign targets,
-    global and shard-local indices."""
+    global and shard-local indices; q = 1 takes S1's register prefix check."""
     n = 120000
     ids = O.gen_ids(91, n)
     top = lambda a: a[:, 0].astype(np.uint32) >> (8 - pbits)
@@ -717,6 +718,7 @@ def test_small_batch_prefix_shard(ctx, pbits, pval):
     gl = np.nonzero(top(ids) == pval)[0].astype(np.uint32)
     tg = O.gen_ids(95, 40)
     tg[:30, 0] = (tg[:30, 0] & (0xFF >> pbits)) | (pval << (8 - pbits))
+    tg = np.ascontiguousarray(tg[:q] if q > 1 else tg[3:4])
     w, wc = O.topk(ids[gl], tg, 8)
     got, cnt = ctx.batch_topk(tg, 8)
     assert np.array_equal(cnt, wc) and np.array_equal(got, gl[w])
