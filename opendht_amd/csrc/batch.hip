@@ -354,10 +354,11 @@ __device__ __forceinline__ uint4 f2_load1g(const uint32_t* __restrict__ w0, uint
     j = j < lim ? j : lim;
     return *reinterpret_cast<const uint4*>(w0 + j);
 }
+template <bool NT>
 __device__ __forceinline__ uint4 f2_load1(__amdgpu_buffer_rsrc_t rs, uint32_t lo, uint32_t c, uint32_t lim) {
     uint32_t j = c + 4 * threadIdx.x;
     j = j < lim ? j : lim;
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((j - lo) * 4u), 0, 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((j - lo) * 4u), 0, NT ? 2 : 0);   // 2: nt
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
@@ -372,11 +373,18 @@ __device__ __forceinline__ uint4 f2_load1(__amdgpu_buffer_rsrc_t rs, uint32_t lo
 // kF2Narrow is kF2Sparse over the 6-B narrow stage (a workgroup's range < 2^16 ids).
 constexpr uint32_t kF2Dense = 0, kF2Sparse = 1, kF2Stream = 2, kF2Seg = 3, kF2Narrow = 4;
 
-// Subs: several sub-partitions (descriptors read from memory, ring through buffer loads); the
-// one-set instantiation takes its descriptor from the kernel arguments and streams with plain
-// global loads
-template <uint32_t Mode, bool Subs>
+// Src: kF2One -- one set: its descriptor from the kernel arguments, the ring through plain
+// global loads; kF2Subs -- several sub-partitions (descriptors read from memory, the ring
+// through buffer loads); kF2SubsNT -- the same with non-temporal ring loads, for sets whose w0
+// planes exceed the Infinity Cache (kNtBytes): the stream then no longer evicts the survivor
+// and target buckets F3 / F4 read next (cfg-3 shard: F2 118 -> 103 us, F3 43 -> 38, F4 19 ->
+// 17, profiles/r03/experiments/stream_nt_ab.txt).  A set the cache holds keeps cached loads:
+// non-temporal ones re-read it from HBM every call (cfg 2: F2 20.5 -> 22.9 us).
+constexpr uint32_t kF2One = 0, kF2Subs = 1, kF2SubsNT = 2;
+constexpr uint64_t kNtBytes = 192ull << 20;   // 3/4 of the 256 MB Infinity Cache
+template <uint32_t Mode, uint32_t Src>
 __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
+    constexpr bool Subs = Src != kF2One, NT = Src == kF2SubsNT;
     constexpr bool Narrow = Mode == kF2Narrow;
     constexpr bool Sparse = Mode == kF2Sparse || Mode == kF2Seg || Narrow;
     extern __shared__ uint32_t sh[];   // (32 spare) | misc[8] | bm[nwords] | hist[np + 1] | wsum[17] | lost[np/32 + 1] | stage
@@ -432,7 +440,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     uint4 ring[kF2Ring];
 #pragma unroll
     for (uint32_t r = 0; r < kF2Ring; ++r)
-        ring[r] = Subs ? f2_load1(rs, lo, lo + r * kF2Sub, lim) : f2_load1g(w0, lo + r * kF2Sub, lim);
+        ring[r] = Subs ? f2_load1<NT>(rs, lo, lo + r * kF2Sub, lim) : f2_load1g(w0, lo + r * kF2Sub, lim);
     if (threadIdx.x < 3) misc[threadIdx.x] = 0;
     for (uint32_t i = threadIdx.x; i <= np / 32; i += kF2Threads) lost[i] = 0;
     sync_lds();
@@ -524,7 +532,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                     cnt += misc[s3 == 0 ? 2u : s3 - 1];
                 }
             }
-            ring[r] = Subs ? f2_load1(rs, lo, sb + kF2Ring * kF2Sub, lim) : f2_load1g(w0, sb + kF2Ring * kF2Sub, lim);
+            ring[r] = Subs ? f2_load1<NT>(rs, lo, sb + kF2Ring * kF2Sub, lim) : f2_load1g(w0, sb + kF2Ring * kF2Sub, lim);
         }
     }
     if (Mode == kF2Stream) { if (cnt == 0x12345678u) a.ctr[4] = cnt; return; }
@@ -1550,11 +1558,14 @@ constexpr int kMaxDevices = 64;
 std::once_flag g_attr_once[kMaxDevices];
 
 void set_lds_attributes() {
-    const void* fs[] = {(const void*)k_f2_filter<kF2Dense, false>, (const void*)k_f2_filter<kF2Sparse, false>,
-                        (const void*)k_f2_filter<kF2Stream, false>, (const void*)k_f2_filter<kF2Seg, false>,
-                        (const void*)k_f2_filter<kF2Dense, true>, (const void*)k_f2_filter<kF2Sparse, true>,
-                        (const void*)k_f2_filter<kF2Stream, true>, (const void*)k_f2_filter<kF2Seg, true>,
-                        (const void*)k_f2_filter<kF2Narrow, false>, (const void*)k_f2_filter<kF2Narrow, true>,
+    const void* fs[] = {(const void*)k_f2_filter<kF2Dense, kF2One>, (const void*)k_f2_filter<kF2Sparse, kF2One>,
+                        (const void*)k_f2_filter<kF2Stream, kF2One>, (const void*)k_f2_filter<kF2Seg, kF2One>,
+                        (const void*)k_f2_filter<kF2Dense, kF2Subs>, (const void*)k_f2_filter<kF2Sparse, kF2Subs>,
+                        (const void*)k_f2_filter<kF2Stream, kF2Subs>, (const void*)k_f2_filter<kF2Seg, kF2Subs>,
+                        (const void*)k_f2_filter<kF2Narrow, kF2One>, (const void*)k_f2_filter<kF2Narrow, kF2Subs>,
+                        (const void*)k_f2_filter<kF2Dense, kF2SubsNT>, (const void*)k_f2_filter<kF2Sparse, kF2SubsNT>,
+                        (const void*)k_f2_filter<kF2Stream, kF2SubsNT>, (const void*)k_f2_filter<kF2Seg, kF2SubsNT>,
+                        (const void*)k_f2_filter<kF2Narrow, kF2SubsNT>,
                         (const void*)k_f3_answer<8, false, true, false>,  (const void*)k_f3_answer<16, false, true, false>,
                         (const void*)k_f3_answer<32, false, true, false>, (const void*)k_f3_answer<8, true, true, false>,
                         (const void*)k_f3_answer<16, true, true, false>,  (const void*)k_f3_answer<32, true, true, false>,
@@ -1729,8 +1740,12 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     const SubSpec one{c.planes, c.w0s, c.stride, c.n, c.gidx, c.base};
     const SubSpec* subs = c.nsub ? c.subs : &one;
     const uint32_t nsub = c.nsub ? c.nsub : 1u;
-    uint64_t n_max = 0;
-    for (uint32_t i = 0; i < nsub; ++i) n_max = std::max<uint64_t>(n_max, subs[i].n);
+    uint64_t n_max = 0, n_all = 0;
+    for (uint32_t i = 0; i < nsub; ++i) {
+        n_max = std::max<uint64_t>(n_max, subs[i].n);
+        n_all += subs[i].n;
+    }
+    const bool nt = 4 * n_all > kNtBytes;   // F2's ring: non-temporal past the Infinity Cache
     const BatchPlan P = plan_batch(n_max, c.q_plan, k, c.num_cus);
     const uint32_t np = 1u << P.b1, NP = nsub * np;
     uint32_t dbg = c.dbg;
@@ -1824,8 +1839,9 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         const size_t l2 = f2_lds(P, narrow);
 #define F2_GO(MM)                                                    \
     do {                                                             \
-        if (nsub > 1) go(1, k_f2_filter<MM, true>, g2, b2, l2, a2);  \
-        else go(1, k_f2_filter<MM, false>, g2, b2, l2, a2);          \
+        if (nsub > 1 && nt) go(1, k_f2_filter<MM, kF2SubsNT>, g2, b2, l2, a2); \
+        else if (nsub > 1) go(1, k_f2_filter<MM, kF2Subs>, g2, b2, l2, a2);   \
+        else go(1, k_f2_filter<MM, kF2One>, g2, b2, l2, a2);                  \
     } while (0)
         if (dbg & 64) F2_GO(kF2Stream);
         else if (narrow) F2_GO(kF2Narrow);
@@ -1951,10 +1967,14 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
     const uint32_t lo = (uint32_t)(lo64 < a.n ? lo64 : a.n);
     const uint32_t hi = (uint32_t)(lo64 + a.per_blk < a.n ? lo64 + a.per_blk : a.n);
     const uint32_t lim = min(a.lim, ((hi + 3u) & ~3u) - 4u);
+    // non-temporal ring loads: q = 1 11.9 -> 10.9 us, q = 8 13.9 -> 12.5 us on the cfg-2 set
+    // (profiles/r03/experiments/stream_nt_ab.txt)
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
     auto load = [&](uint32_t c) {
         uint32_t j = c + 4 * threadIdx.x;
         j = j < lim ? j : lim;
-        return *reinterpret_cast<const uint4*>(a.w0 + j);
+        const u4v x = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(a.w0 + j));
+        return make_uint4(x[0], x[1], x[2], x[3]);
     };
     // the id ring first: the setup below runs while its loads are in flight
     uint4 ring[kRing];
