@@ -304,6 +304,10 @@ int dhtgpu_net_prepare(dhtgpu_ctx* ctx, const uint8_t* dead, uint64_t table_seed
 int dhtgpu_search_batch(dhtgpu_ctx* ctx, const uint8_t* targets20, uint32_t q, const uint32_t* searchers,
                         uint32_t max_rounds, uint32_t* out_idx, uint8_t* out_flags, uint32_t* out_len,
                         uint32_t* out_rounds, uint32_t* out_queries);
+/* Requests a search sends per round (alpha, 1..8) for the following search_batch calls on this
+ * context: default 4 = MAX_REQUESTED_SEARCH_NODES (include/opendht/dht.h:321); BASELINE cfg 5
+ * states a 3-way alpha. */
+int dhtgpu_set_search_alpha(dhtgpu_ctx* ctx, uint32_t alpha);
 int dhtgpu_search_batch_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
                             const uint32_t* searchers, uint32_t max_rounds, uint32_t* out_idx, uint8_t* out_flags,
                             uint32_t* out_len, uint32_t* out_rounds, uint32_t* out_queries, void* stream);

@@ -20,7 +20,7 @@ import numpy as np
 
 __all__ = ["Context", "DhtGpuError", "NONE", "MAX_K", "lib", "LIB_PATH", "id_words"]
 
-# DHTGPU_LIB: another build of the same library (A/B experiments, tools/gpu_ab_lib.sh)
+# DHTGPU_LIB: another build of the same library (A/B experiments, tools/experiments/gpu_ab_lib.sh)
 LIB_PATH = os.environ.get("DHTGPU_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdhtgpu.so")
 NONE = 0xFFFFFFFF
 MAX_K = 32
@@ -68,6 +68,7 @@ def lib():
         "dhtgpu_gen_ids": ([_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64], ctypes.c_int),
         "dhtgpu_num_ids": ([_vp], ctypes.c_uint64),
         "dhtgpu_set_global_indices": ([_vp, ctypes.c_int], ctypes.c_int),
+        "dhtgpu_set_search_alpha": ([_vp, ctypes.c_uint32], ctypes.c_int),
         "dhtgpu_get_ids": ([_vp, ctypes.c_uint64, ctypes.c_uint64, _u8p], ctypes.c_int),
         "dhtgpu_ids_dev": ([_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
         "dhtgpu_topk": ([_vp, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p], ctypes.c_int),
@@ -139,7 +140,7 @@ def exported_symbols():
             "dhtgpu_index_build_timed", "dhtgpu_gen_ids_prefix", "dhtgpu_select_prefix_dev",
             "dhtgpu_batch_topk_dev", "dhtgpu_batch_topk_timed", "dhtgpu_batch_topk", "dhtgpu_table_depth",
             "dhtgpu_buffer_nodes_dev", "dhtgpu_buffer_nodes", "dhtgpu_deserialize_nodes", "dhtgpu_net_prepare",
-            "dhtgpu_search_batch", "dhtgpu_search_batch_dev", "dhtgpu_set_global_indices", "dhtgpu_cache_set",
+            "dhtgpu_search_batch", "dhtgpu_search_batch_dev", "dhtgpu_set_global_indices", "dhtgpu_set_search_alpha", "dhtgpu_cache_set",
             "dhtgpu_cache_nodes", "dhtgpu_cache_sorted", "dhtgpu_buffer_nodes_ids", "dhtgpu_batch_events",
             "dhtgpu_search_insert", "dhtgpu_table_stats"]
 
@@ -365,8 +366,16 @@ class Context:
                 raise ValueError("dead mask must have one byte per id")
         _check(lib().dhtgpu_net_prepare(self._h, _p(d, _u8p) if d is not None else None, table_seed), "net_prepare")
 
-    def search_batch(self, targets, searchers, max_rounds=64):
-        """Iterative searches: (idx (q,64), flags (q,64), len (q,), rounds (q,), queries (q,))."""
+    def set_search_alpha(self, alpha):
+        """Requests per search round for later search_batch calls (default 4 =
+        MAX_REQUESTED_SEARCH_NODES, include/opendht/dht.h:321)."""
+        _check(lib().dhtgpu_set_search_alpha(self._h, int(alpha)), "set_search_alpha")
+
+    def search_batch(self, targets, searchers, max_rounds=64, alpha=None):
+        """Iterative searches: (idx (q,64), flags (q,64), len (q,), rounds (q,), queries (q,)).
+        alpha (optional): requests per round, set on the context for this and later calls."""
+        if alpha is not None:
+            self.set_search_alpha(alpha)
         t = _ids(targets, "targets")
         q = t.shape[0]
         sr = np.ascontiguousarray(searchers, dtype=np.uint32).reshape(q)

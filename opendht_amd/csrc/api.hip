@@ -138,13 +138,11 @@ struct dhtgpu_ctx {
     uint64_t cache_version = 0;
     DevBuf cache_in, sort_scratch, cache_acc;
     DevBuf srch;            // search_insert / table_stats staging
-    // diagnostics (DHTGPU_DBG, read once at creation; phase stamps per context)
+    // diagnostics: DHTGPU_DBG, the library's one diagnostics switch (bit 256 =
+    // per-block phase stamps of F2 / F3 printed to stderr, the other bits = the measurement
+    // ablations of DESIGN §5a, results then incomplete); read once at creation, 0 in production
     uint32_t dbg = 0;
-    uint32_t f2_seg = 0;          // DHTGPU_F2SEG: F2 sparse-mode segment override (ids; 0 = plan's)
-    int32_t f3_spec = -1;         // DHTGPU_F3SPEC: F3 speculative slots per set (-1 = plan's, 0 = exact gather)
-    uint32_t f2_noseg = 0;        // DHTGPU_F2NOSEG: F2 ranges never segmented (more workgroups instead)
-    uint32_t f2_wide = 0;         // DHTGPU_F2WIDE: F2's 8-B stage even where the narrow one fits (A/B)
-    uint32_t f4_quiet = 0;        // DHTGPU_F4QUIET: F4's grid after an empty fallback list (A/B; 0 = the default)
+    uint32_t search_alpha = 4;   // crawl model: requests per search round (MAX_REQUESTED_SEARCH_NODES)
     hipEvent_t next_ev[8] = {};   // dhtgpu_batch_events: the next K6 call records its kernels here
     bool has_next_ev = false;
     DevBuf stamps;
@@ -206,11 +204,6 @@ int dhtgpu_ctx_create(int device, dhtgpu_ctx** out) {
     hipError_t e = c->bind();
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (const char* d = getenv("DHTGPU_DBG")) c->dbg = (uint32_t)atoi(d);
-    if (const char* d = getenv("DHTGPU_F2SEG")) c->f2_seg = (uint32_t)atoi(d);
-    if (const char* d = getenv("DHTGPU_F3SPEC")) c->f3_spec = (int32_t)atoi(d);
-    if (const char* d = getenv("DHTGPU_F2NOSEG")) c->f2_noseg = (uint32_t)atoi(d);
-    if (const char* d = getenv("DHTGPU_F2WIDE")) c->f2_wide = (uint32_t)atoi(d);
-    if (const char* d = getenv("DHTGPU_F4QUIET")) c->f4_quiet = (uint32_t)atoi(d);
     if (e == hipSuccess) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
@@ -733,11 +726,6 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     bc.out_cnt = lc;
     bc.num_cus = c->num_cus;
     bc.dbg = c->dbg;
-    bc.f2_seg = c->f2_seg;
-    bc.f3_spec = c->f3_spec;
-    bc.f2_noseg = c->f2_noseg;
-    bc.f2_wide = c->f2_wide;
-    bc.f4_quiet = c->f4_quiet;
     bc.ev = ev;
     bc.subs = specs.data();
     bc.nsub = S;
@@ -797,7 +785,10 @@ static int small_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     bc.out_cnt = lc;
     bc.num_cus = c->num_cus;
     bc.ev = ev;
-    DHT_TRY(launch_small_topk(bc, b.sws.p, b.spar, s));
+    if (hipError_t e = launch_small_topk(bc, b.sws.p, b.spar, s)) {
+        b.sclean = false;   // S1 may have counted into this call's set: the next call re-zeroes it all
+        return map_err(e);
+    }
     b.spar ^= 1u;
     b.last = s;
     c->last_small = true;
@@ -852,11 +843,6 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     bc.out_cnt = lc;
     bc.num_cus = c->num_cus;
     bc.dbg = c->dbg;
-    bc.f2_seg = c->f2_seg;
-    bc.f3_spec = c->f3_spec;
-    bc.f2_noseg = c->f2_noseg;
-    bc.f2_wide = c->f2_wide;
-    bc.f4_quiet = c->f4_quiet;
     bc.ev = ev;
     int r = batch_slot_run(c, si, bc, s, ev);
     if (r) return r;
@@ -1395,6 +1381,12 @@ int dhtgpu_net_prepare(dhtgpu_ctx* c, const uint8_t* dead, uint64_t table_seed) 
     return DHTGPU_OK;
 }
 
+int dhtgpu_set_search_alpha(dhtgpu_ctx* c, uint32_t alpha) {
+    if (!c || alpha < 1 || alpha > 8) return DHTGPU_EINVAL;
+    c->search_alpha = alpha;
+    return DHTGPU_OK;
+}
+
 int dhtgpu_search_batch_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, const uint32_t* searchers,
                             uint32_t max_rounds, uint32_t* out_idx, uint8_t* out_flags, uint32_t* out_len,
                             uint32_t* out_rounds, uint32_t* out_queries, void* stream) {
@@ -1405,7 +1397,7 @@ int dhtgpu_search_batch_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint
     DHT_TRY(c->bind());
     DHT_TRY(launch_search(c->planes.as<uint32_t>(), c->stride, c->net_sorted.as<uint2>(), c->index.p, c->n,
                           c->index_B, c->net_has_dead ? c->net_dead.as<uint8_t>() : nullptr, c->net_seed, tp, ts, q,
-                          searchers, max_rounds, out_idx, out_flags, out_len, out_rounds, out_queries,
+                          searchers, max_rounds, c->search_alpha, out_idx, out_flags, out_len, out_rounds, out_queries,
                           stream ? (hipStream_t)stream : c->stream));
     return DHTGPU_OK;
 }

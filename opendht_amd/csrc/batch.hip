@@ -615,8 +615,6 @@ struct F3Args {
     const SubDesc* subs; uint32_t np_sub;   // sub-partitions, partitions per sub-partition
     uint32_t dbg;
     unsigned long long* stamps;          // dbg & 256: per-block phase timestamps [np][16]
-    uint32_t spec;                       // speculative gather: slots per bucket set loaded with the counts
-                                         // (<= kF3Cap / kSets; 0: counts first, then the exact gather)
     uint32_t cap;                        // LDS stage entries (the plan's, <= kF3Cap)
 };
 
@@ -770,13 +768,11 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         a.bitmap[sub * a.nwords + i] = 0;
     for (uint32_t i = threadIdx.x; i <= nsub; i += kF3Threads) sofs[i] = 0;
     if (threadIdx.x == 0) ntie[0] = ntie[1] = 0;
-    // survivors of this partition in each of the kSets bucket sets (F2), its targets (F1), and
-    // -- speculatively, in the same round trip -- the first a.spec slots of every set (entry
-    // u * kF3Threads + tid = slot (u & 1) * kF3Threads + tid of set u >> 1) and the first
-    // chunk of targets; slots past a set's count are dropped below.  a.spec is the plan's
-    // expected per-set count plus a few sigma (the host sizes it): the slots past it are not
-    // loaded at all, so a partition's speculative bytes follow its survivors
-    static_assert(kF3Cap / kSets == 2 * kF3Threads && kF3Per == 2 * kSets, "speculative gather layout");
+    // survivors of this partition in each of the kSets bucket sets (F2) and its targets (F1) --
+    // the counts and the first chunk of targets in one round trip; the survivors themselves are
+    // gathered exactly once the counts are known (a speculative gather of fixed slots with the
+    // counts fetched 2x the algorithmic bytes at cfg 2 for no measured gain)
+    static_assert(kF3Cap / kSets == 2 * kF3Threads && kF3Per == 2 * kSets, "gather layout");
     uint32_t ms[kSets];
 #pragma unroll
     for (uint32_t x = 0; x < kSets; ++x) ms[x] = a.pcount[x * np + p];
@@ -785,13 +781,8 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     const uint2 tfirst = tsrc[threadIdx.x < a.tcap ? threadIdx.x : 0u];
     uint2 e[kF3Per];
     const uint2* pb = a.pbuf + (uint64_t)p * kSets * a.pcap;
-    const uint32_t spec = a.spec < a.pcap ? a.spec : a.pcap;
 #pragma unroll
-    for (uint32_t u = 0; u < kF3Per; ++u) {
-        const uint32_t pos = (u & 1) * kF3Threads + threadIdx.x;
-        e[u] = make_uint2(0u, 0u);
-        if (pos < spec) e[u] = pb[(u >> 1) * a.pcap + pos];
-    }
+    for (uint32_t u = 0; u < kF3Per; ++u) e[u] = make_uint2(0u, 0u);
     const uint32_t mt = mt0 < a.tcap ? mt0 : a.tcap;
     if (p == 0) {   // spilled targets (foreign, or a full bucket) join the fallback list
         const uint32_t nsp = a.ctr[kSpill];
@@ -805,15 +796,13 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         }
     }
     sync_lds();   // every thread has read the counts
-    // set offsets inside the partition (soff[x] = entries of sets < x); over = a set overflowed;
-    // spec_ok = every set fits its speculative slots
+    // set offsets inside the partition (soff[x] = entries of sets < x); over = a set overflowed
     uint32_t soff[kSets + 1];
-    bool over = false, spec_ok = true;
+    bool over = false;
     soff[0] = 0;
 #pragma unroll
     for (uint32_t x = 0; x < kSets; ++x) {
         over = over || ms[x] > a.pcap;
-        spec_ok = spec_ok && ms[x] <= spec;
         soff[x + 1] = soff[x] + (ms[x] < a.pcap ? ms[x] : a.pcap);
     }
     const uint32_t m = soff[kSets];
@@ -843,12 +832,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     const uint32_t sq_sh = 32 - a.Lq;                            // sub-prefix = bfe(w, 32 - Lq, Lq - b1)
     // valid[u]: slot u holds one of the partition's entries
     uint32_t valid = 0;
-    if (spec_ok) {
-#pragma unroll
-        for (uint32_t u = 0; u < kF3Per; ++u)
-            valid |= (uint32_t)((u & 1) * kF3Threads + threadIdx.x < ms[u >> 1]) << u;
-    } else {
-        // a set past its speculative slots (rare with the planned spec; always with spec 0):
+    {
         // gather the partition exactly, entry j from set x (soff[x] <= j < soff[x + 1]) at slot
         // j - soff[x] -- only the m entries are loaded
 #pragma unroll
@@ -1303,7 +1287,7 @@ struct BatchPlan {
     uint32_t nstage; // F2's narrow stage entries (6 B each; 0: none) -- F2 then leaves room for an F3 workgroup
     uint32_t f3cap;  // F3's LDS stage entries (kF3Cap, or the 6-sigma bound when that buys a 4th workgroup per CU)
     uint32_t scap;   // survivors per (bucket set, partition)
-    uint32_t spec;   // F3's speculative slots per set (0: exact gather after the counts)
+    uint32_t f3cap_wide;   // F3's LDS stage entries when F2 runs its 8-B stage (no narrow stage)
     bool fits;   // partitions' survivors fit the F3 stage on uniform ids
     uint64_t per_blk;
 };
@@ -1365,12 +1349,9 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
         const double mean = sub * f * mu, var = sub * f * (1.0 - f) * mu * mu + sub * f * mu;
         const double cap = mean + 8.0 * std::sqrt(var) + 64.0;
         P.scap = cap >= (double)kF3Cap ? kF3Cap : ((uint32_t)cap + 63u) & ~63u;
-        // F3's speculative gather (slots per set loaded with the counts, one round trip) is off:
-        // the exact gather after the counts fetches the survivors' bytes only (PMC at cfg 2:
-        // 18.5 MB against 19.7 MB algorithmic; the fixed 512 slots of round 2 fetched 40 MB) and
-        // measured no slower (cfg-2 step 37.7-38.1 us against 38.3-38.4 with the planned mean +
-        // 5 sigma, F3 15.4 against 15.8 us).  DHTGPU_F3SPEC sets a slot count for experiments.
-        P.spec = 0;
+        // F3 gathers exactly after the counts: the survivors' bytes only (PMC at cfg 2: 18.5 MB
+        // against 19.7 MB algorithmic; round 2's fixed speculative slots fetched 40 MB) and no
+        // slower (cfg-2 step 37.7-38.1 us against 38.3-38.4 with a planned mean + 5 sigma)
     }
     // F3 sorts by up to 1 bit below the mark level (finer candidate ranges), <= 4096 bins
     P.Lq = P.Lm + 1 < 32 ? P.Lm + 1 : 32;
@@ -1427,18 +1408,23 @@ BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     // its targets to the exact fallback, as one past kF3Cap does).  1 KB of margin per kernel
     // for the LDS allocation granule.
     P.nstage = 0;
+    P.f3cap_wide = P.f3cap;
     if (P.sparse && P.per_blk <= 65536) {
         const double mean = (double)P.per_blk * f, sd = std::sqrt(mean * (1.0 - f));
         const double need2 = mean + 8.0 * sd + 256.0;
         for (int pass = 0; pass < 2 && !P.nstage; ++pass) {
+            uint32_t cap3 = P.f3cap_wide;   // pass 1: F3 stages the 6-sigma bound to make room
             if (pass == 1) {
-                if (!P.fits || cap6 >= P.f3cap) break;
-                P.f3cap = cap6;
+                if (!P.fits || cap6 >= cap3) break;
+                cap3 = cap6;
             }
-            const size_t f3l = (lds3(P.Lq, P.f3cap) + 1023) & ~(size_t)1023;
+            const size_t f3l = (lds3(P.Lq, cap3) + 1023) & ~(size_t)1023;
             if (fixed + f3l + 1024 >= kLdsMax) continue;
             const size_t room6 = (kLdsMax - f3l - fixed - 1024) / 6;
-            if ((double)room6 >= need2) P.nstage = (uint32_t)std::min<size_t>(room6, kStage) & ~1u;
+            if ((double)room6 >= need2) {
+                P.nstage = (uint32_t)std::min<size_t>(room6, kStage) & ~1u;
+                P.f3cap = cap3;   // committed only with the narrow stage it makes room for
+            }
         }
     }
     return P;
@@ -1448,9 +1434,9 @@ size_t f2_lds(const BatchPlan& P, bool narrow = false) {
     return (size_t)f2_fixed_words(P.nwords, 1u << P.b1) * 4 + (narrow ? (size_t)P.nstage * 6 : (size_t)P.stage * 8);
 }
 
-size_t f3_lds(const BatchPlan& P) {
+size_t f3_lds(const BatchPlan& P, uint32_t cap) {
     const uint32_t nsub = 1u << (P.Lq - P.b1);
-    return (size_t)f3_words(nsub) * 4 + (size_t)(P.f3cap + kF3Threads) * 8;
+    return (size_t)f3_words(nsub) * 4 + (size_t)(cap + kF3Threads) * 8;
 }
 
 // DHTGPU_DBG=256: per-block phase profiles of F2 and F3 from their s_memrealtime stamps
@@ -1552,10 +1538,7 @@ void print_phase_profile(const BatchPlan& P, uint32_t nblk2, uint32_t np, unsign
     }
 }
 
-// hipFuncSetAttribute(MaxDynamicSharedMemorySize) applies to the device current at the call:
-// once per device, from whichever thread gets there first
-constexpr int kMaxDevices = 64;
-std::once_flag g_attr_once[kMaxDevices];
+std::once_flag g_attr_once[kMaxDevices];   // set_lds_attributes, per device (per_device_once)
 
 void set_lds_attributes() {
     const void* fs[] = {(const void*)k_f2_filter<kF2Dense, kF2One>, (const void*)k_f2_filter<kF2Sparse, kF2One>,
@@ -1633,7 +1616,7 @@ WsLayout ws_layout(const BatchPlan& P, uint32_t nsub, uint32_t q, uint32_t k) {
 // turns -- one round of workgroups however large the set; when not even one ring turn fits, no
 // workgroup gets more ids than that bound.
 uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, uint32_t q_plan, int num_cus,
-                        SubDesc* d, uint32_t* seg, bool no_seg = false) {
+                        SubDesc* d, uint32_t* seg) {
     const double f = 1.0 - std::exp(-(double)q_plan / (double)(1ull << P.Lm));
     uint64_t pb_cap = 1ull << 40;   // dense mode: no cap
     if (P.sparse) {
@@ -1646,7 +1629,7 @@ uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, 
     }
     *seg = 0xFFFFFFFFu;
     constexpr uint64_t turn = (uint64_t)kF2Ring * kF2Sub;
-    if (P.sparse && pb_cap >= turn && !no_seg) {   // (no_seg: more workgroups instead, in whole rounds)
+    if (P.sparse && pb_cap >= turn) {
         *seg = (uint32_t)std::min<uint64_t>(pb_cap / turn * turn, 0x80000000ull);
         pb_cap = 1ull << 40;
     }
@@ -1688,7 +1671,7 @@ bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t n
     if (((uint64_t)nsub << P.b1) > kMaxParts) return false;
     // dense mode flushes whenever less than one sub-step of room is left
     if (!P.fits || P.Lm - P.b1 > 13 || (!P.sparse && P.stage < kF2Sub + 1024)) return false;
-    return f3_lds(P) <= kLdsMax && f2_lds(P) <= kLdsMax;
+    return f3_lds(P, P.f3cap_wide) <= kLdsMax && f2_lds(P) <= kLdsMax;
 }
 
 size_t batch_clean_bytes(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub) {
@@ -1732,8 +1715,10 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     if (c.skip && !c.w0s && !c.nsub) return hipErrorInvalidValue;
     if (c.nsub > kMaxSubs) return hipErrorInvalidValue;
     if (!c.q) return hipSuccess;
-    int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDevices) std::call_once(g_attr_once[dev], set_lds_attributes);
+    {
+        const hipError_t e = per_device_once(g_attr_once, set_lds_attributes);
+        if (e != hipSuccess) return e;
+    }
     const uint32_t q = c.q, k = c.k;
     // the sub-partitions (a set that needs no split is its own one sub-partition); the plan is
     // the largest one's
@@ -1774,17 +1759,13 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     // (steady-state calls upload nothing)
     SubDesc hd[kMaxSubs];
     uint32_t seg = 0;
-    const uint32_t nblk2 = deal_f2_blocks(P, subs, nsub, c.q_plan, c.num_cus, hd, &seg, c.f2_noseg != 0);
-    if (c.f2_seg && P.sparse && seg != 0xFFFFFFFFu) {   // experiment: segments of whole ring turns
-        constexpr uint32_t turn = kF2Ring * kF2Sub;
-        seg = std::max<uint32_t>(turn, c.f2_seg / turn * turn);
-    }
+    const uint32_t nblk2 = deal_f2_blocks(P, subs, nsub, c.q_plan, c.num_cus, hd, &seg);
     bool seg_used = false;   // some workgroup's range spans more than one segment
     for (uint32_t i = 0; i < nsub; ++i) seg_used = seg_used || (hd[i].nblk && hd[i].per_blk > seg);
     if (nblk2 > kMaxF2Blocks) return hipErrorInvalidValue;
     // the narrow stage: every workgroup's range under 2^16 ids and its survivors (mean + 8 sigma
     // + 256 on uniform ids) within the narrow stage; no segments
-    bool narrow = P.nstage && P.sparse && !seg_used && !c.f2_wide && !(dbg & 64);
+    bool narrow = P.nstage && P.sparse && !seg_used && !(dbg & 64);
     {
         const double f = 1.0 - std::exp(-(double)c.q_plan / (double)(1ull << P.Lm));
         for (uint32_t i = 0; i < nsub && narrow; ++i) {
@@ -1862,8 +1843,9 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     // the base arguments are the whole set's: F4's scan (fallback targets) runs over all its ids
     F3Args a{pbuf, pcount, P.scap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, c.planes, c.stride,
              c.n, c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, fb_sub, pstat, tie_hdr, tie_cand, tie_cnt,
-             d_desc, np, dbg, stamps, c.f3_spec < 0 ? P.spec : (uint32_t)c.f3_spec, P.f3cap};
-    size_t l3 = f3_lds(P);
+             d_desc, np, dbg, stamps, narrow ? P.f3cap : P.f3cap_wide};
+    // F3 stages the plan's 6-sigma bound only beside F2's narrow stage (which it makes room for)
+    size_t l3 = f3_lds(P, a.cap);
     if (dbg & 4096) l3 = l3 > 81920 ? l3 : 81920;   // experiment: 2 F3 blocks per CU
     if (dbg & 8192) l3 = l3 > 54000 ? l3 : 54000;   // experiment: 3 F3 blocks per CU
     const dim3 g3(NP), b3(kF3Threads);
@@ -1895,8 +1877,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     // fallback scan's parallelism).  Measured at three in flight: step -1.3 µs, latency +1.5.
     // (a sub-partitioned call fills the chip alone and defers ~1 tie per partition over 2,048+
     // partitions: the full grid keeps them at about one per wave)
-    const uint32_t quiet = c.f4_quiet && c.f4_quiet <= kFbBlocks ? c.f4_quiet : kFbBlocks / 2;
-    const uint32_t nfb = (c.fb_hint && *c.fb_hint == 0u && nsub == 1) ? quiet : kFbBlocks;
+    const uint32_t nfb = (c.fb_hint && *c.fb_hint == 0u && nsub == 1) ? kFbBlocks / 2 : kFbBlocks;
     const FbArgs fa{fb_rec, fb_done, nfb, NP, c.fb_hint_dev};
     const dim3 g4(nfb), b4(kF4Threads);
     if (k <= 8) go(3, k_f4<8>, g4, b4, 0, a, fa);

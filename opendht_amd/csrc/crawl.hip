@@ -23,7 +23,9 @@
 namespace dhtgpu {
 namespace {
 
-constexpr uint32_t kSearchNodes = 14, kTargetNodes = 8, kAlpha = 4, kBucket = 8, kLevels = 32;
+// kAlphaMax bounds the run-time alpha (requests per round; the reference's MAX_REQUESTED_SEARCH_NODES
+// = 4, src/dht.h:321, is the default; BASELINE cfg 5 states 3)
+constexpr uint32_t kSearchNodes = 14, kTargetNodes = 8, kAlphaMax = 8, kBucket = 8, kLevels = 32;
 constexpr uint32_t kListCap = 64, kDeadCap = 64;
 constexpr uint32_t kQ = 1, kReplied = 2, kBad = 4;
 constexpr int kSearchThreads = 64;
@@ -200,7 +202,7 @@ struct List {
 
 __global__ __launch_bounds__(kSearchThreads) void k_search(Net net, const uint32_t* __restrict__ tp, uint64_t ts,
                                                          const uint32_t* __restrict__ searchers, uint32_t q,
-                                                         uint32_t max_rounds, uint32_t* __restrict__ out_idx,
+                                                         uint32_t max_rounds, uint32_t alpha, uint32_t* __restrict__ out_idx,
                                                          uint8_t* __restrict__ out_flags,
                                                          uint32_t* __restrict__ out_len,
                                                          uint32_t* __restrict__ out_rounds,
@@ -223,8 +225,8 @@ __global__ __launch_bounds__(kSearchThreads) void k_search(Net net, const uint32
     uint32_t rounds = 0, queries = 0;
     for (; rounds < max_rounds; ++rounds) {
         if (L.synced()) break;
-        uint32_t sel[kAlpha], ns = 0;
-        for (uint32_t k = 0; k < L.len && ns < kAlpha; ++k)
+        uint32_t sel[kAlphaMax], ns = 0;
+        for (uint32_t k = 0; k < L.len && ns < alpha; ++k)
             if (!(L.F(k) & (kBad | kQ | kReplied))) {   // canGet: not bad, not asked, no reply yet
                 L.F(k) |= kQ;
                 sel[ns++] = L.I(k);
@@ -268,14 +270,15 @@ hipError_t launch_net_sort(const void* index_ws, uint64_t n, uint32_t B, uint2* 
 
 hipError_t launch_search(const uint32_t* planes, uint64_t stride, const uint2* sorted, const void* index_ws,
                          uint64_t n, uint32_t B, const uint8_t* dead, uint64_t seed, const uint32_t* tp, uint64_t ts,
-                         uint32_t q, const uint32_t* searchers, uint32_t max_rounds, uint32_t* out_idx,
+                         uint32_t q, const uint32_t* searchers, uint32_t max_rounds, uint32_t alpha, uint32_t* out_idx,
                          uint8_t* out_flags, uint32_t* out_len, uint32_t* out_rounds, uint32_t* out_queries,
                          hipStream_t s) {
     if (!q) return hipSuccess;
+    if (alpha < 1 || alpha > kAlphaMax) return hipErrorInvalidValue;
     Net net{planes, stride, sorted,
             reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(index_ws) + (size_t)n * 8), B, n, dead, seed};
     k_search<<<(q + kSearchThreads - 1) / kSearchThreads, kSearchThreads, 0, s>>>(
-        net, tp, ts, searchers, q, max_rounds, out_idx, out_flags, out_len, out_rounds, out_queries);
+        net, tp, ts, searchers, q, max_rounds, alpha, out_idx, out_flags, out_len, out_rounds, out_queries);
     return hipGetLastError();
 }
 

@@ -4,7 +4,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 namespace dhtgpu {
+
+// hipFuncSetAttribute (e.g. MaxDynamicSharedMemorySize) applies to the device current on the
+// calling thread: set() runs once per device id below kMaxDevices, from whichever thread gets
+// there first, and on every call for a device id past the table.  Returns hipGetDevice's error.
+constexpr int kMaxDevices = 64;
+inline hipError_t per_device_once(std::once_flag* flags, void (*set)()) {
+    int dev = 0;
+    const hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev >= 0 && dev < kMaxDevices) std::call_once(flags[dev], set);
+    else set();
+    return hipSuccess;
+}
 
 // ID-plane geometry: planes are padded to a multiple of kTile ids so that the scan
 // kernel can stream whole tiles without bounds checks.
@@ -120,12 +135,7 @@ struct BatchCall {
     const uint32_t* gidx; uint32_t base;   // result index map (nullable) or offset
     uint32_t* out_idx; uint32_t* out_cnt;  // rows of the ORIGINAL target indices
     int num_cus;
-    uint32_t dbg;                          // DHTGPU_DBG experiment switches (0 in production)
-    uint32_t f2_seg;                       // F2 sparse-mode segment override in ids (0: the plan's)
-    int32_t f3_spec;                       // F3 speculative slots per bucket set (< 0: the plan's; 0: exact gather)
-    uint32_t f2_noseg;                     // experiment: never segment F2's ranges (more workgroups, whole rounds)
-    uint32_t f2_wide;                      // experiment: F2's 8-B stage where the 6-B narrow one fits
-    uint32_t f4_quiet;                     // experiment: F4's grid after an empty list (0: kFbBlocks / 2)
+    uint32_t dbg;                          // DHTGPU_DBG diagnostics switches (0 in production)
     const volatile uint32_t* fb_hint;      // nullable: the slot's last fallback-list length (mapped host memory)
     uint32_t* fb_hint_dev;                 // its device address (F4 writes it)
     unsigned long long* stamps;            // dbg & 256: phase stamps [2 * 8192 * 16]
@@ -170,7 +180,7 @@ uint32_t search_list_cap();
 hipError_t launch_net_sort(const void* index_ws, uint64_t n, uint32_t B, uint2* out, hipStream_t s);
 hipError_t launch_search(const uint32_t* planes, uint64_t stride, const uint2* sorted, const void* index_ws,
                          uint64_t n, uint32_t B, const uint8_t* dead, uint64_t seed, const uint32_t* tp, uint64_t ts,
-                         uint32_t q, const uint32_t* searchers, uint32_t max_rounds, uint32_t* out_idx,
+                         uint32_t q, const uint32_t* searchers, uint32_t max_rounds, uint32_t alpha, uint32_t* out_idx,
                          uint8_t* out_flags, uint32_t* out_len, uint32_t* out_rounds, uint32_t* out_queries,
                          hipStream_t s);
 

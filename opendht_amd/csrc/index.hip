@@ -498,8 +498,7 @@ static void index_layout(void* ws, uint64_t n, uint32_t B, uint2*& pairs, uint32
     (void)B;
 }
 
-constexpr int kIdxMaxDevices = 64;
-std::once_flag g_idx_attr_once[kIdxMaxDevices];
+std::once_flag g_idx_attr_once[kMaxDevices];   // k_p1_scatter / k_p2_buckets LDS attributes (per_device_once)
 
 hipError_t launch_index_build(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t B, void* ws,
                               hipStream_t s, hipEvent_t* ev) {
@@ -518,12 +517,13 @@ hipError_t launch_index_build(const uint32_t* planes, uint64_t stride, uint64_t 
     // hipFuncSetAttribute applies to the device current at the call: once per device, from
     // whichever thread gets there first (a plain static flag raced between threads and skipped
     // every device after the first)
-    int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kIdxMaxDevices)
-        std::call_once(g_idx_attr_once[dev], [] {
+    {
+        const hipError_t e = per_device_once(g_idx_attr_once, [] {
             (void)hipFuncSetAttribute((const void*)k_p2_buckets, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
             (void)hipFuncSetAttribute((const void*)k_p1_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
         });
+        if (e != hipSuccess) return e;
+    }
     if (ev) (void)hipEventRecord(ev[0], s);
     if (n) {
         k_p0_hist<<<nblk, kBlk, np * 4, s>>>(planes, n, b1, nblk, p1_tile(n), H);

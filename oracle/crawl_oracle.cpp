@@ -58,7 +58,9 @@ inline uint32_t be32(const uint8_t* p) {
     return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
 }
 
-constexpr unsigned kSearchNodes = 14, kTargetNodes = 8, kAlpha = 4, kBucket = 8, kLevels = 32;
+// alpha (requests per round) is a parameter: the reference's MAX_REQUESTED_SEARCH_NODES = 4
+// (include/opendht/dht.h:321) by default, BASELINE cfg 5's 3-way alpha on request
+constexpr unsigned kSearchNodes = 14, kTargetNodes = 8, kBucket = 8, kLevels = 32;
 constexpr unsigned kListCap = 64, kDeadCap = 64;
 enum : uint8_t { Q = 1, REPLIED = 2, BAD = 4 };
 
@@ -182,7 +184,7 @@ extern "C" {
 void orc_search_batch(const uint8_t* ids20, uint64_t n, const uint8_t* dead, uint64_t table_seed,
                       const uint8_t* targets20, const uint32_t* searchers, uint32_t q, uint32_t max_rounds,
                       uint32_t* out_idx, uint8_t* out_flags, uint32_t* out_len, uint32_t* out_rounds,
-                      uint32_t* out_queries, int threads) {
+                      uint32_t* out_queries, int threads, uint32_t alpha) {
     Net net;
     net.n = n;
     net.ids = ids20;
@@ -209,7 +211,7 @@ void orc_search_batch(const uint8_t* ids20, uint64_t n, const uint8_t* dead, uin
         for (; rounds < max_rounds; ++rounds) {
             if (sr.synced()) break;
             std::vector<uint32_t> sel;
-            for (size_t k = 0; k < sr.idx.size() && sel.size() < kAlpha; ++k)
+            for (size_t k = 0; k < sr.idx.size() && sel.size() < alpha; ++k)
                 if (!(sr.fl[k] & (BAD | Q | REPLIED))) {   // canGet: not bad, not asked, no reply yet
                     sr.fl[k] |= Q;
                     sel.push_back(sr.idx[k]);

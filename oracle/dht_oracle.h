@@ -113,7 +113,7 @@ void orc_classify_mt(uint32_t nb, const uint8_t* firsts20, const uint8_t* myid20
 void orc_search_batch(const uint8_t* ids20, uint64_t n, const uint8_t* dead, uint64_t table_seed,
                       const uint8_t* targets20, const uint32_t* searchers, uint32_t q, uint32_t max_rounds,
                       uint32_t* out_idx, uint8_t* out_flags, uint32_t* out_len, uint32_t* out_rounds,
-                      uint32_t* out_queries, int threads);
+                      uint32_t* out_queries, int threads, uint32_t alpha);
 
 #ifdef __cplusplus
 }

@@ -99,7 +99,7 @@ def _load(path):
     L.orc_deserialize_node.argtypes = [u8p, ctypes.c_uint32, u8p, ctypes.c_uint32, u8p, u8p]
     L.orc_deserialize_node.restype = ctypes.c_int
     L.orc_search_batch.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint64, u8p, u32p, ctypes.c_uint32,
-                                   ctypes.c_uint32, u32p, u8p, u32p, u32p, u32p, ctypes.c_int]
+                                   ctypes.c_uint32, u32p, u8p, u32p, u32p, u32p, ctypes.c_int, ctypes.c_uint32]
     return L
 
 
@@ -300,8 +300,9 @@ def deserialize_node(rec, af, myid, from_af, from_addr):
     return st, out
 
 
-def search_batch(ids, dead, table_seed, targets, searchers, max_rounds=64, threads=None):
-    """Crawl-replay model (oracle/crawl_oracle.cpp): (idx, flags, len, rounds, queries)."""
+def search_batch(ids, dead, table_seed, targets, searchers, max_rounds=64, threads=None, alpha=4):
+    """Crawl-replay model (oracle/crawl_oracle.cpp): (idx, flags, len, rounds, queries); alpha =
+    requests per round (4 = MAX_REQUESTED_SEARCH_NODES, include/opendht/dht.h:321)."""
     ids = np.ascontiguousarray(ids, dtype=np.uint8)
     targets = np.ascontiguousarray(targets, dtype=np.uint8)
     q = targets.shape[0]
@@ -312,7 +313,7 @@ def search_batch(ids, dead, table_seed, targets, searchers, max_rounds=64, threa
     ln, rd, qs = (np.empty(q, np.uint32) for _ in range(3))
     lib().orc_search_batch(_p(ids, u8p), ids.shape[0], _p(d, u8p) if d is not None else None, table_seed,
                            _p(targets, u8p), _p(sr, u32p), q, max_rounds, _p(idx, u32p), _p(fl, u8p),
-                           _p(ln, u32p), _p(rd, u32p), _p(qs, u32p), int(threads or default_threads()))
+                           _p(ln, u32p), _p(rd, u32p), _p(qs, u32p), int(threads or default_threads()), int(alpha))
     return idx, fl, ln, rd, qs
 
 

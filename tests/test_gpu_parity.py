@@ -566,10 +566,12 @@ def test_deserialize_nodes_vs_oracle(ctx, af):
 
 
 
-@pytest.mark.parametrize("n,dead_frac,seed", [(3000, 0.0, 1), (100000, 0.2, 2), (40000, 0.5, 3)])
-def test_search_batch_vs_oracle(ctx, n, dead_frac, seed):
+@pytest.mark.parametrize("n,dead_frac,seed,alpha", [(3000, 0.0, 1, 4), (100000, 0.2, 2, 4), (40000, 0.5, 3, 4),
+                                                    (100000, 0.2, 4, 3), (40000, 0.3, 5, 1), (20000, 0.1, 6, 8)])
+def test_search_batch_vs_oracle(ctx, n, dead_frac, seed, alpha):
     """Crawl-replay search kernel == the oracle's model, list for list (indices, flags,
-    lengths, rounds, requests)."""
+    lengths, rounds, requests); alpha = requests per round: the reference's 4
+    (MAX_REQUESTED_SEARCH_NODES, include/opendht/dht.h:321), BASELINE cfg 5's 3, and 1 / 8."""
     ids = O.gen_ids(1000 + seed, n)
     dead = (np.random.default_rng(seed).random(n) < dead_frac).astype(np.uint8) if dead_frac else None
     tg = O.gen_ids(2000 + seed, 700)
@@ -577,8 +579,9 @@ def test_search_batch_vs_oracle(ctx, n, dead_frac, seed):
     sr = ((np.arange(700, dtype=np.uint64) * 7919) % n).astype(np.uint32)
     ctx.set_ids(ids)
     ctx.net_prepare(dead, table_seed=seed)
-    got = ctx.search_batch(tg, sr)
-    want = O.search_batch(ids, dead, seed, tg, sr)
+    got = ctx.search_batch(tg, sr, alpha=alpha)
+    ctx.set_search_alpha(4)
+    want = O.search_batch(ids, dead, seed, tg, sr, alpha=alpha)
     names = ["idx", "flags", "len", "rounds", "queries"]
     for g, w, nm in zip(got, want, names):
         bad = np.nonzero((g != w).reshape(g.shape[0], -1).any(axis=1))[0]
@@ -670,8 +673,8 @@ def test_table_stats_lowbit_depth(ctx):
 @pytest.mark.parametrize("q", [1, 5, 8, 13, 64])
 def test_small_batch_path(ctx, n, k, q):
     """Batches of <= 64 targets take the small-batch path (one pass over word 0 + one
-    workgroup per target prefix, the K1 scan for short subtrees): bit-exact like K6.  q = 1 and
-    q <= 8 run S1's register prefix check, q > 8 its LDS bitmap."""
+    workgroup per target prefix, the K1 scan for short subtrees): bit-exact like K6.  q = 1 runs
+    S1's register prefix check, q > 1 its LDS bitmap."""
     ids = O.gen_ids(3000 + n, n)
     tg = O.gen_ids(3100 + q, q)
     ctx.set_ids(ids)
@@ -686,7 +689,7 @@ def test_small_batch_path(ctx, n, k, q):
 def test_small_batch_clusters_duplicates_fallback(ctx, rows):
     """Small batches over clustered ids (w0 ties, buckets past their capacity, subtrees short
     of k ids: the K1 fallback), targets sharing a prefix (one bucket, several targets) and
-    duplicated ids; the whole batch and sub-batches of 8 and 1 (S1's register prefix check)."""
+    duplicated ids; the whole batch and sub-batches of 8 and 1 (q = 1: S1's register prefix check)."""
     ids = O.gen_ids(51, 40000)
     ids[:20000, :4] = ids[0, :4]          # 20,000 ids in one 32-bit prefix: bucket overflow
     ids[:5000, 4:8] = ids[0, 4:8]

@@ -1,5 +1,5 @@
 # Build libdhtgpu at a commit (default HEAD) into opendht_amd/ab/<name>.so for A/B runs against
-# the in-tree build (tools/gpu_ab_lib.sh, tools/gpu_ab_libs.sh).   usage: bash tools/build_prev.sh [rev] [name]
+# the in-tree build (tools/experiments/gpu_ab_lib.sh, tools/experiments/gpu_ab_libs.sh).   usage: bash tools/experiments/build_prev.sh [rev] [name]
 set -e
 REV=${1:-HEAD}; NAME=${2:-prev}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)

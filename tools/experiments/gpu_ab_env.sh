@@ -1,5 +1,5 @@
 # A/B of one library knob (an environment variable) on the cfg-2 headline and the probes.
-# usage: bash tools/gpu_ab_env.sh <out-tag> <VAR=value for B> [test-selection]
+# usage: bash tools/experiments/gpu_ab_env.sh <out-tag> <VAR=value for B> [test-selection]
 # Runs the named GPU tests first (default: the K6 parity + fuzz suites), then alternates
 # A (knob unset) and B over 1,000-step and 20-step benches, then the per-kernel event probe.
 set -o pipefail

@@ -1,7 +1,7 @@
 # A/B of two builds of libdhtgpu on the cfg-2 headline: A = opendht_amd/ab/prev.so (an earlier
 # commit, built by hand), B = the in-tree build.  GPU tests of B first (default: the K6 parity +
 # fuzz suites), then alternating 1,000- and 20-step benches, then the per-kernel event probes.
-# usage: bash tools/gpu_ab_lib.sh <out-tag> [test-selection | none]
+# usage: bash tools/experiments/gpu_ab_lib.sh <out-tag> [test-selection | none]
 set -o pipefail
 TAG=$1; SEL=${2:-"tests/test_gpu_parity.py tests/test_gpu_fuzz.py"}
 OUT=gpurun_out/$TAG; mkdir -p $OUT

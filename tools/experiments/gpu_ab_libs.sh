@@ -1,6 +1,6 @@
 # Compare several builds of libdhtgpu on the cfg-2 headline (1,000- and 20-step benches, rotated
 # twice) and the cfg-3 shard probe.  Builds: name=path pairs ("tree" = the in-tree build).
-# usage: bash tools/gpu_ab_libs.sh <out-tag> "<tests | none>" name=path [name=path ...]
+# usage: bash tools/experiments/gpu_ab_libs.sh <out-tag> "<tests | none>" name=path [name=path ...]
 set -o pipefail
 TAG=$1; SEL=$2; shift 2
 OUT=gpurun_out/$TAG; mkdir -p $OUT

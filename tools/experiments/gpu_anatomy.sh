@@ -2,7 +2,7 @@
 #   A   opendht_amd/ab/prev.so (an earlier commit)
 #   B   the in-tree build
 #   F12 the in-tree build with DHTGPU_DBG=1: F1 + F2 only (measurement)
-# then the cfg-3 shard probe on A and B.   usage: bash tools/gpu_anatomy.sh <tag> [tests]
+# then the cfg-3 shard probe on A and B.   usage: bash tools/experiments/gpu_anatomy.sh <tag> [tests]
 set -o pipefail
 TAG=$1; SEL=${2:-none}
 OUT=gpurun_out/$TAG; mkdir -p $OUT

@@ -1,5 +1,5 @@
 # K2 (cfg 4 classify, 10^8 ids) across library builds: name=path pairs ("tree" = in-tree),
-# classify_probe.py three times each, rotated.   usage: bash tools/gpu_k2_libs.sh <tag> name=path ...
+# classify_probe.py three times each, rotated.   usage: bash tools/experiments/gpu_k2_libs.sh <tag> name=path ...
 set -o pipefail
 TAG=$1; shift; OUT=gpurun_out/$TAG; mkdir -p $OUT
 for i in 1 2 3; do

@@ -1,7 +1,7 @@
 # Round-3 final evidence at HEAD: the whole GPU suite and smoke(), the driver's bench (20 steps,
 # every leg, CPU baseline), the 1,000-step headline, a 2-rank rehearsal of the N > 1 path on one
 # GPU (bench.py --gpus 2 starting its ranks itself; gloo: RCCL refuses two ranks on one GPU),
-# F2/F3 phase stamps.   usage: bash tools/gpu_r03_final.sh [out-tag]
+# F2/F3 phase stamps.   usage: bash tools/experiments/gpu_r03_final.sh [out-tag]
 set -o pipefail
 OUT=gpurun_out/${1:-r03final}; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -40 $OUT/gpu_tests.log; exit 1; }

@@ -1,7 +1,7 @@
 # Round-3 pass B: the whole GPU parity suite, KS timings, and the counter evidence:
 # PMC HBM traffic (separate FETCH_SIZE / WRITE_SIZE passes) for KS at q = 1 / 8 / 32, K6 at
 # cfg 2 (warm and Infinity-Cache-evicted) and the 2^27-id cfg-3 shard, plus a rocprofv3 kernel
-# trace of the cfg-3 shard.   usage: bash tools/gpu_r03b.sh <out-tag> [skip-tests]
+# trace of the cfg-3 shard.   usage: bash tools/experiments/gpu_r03b.sh <out-tag> [skip-tests]
 set -o pipefail
 TAG=${1:-r03b}; OUT=gpurun_out/$TAG; mkdir -p $OUT profiles/r03
 export TMPDIR=/tmp

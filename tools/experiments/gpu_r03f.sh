@@ -3,7 +3,7 @@
 #  2. PMC HBM traffic (separate FETCH_SIZE / WRITE_SIZE passes): KS at q = 1 / 8 / 32, K6 at cfg 2
 #     (warm, Infinity-Cache evicted), the 2^27-id cfg-3 shard, K2 at 10^8 ids
 #  3. rocprofv3 kernel traces: cfg-3 shard, K2, the bench's 20-step run
-# usage: bash tools/gpu_r03f.sh [out-tag]
+# usage: bash tools/experiments/gpu_r03f.sh [out-tag]
 set -o pipefail
 TAG=${1:-r03f}; OUT=gpurun_out/$TAG; mkdir -p $OUT
 export TMPDIR=/tmp

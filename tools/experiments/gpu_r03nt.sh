@@ -1,7 +1,7 @@
 # Round-3 pass NT: counters and kernel traces after the non-temporal stream loads (S1; F2 on
 # sub-partitioned sets past the Infinity Cache): PMC HBM traffic of KS q = 1 / 8 / 32 and the
 # cfg-3 shard (merged into a copy of profiles/r03/pmc_traffic.json), rocprofv3 kernel traces of
-# the cfg-3 shard and KS.   usage: bash tools/gpu_r03nt.sh [out-tag]
+# the cfg-3 shard and KS.   usage: bash tools/experiments/gpu_r03nt.sh [out-tag]
 set -o pipefail
 TAG=${1:-r03nt}; OUT=gpurun_out/$TAG; mkdir -p $OUT
 export TMPDIR=/tmp

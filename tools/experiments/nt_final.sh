@@ -10,4 +10,4 @@ for i in 1 2; do
     echo -n "${nv%%=*} "; timeout -k 10 120 env $lib X=1 python tools/small_probe.py --q 1 8 64 2>/dev/null | tr '\n' ' '; echo
   done
 done | tee $OUT/ks.txt
-bash tools/gpu_ab_libs.sh ntfin2 none head=opendht_amd/ab/head.so tree=tree
+bash tools/experiments/gpu_ab_libs.sh ntfin2 none head=opendht_amd/ab/head.so tree=tree
