@@ -16,16 +16,23 @@ Algorithms (--algo):
 Nothing is cached between steps in any algorithm.
 
 Multi-GPU (one process per GPU, torch.distributed over RCCL; --route):
-  prefix     (default for a power-of-two world) ids AND targets are partitioned by their
-             top log2(N) bits; each rank answers only its own targets from its own shard.
-             If every shard holds >= k ids, a target's top-k provably lies in its own
-             prefix subtree, so the data path needs no collective; the setup checks the
-             minimum shard size with one all-reduce and refuses otherwise.
-  broadcast  ids range-sharded, all targets on every rank, per-rank candidate records
-             exchanged by one RCCL all-gather, merged by K3 (SURVEY §8(e) north-star scheme).
-Scaling (--scaling): "weak" (default with the prefix route: every rank keeps the one-GPU
-workload -- --n ids and --q targets per GPU out of a global problem N times as large; value =
-all ranks' targets / the slowest rank's time) or "strong" (--n and --q are global totals).
+  broadcast  (default for N > 1; SURVEY §8(e) north-star scheme) the metric's own workload,
+             strong scaling: the 2^24 cfg-2 ids range-sharded over the ranks, all 65,536 targets
+             on every rank, K6 in record mode per rank (k candidate records of 24 B per target),
+             one RCCL exchange (--exchange allgather: all_gather_into_tensor, every rank merges
+             every target; alltoall: all_to_all_single by target slice, each rank merges its
+             q / N targets), K3 merge.  value = the 65,536 targets / the slowest rank's step.
+             Consecutive steps rotate over --inflight streams, so one step's exchange overlaps
+             the next step's K6.  The other exchange and the prefix route are measured beside
+             it (extra: broadcast_<exchange>, prefix_weak), each labelled.
+  prefix     ids AND targets are partitioned by their top log2(N) bits; each rank answers only
+             its own targets from its own shard.  If every shard holds >= k ids, a target's
+             top-k provably lies in its own prefix subtree, so the data path needs no
+             collective; the setup checks the minimum shard size with one all-reduce.
+Scaling (--scaling): "strong" (default with the broadcast route: --n and --q are global
+totals) or "weak" (default with the prefix route: every rank keeps the one-GPU workload --
+--n ids and --q targets per GPU out of a global problem N times as large; value = all ranks'
+targets / the slowest rank's time).  N = 1 runs the one-GPU K6 over the whole set.
 
 Beside the headline (`value`) the line carries, measured in the same run:
   roofline        F2 (the dominant K6 kernel) timed by events its own dispatches record in
@@ -55,6 +62,74 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); N > 1 outside torch.distributed.run re-launches itself under it")
+    ap.add_argument("--dry-run", action="store_true", help="print the launch plan and exit (no GPU)")
+    ap.add_argument("--dry-run-ranks", action="store_true",
+                    help="launch the ranks for real; each prints its identity and exits (no GPU)")
+    ap.add_argument("--steps", type=int, default=1000)   # ~40 ms timed: steady state, not ramp-up
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--n", type=int, default=1 << 24, help="node ids (per GPU with weak scaling)")
+    ap.add_argument("--q", type=int, default=65536, help="targets per step (per GPU with weak scaling)")
+    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--algo", choices=["batch", "index", "scan"], default="batch")
+    ap.add_argument("--route", choices=["auto", "prefix", "broadcast"], default="auto",
+                    help="auto = broadcast for N > 1 (the metric's workload, strong scaling), the whole set at N = 1")
+    ap.add_argument("--exchange", choices=["allgather", "alltoall"], default="allgather",
+                    help="broadcast route: RCCL all-gather of the candidate records (north star) or all-to-all by "
+                         "target slice")
+    ap.add_argument("--shard-index", choices=["local", "global"], default="local",
+                    help="prefix shards: results as shard-local node indices (the rank owns its shard's "
+                         "node table) or mapped to global stream indices (one gather per result)")
+    ap.add_argument("--scaling", choices=["auto", "weak", "strong"], default="auto",
+                    help="weak: --n/--q per GPU (global problem grows with N); strong: --n/--q global. "
+                         "auto = weak for the prefix route, strong for broadcast")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="multi-rank correctness rehearsal on a one-GPU box: every rank on cuda:0, gloo "
+                         "process group (timings are contended; not a scaling measurement)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="use the multi-GPU code path (and its collectives) even with one rank")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="prefix route only: run rank --simulate-rank of a world of this size on one GPU")
+    ap.add_argument("--simulate-rank", type=int, default=0)
+    ap.add_argument("--cpu-targets", type=int, default=256, help="cpu_baseline sample (targets, all host threads)")
+    ap.add_argument("--cpu-threads", type=int, default=os.cpu_count() or 1,
+                    help="cpu_baseline threads (default: every host CPU, nproc; the rate at the job's cgroup CPU "
+                         "quota and the single-core figures are reported too)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the extra legs (small batch, cfg 1/3/4/5)")
+    ap.add_argument("--no-scan", action="store_true", help="skip the reference K1 scan measurement")
+    ap.add_argument("--verify", type=int, default=16, help="targets re-checked against the oracle (rank 0)")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="batch algo: consecutive steps rotate over this many streams, so one step's "
+                         "latency-bound F3/F4 overlaps the other steps' HBM-bound F2 (1 = strictly serial; "
+                         "3 measured best: 2 leaves each stream's F1-F4 chain exposed, 4 over-subscribes F2); "
+                         "broadcast route: one step's exchange + merge overlap the next step's K6")
+    return ap.parse_args(argv)
+
+
+def run_plan(a, world):
+    """The workload a run measures (pure: tests/test_bench_launch.py asserts the defaults).
+    N > 1 defaults to the metric's own workload -- 2^24 ids and 65,536 targets in TOTAL -- on
+    the broadcast route (SURVEY §8(e) north star) with strong scaling; N = 1 is the one-GPU K6
+    over the whole set (one range shard, no collective): the first point of the same strong-scaling
+    series."""
+    pow2 = lambda g: g > 0 and (g & (g - 1)) == 0
+    route = a.route
+    if route == "auto":   # N = 1: one range shard = the whole set, no collective
+        route = "broadcast"
+    if route == "prefix" and not pow2(a.simulate_world or world):
+        raise SystemExit("the prefix route needs a power-of-two world")
+    scaling = a.scaling if a.scaling != "auto" else ("weak" if route == "prefix" else "strong")
+    G = a.simulate_world if a.simulate_world else world
+    n_total, q_total = (a.n * G, a.q * G) if scaling == "weak" else (a.n, a.q)
+    return {"route": route, "scaling": scaling, "world": G, "n_total": n_total, "q_total": q_total,
+            "exchange": a.exchange if route == "broadcast" and world > 1 else None}
 
 
 def launcher_cmd(gpus, argv):
@@ -90,9 +165,11 @@ def maybe_launch(argv):
     if a.dry_run or a.dry_run_ranks:
         # one write of line + newline: the ranks share the launcher's stdout pipe, and a write
         # under PIPE_BUF bytes is atomic there (print's separate newline write could interleave)
+        world = int(env_world or 1)
         line = json.dumps({"mode": "rank" if env_world is not None else "single", "gpus": a.gpus,
-                           "world_size": int(env_world or 1), "rank": int(os.environ.get("RANK", "0")),
-                           "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}) + "\n"
+                           "world_size": world, "rank": int(os.environ.get("RANK", "0")),
+                           "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                           "plan": run_plan(parse(argv), world)}) + "\n"
         os.write(sys.stdout.fileno(), line.encode())
         return 0
     return None
@@ -128,51 +205,7 @@ HBM_PEAK_GBS = 8000.0
 # 64-bit lane; both fractions are reported (the packed prefilter is an algorithmic win).
 OPS_PER_PAIR = 1.0
 SURVEY_OPS_PER_PAIR = 3.0
-PMC_FILE = "profiles/r03/pmc_traffic.json"
-
-
-def parse():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1,
-                    help="ranks (one per GPU); N > 1 outside torch.distributed.run re-launches itself under it")
-    ap.add_argument("--dry-run", action="store_true", help="print the launch plan and exit (no GPU)")
-    ap.add_argument("--dry-run-ranks", action="store_true",
-                    help="launch the ranks for real; each prints its identity and exits (no GPU)")
-    ap.add_argument("--steps", type=int, default=1000)   # ~40 ms timed: steady state, not ramp-up
-    ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--n", type=int, default=1 << 24, help="node ids (per GPU with weak scaling)")
-    ap.add_argument("--q", type=int, default=65536, help="targets per step (per GPU with weak scaling)")
-    ap.add_argument("--k", type=int, default=8)
-    ap.add_argument("--seed", type=int, default=2024)
-    ap.add_argument("--algo", choices=["batch", "index", "scan"], default="batch")
-    ap.add_argument("--route", choices=["auto", "prefix", "broadcast"], default="auto")
-    ap.add_argument("--shard-index", choices=["local", "global"], default="local",
-                    help="prefix shards: results as shard-local node indices (the rank owns its shard's "
-                         "node table) or mapped to global stream indices (one gather per result)")
-    ap.add_argument("--scaling", choices=["auto", "weak", "strong"], default="auto",
-                    help="weak: --n/--q per GPU (global problem grows with N); strong: --n/--q global. "
-                         "auto = weak for the prefix route, strong for broadcast")
-    ap.add_argument("--rehearse-one-gpu", action="store_true",
-                    help="multi-rank correctness rehearsal on a one-GPU box: every rank on cuda:0, gloo "
-                         "process group (timings are contended; not a scaling measurement)")
-    ap.add_argument("--sharded", action="store_true",
-                    help="use the multi-GPU code path (and its collectives) even with one rank")
-    ap.add_argument("--simulate-world", type=int, default=0,
-                    help="prefix route only: run rank --simulate-rank of a world of this size on one GPU")
-    ap.add_argument("--simulate-rank", type=int, default=0)
-    ap.add_argument("--cpu-targets", type=int, default=256, help="cpu_baseline sample (targets, all host threads)")
-    ap.add_argument("--cpu-threads", type=int, default=os.cpu_count() or 1,
-                    help="cpu_baseline threads (default: every host CPU, nproc; the rate at the job's cgroup CPU "
-                         "quota and the single-core figures are reported too)")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip the extra legs (small batch, cfg 1/3/4/5)")
-    ap.add_argument("--no-scan", action="store_true", help="skip the reference K1 scan measurement")
-    ap.add_argument("--verify", type=int, default=16, help="targets re-checked against the oracle (rank 0)")
-    ap.add_argument("--inflight", type=int, default=3,
-                    help="batch algo: consecutive steps rotate over this many streams, so one step's "
-                         "latency-bound F3/F4 overlaps the other steps' HBM-bound F2 (1 = strictly serial; "
-                         "3 measured best: 2 leaves each stream's F1-F4 chain exposed, 4 over-subscribes F2)")
-    return ap.parse_args()
+PMC_FILE = "profiles/r04/pmc_traffic.json"
 
 
 def oracle():
@@ -358,18 +391,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.rehearse_one_gpu:
         local = 0
-    pow2 = lambda g: g > 0 and (g & (g - 1)) == 0
-    route = a.route
-    if route == "auto":
-        route = "prefix" if (a.algo in ("index", "batch") and pow2(world)) else "broadcast"
     if a.simulate_world:
-        assert world == 1 and route == "prefix" and pow2(a.simulate_world)
-    scaling = a.scaling if a.scaling != "auto" else ("weak" if route == "prefix" else "strong")
-    G_eff = a.simulate_world if a.simulate_world else world
-    if scaling == "weak":   # --n / --q are per GPU: the global problem is G times larger
-        a.n_total, a.q_total = a.n * G_eff, a.q * G_eff
-    else:
-        a.n_total, a.q_total = a.n, a.q
+        assert world == 1 and a.route == "prefix", "--simulate-world runs one rank of the prefix route"
+    plan = run_plan(a, world)
+    route, scaling, G_eff = plan["route"], plan["scaling"], plan["world"]
+    a.n_total, a.q_total = plan["n_total"], plan["q_total"]
     use_dist = world > 1 or a.sharded
     if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -419,9 +445,11 @@ def main():
         tp, q_local, tgidx = tp_all, a.q_total, None
         n_local = hi - lo
     collective = use_dist and route == "broadcast"
-    qk = max(q_local, 1)
-    rec = torch.empty((a.q_total, a.k, 6), dtype=torch.int32, device=dev) if collective else None
-    gathered = torch.empty((world * a.q_total, a.k, 6), dtype=torch.int32, device=dev) if collective else None
+    a2a = collective and plan["exchange"] == "alltoall"
+    # alltoall: this rank merges (and owns the results of) targets [tlo, thi)
+    tlo, thi = sharding.shard_range(a.q_total, world, rank) if a2a else (0, a.q_total)
+    q_out = thi - tlo if collective else q_local
+    qk = max(q_out, 1)
 
     def local_lookup(out_i, out_c, out_r, base, s=stream):
         if a.algo == "batch":
@@ -432,25 +460,45 @@ def main():
         else:
             ctx.topk_dev(tp.data_ptr(), ts, q_local, a.k, out_i, out_c, out_r, base, s)
 
-    # in-flight calls: step i runs on stream i % D with its own output buffers
-    D = max(1, a.inflight) if (a.algo == "batch" and not collective) else 1
+    # in-flight calls: step i runs on stream i % D with its own buffers (broadcast route: K6 of
+    # step i + 1 runs while step i's records cross xGMI -- RCCL orders its collectives on its own
+    # stream after each step's K6, and the merge waits for its collective)
+    D = max(1, a.inflight) if a.algo == "batch" else 1
     streams = [tstream] + [torch.cuda.Stream(dev) for _ in range(D - 1)]
     outs = [(torch.empty((qk, a.k), dtype=torch.int32, device=dev), torch.empty(qk, dtype=torch.int32, device=dev))
             for _ in range(D)]
     out_idx, out_cnt = outs[0]
+    # the diagnostics' one-rank calls answer all q_local targets (alltoall: more rows than q_out)
+    dg_idx, dg_cnt = (out_idx, out_cnt) if q_out >= q_local else \
+        (torch.empty((max(q_local, 1), a.k), dtype=torch.int32, device=dev),
+         torch.empty(max(q_local, 1), dtype=torch.int32, device=dev))
+    recs = [torch.empty((a.q_total, a.k, 6), dtype=torch.int32, device=dev) for _ in range(D)] if collective else None
+    rec = recs[0] if collective else None
+    xbufs = [torch.empty((world * q_out, a.k, 6), dtype=torch.int32, device=dev) for _ in range(D)] \
+        if collective else None
     step_no = [0]
+
+    def exchange_merge(r, xb, oi, oc, s):
+        """the records of every rank for this rank's merged targets, then K3 (same stream)"""
+        if a2a:
+            sharding.exchange_records(r, out=xb)
+        else:
+            sharding.gather_records(r, out=xb)
+        if q_out:
+            assert L.dhtgpu_merge_dev(xb.data_ptr(), world, q_out, a.k, tp.data_ptr() + 4 * tlo, ts, a.k,
+                                      oi.data_ptr(), oc.data_ptr(), s) == 0
 
     def step():
         i = step_no[0]
         step_no[0] += 1
+        oi, oc = outs[i % D]
+        st_ = streams[i % D]
         if not collective:
-            oi, oc = outs[i % D]
-            local_lookup(oi.data_ptr(), oc.data_ptr(), None, 0, streams[i % D].cuda_stream)
+            local_lookup(oi.data_ptr(), oc.data_ptr(), None, 0, st_.cuda_stream)
         else:
-            local_lookup(None, None, rec.data_ptr(), lo)
-            sharding.gather_records(rec, out=gathered)
-            assert L.dhtgpu_merge_dev(gathered.data_ptr(), world, a.q_total, a.k, tp.data_ptr(), ts, a.k,
-                                      out_idx.data_ptr(), out_cnt.data_ptr(), stream) == 0
+            with torch.cuda.stream(st_):   # the collective runs after this stream's K6
+                local_lookup(None, None, recs[i % D].data_ptr(), lo, st_.cuda_stream)
+                exchange_merge(recs[i % D], xbufs[i % D], oi, oc, st_.cuda_stream)
 
     progress(f"setup done: {n_local} ids, {q_local} targets on this rank; warmup")
     for _ in range(a.warmup):
@@ -482,20 +530,26 @@ def main():
     wall = float(t.item())
     ms_per_step = wall * 1e3 / a.steps
     last = (step_no[0] - 1) % D
-    got_idx = outs[last][0][:q_local].cpu().numpy().view(np.uint32).copy() if not collective \
-        else out_idx.cpu().numpy().view(np.uint32).copy()
-    got_tg = tgidx[:q_local].cpu().numpy().view(np.uint32).copy() if tgidx is not None else np.arange(q_local)
+    got_idx = outs[last][0][:q_out].cpu().numpy().view(np.uint32).copy()
+    got_tg = tgidx[:q_local].cpu().numpy().view(np.uint32).copy() if tgidx is not None \
+        else np.arange(tlo, tlo + q_out)
     progress(f"timed {a.steps} steps: {ms_per_step:.4f} ms/step; diagnostics")
     reps = max(3, min(a.steps, 20))
     res = {}
     extra = {}
-    # single-batch latency: the same step strictly serial on one stream
-    lat_ms = ev_time(lambda: local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0), reps, tstream) \
-        if not collective else None
+    # single-batch latency: the same step strictly serial on one stream (broadcast route: K6 in
+    # record mode + the exchange + K3 on every rank)
+    if collective:
+        if use_dist:
+            dist.barrier()
+        lat_ms = ev_time(lambda: (local_lookup(None, None, rec.data_ptr(), lo),
+                                  exchange_merge(rec, xbufs[0], out_idx, out_cnt, stream)), reps, tstream)
+    else:
+        lat_ms = ev_time(lambda: local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0), reps, tstream)
     if route == "prefix" and pbits and a.shard_index == "local":
         ctx.set_global_indices(True)
         extra["latency_ms_per_batch_global_indices"] = ev_time(
-            lambda: local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0), reps, tstream)
+            lambda: local_lookup(dg_idx.data_ptr(), dg_cnt.data_ptr(), None, 0), reps, tstream)
         ctx.set_global_indices(False)
     if a.algo == "batch":
         # per-kernel device time: HIP events recorded by the kernels' own dispatches
@@ -505,10 +559,10 @@ def main():
         kt = EvSets(reps, tstream)
         for _ in range(reps):
             kt.arm(ctx)
-            local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), rec.data_ptr() if collective else None, lo)
+            local_lookup(dg_idx.data_ptr(), dg_cnt.data_ptr(), rec.data_ptr() if collective else None, lo)
         live = kt.mean_ms()
-        tms, n_fb, surv, n_slow = ctx.batch_topk_timed(tp.data_ptr(), ts, q_local, a.k, out_idx.data_ptr(),
-                                                       out_cnt.data_ptr(), stream)
+        tms, n_fb, surv, n_slow = ctx.batch_topk_timed(tp.data_ptr(), ts, q_local, a.k, dg_idx.data_ptr(),
+                                                       dg_cnt.data_ptr(), stream)
         kern = k6_kernels(live, n_local, q_local, a.k, surv)
         dom = "k_f2_filter"
         dom_ms, dom_bytes = kern[dom]
@@ -537,14 +591,21 @@ def main():
         if use_dist:
             # aggregate over the ranks: every rank's F2 bytes / the slowest rank's F2 time, against
             # world x the one-GPU peak (each rank streams its own shard from its own HBM)
-            agg = torch.tensor([float(dom_bytes), float(step_bytes)], dtype=torch.float64, device=dev)
+            # traffic: every rank's PMC bytes for its own shard workload (committed rocprofv3 passes
+            # keyed by the per-rank shard, tools/batch_probe.py --n n_local); None if a rank has none
+            agg = torch.tensor([float(dom_bytes), float(step_bytes), float(tb or 0.0), 0.0 if tb else 1.0],
+                               dtype=torch.float64, device=dev)
             slow = torch.tensor([dom_ms], dtype=torch.float64, device=dev)
             dist.all_reduce(agg, op=dist.ReduceOp.SUM)
             dist.all_reduce(slow, op=dist.ReduceOp.MAX)
             ab, sb, sm = float(agg[0].item()), float(agg[1].item()), float(slow.item())
+            tball = float(agg[2].item()) if float(agg[3].item()) == 0.0 else None
             roof["aggregate"] = {"ranks": world, "alg_bytes_all_ranks": ab, "slowest_rank_kernel_ms": sm,
                                  "achieved": ab / (sm * 1e-3) / 1e9, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
                                  "frac": ab / (sm * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
+                                 "traffic": tball / (sm * 1e-3) / 1e9 if tball else None,
+                                 "traffic_bytes_all_ranks": tball,
+                                 "traffic_source": f"{PMC_FILE} workloads[{wl!r}] per rank" if tball else None,
                                  "step_frac": sb / (ms_per_step * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
                                  "how": "sum of the ranks' F2 algorithmic bytes / the slowest rank's F2 time / "
                                         "(ranks x 8 TB/s); step_frac: all four kernels' bytes over the timed step"}
@@ -554,7 +615,7 @@ def main():
         for _ in range(8):
             l3_evict(ebuf)
             cold.arm(ctx)
-            local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(), None, 0)
+            local_lookup(dg_idx.data_ptr(), dg_cnt.data_ptr(), None, 0)
         cms = cold.mean_ms()
         del ebuf
         ckern = k6_kernels(cms, n_local, q_local, a.k, surv)
@@ -568,8 +629,8 @@ def main():
     elif a.algo == "index":
         phases = [ctx.index_build_timed(stream) for _ in range(reps)]
         ph = [sum(p[i] for p in phases) / reps for i in range(4)]
-        q_ms = ev_time(lambda: ctx.index_topk_dev(tp.data_ptr(), ts, q_local, a.k, out_idx.data_ptr(),
-                                                  out_cnt.data_ptr(), None, 0, stream), reps, tstream)
+        q_ms = ev_time(lambda: ctx.index_topk_dev(tp.data_ptr(), ts, q_local, a.k, dg_idx.data_ptr(),
+                                                  dg_cnt.data_ptr(), None, 0, stream), reps, tstream)
         kern = {"k_p0_hist": (ph[0], 4 * n_local), "k_p0_scans": (ph[1], 0),
                 "k_p1_scatter": (ph[2], 12 * n_local), "k_p2_buckets": (ph[3], 16 * n_local),
                 "k_query": (q_ms, q_local * (20 + a.k * 4))}
@@ -581,7 +642,7 @@ def main():
                 "kernels_ms": {k: v[0] for k, v in kern.items()}}
         extra.update({"query_only_qps_per_gpu": q_local / (q_ms * 1e-3), "index_build_ms": sum(ph)})
     else:
-        kern_ms = ev_time(lambda: local_lookup(out_idx.data_ptr(), out_cnt.data_ptr(),
+        kern_ms = ev_time(lambda: local_lookup(dg_idx.data_ptr(), dg_cnt.data_ptr(),
                                                rec.data_ptr() if collective else None, lo), reps, tstream)
         pairs = q_local * n_local
         achieved = OPS_PER_PAIR * pairs / (kern_ms * 1e-3) / 1e12
@@ -608,7 +669,7 @@ def main():
     single = world == 1 and not a.simulate_world and not a.no_extra and a.algo == "batch"
     if single:
         progress("small-batch and table legs")
-        extra["small_batch"] = small_batch_leg(ctx, tp, ts, n_local, a.k, stream, tstream, dev)
+        extra["small_batch"] = small_batch_leg(ctx, tp, ts, n_local, a.k, stream, tstream, dev, a.seed)
         extra["find_closest"] = find_closest_leg(ctx, a, dev)
         ctx.close()   # the cfg-2 set is no longer needed: free HBM for the size legs
         ctx = None
@@ -618,6 +679,21 @@ def main():
                 extra[name] = fn(a, L, dev, stream, tstream)
             except Exception as e:  # noqa: BLE001 -- an extra leg must not cost the headline
                 extra[name] = {"error": repr(e)}
+    if world > 1 and not a.no_extra and a.algo == "batch" and route == "broadcast" and not a.simulate_world:
+        # the same cfg-2 problem with the other exchange, and the prefix route (weak scaling),
+        # each labelled; measured after the headline, on fresh contexts
+        progress("N > 1 legs: the other exchange, the prefix route")
+        other = "alltoall" if plan["exchange"] == "allgather" else "allgather"
+        try:
+            extra[f"broadcast_{other}"] = broadcast_leg(a, L, dev, world, rank, other, tp_all, ts, ctx, lo,
+                                                        got_idx.reshape(-1, a.k), tlo)
+        except Exception as e:  # noqa: BLE001 -- an extra leg must not cost the headline
+            extra[f"broadcast_{other}"] = {"error": repr(e)}
+        try:
+            if (world & (world - 1)) == 0:
+                extra["prefix_weak"] = prefix_weak_leg(a, L, dev, world, rank)
+        except Exception as e:  # noqa: BLE001
+            extra["prefix_weak"] = {"error": repr(e)}
     if world > 1 and not a.no_extra and a.algo == "batch" and not a.rehearse_one_gpu:
         progress("cfg3 leg over the ranks")
         try:
@@ -630,7 +706,8 @@ def main():
 
     if rank == 0:
         par = {"prefix": f"prefix-routed shards x{G} (top {pbits} id bits; no data-path collective)",
-               "broadcast": f"id-range shards x{world}" + (" + RCCL all-gather + K3 merge" if collective else "")}[route]
+               "broadcast": f"id-range shards x{world}" + ((" + RCCL all-to-all by target slice + K3 merge" if a2a else
+                                                             " + RCCL all-gather + K3 merge") if collective else "")}[route]
         res = {
             "metric": METRIC,
             "value": (a.q_total if not a.simulate_world else q_local) / (ms_per_step * 1e-3),
@@ -653,7 +730,8 @@ def main():
                                       if scaling == "weak" and G_eff > 1 else ""),
                        "n_ids": a.n_total, "n_targets": a.q_total, "k": a.k, "algo": a.algo, "route": route,
                        "ids_per_gpu": n_local, "targets_per_gpu": q_local, "parallelism": par,
-                       "inflight": D,
+                       "inflight": D, "exchange": plan["exchange"],
+                       "results_on_this_rank": f"targets [{tlo}, {tlo + q_out})" if collective else None,
                        "result_indices": ("shard-local" if a.shard_index == "local" else "global")
                        if route == "prefix" and pbits else "global"},
             "latency_ms_per_batch": lat_ms,
@@ -666,7 +744,7 @@ def main():
         if not a.no_cpu and (a.verify or world == 1):
             progress("verifying against the oracle")
             O = oracle()
-            nv = min(q_local, max(a.verify, a.cpu_targets if world == 1 else 0))
+            nv = min(q_out, max(a.verify, a.cpu_targets if world == 1 else 0))
             tg_all = O.gen_ids(a.seed + 1, a.q_total)
             tg = tg_all[got_tg[:nv]]
             local_ix = route == "prefix" and pbits and a.shard_index == "local"
@@ -692,37 +770,86 @@ def main():
         dist.destroy_process_group()
 
 
-def small_batch_leg(ctx, tp, ts, n, k, stream, tstream, dev):
-    """Q = 1 / 8 / 32 / 64 targets over the same id set: latency per call and the bytes the call
-    has to stream (4 B/id of the w0 plane; SURVEY's contract counts 20 B/id).  The library's
-    batch entry point takes the small-batch path (KS: S1 one pass over w0, S2 one workgroup per
-    target prefix beside the scan roles that answer short subtrees -- none here) for q <= 64; K1
-    is the plain scan beside it."""
+def small_batch_leg(ctx, tp, ts, n, k, stream, tstream, dev, seed=2024):
+    """Q = 1 / 8 / 32 / 64 targets -- the reference's real call pattern is one target per request
+    (src/dht.cpp:2128-2138 -> findClosestNodes): latency per call and the bytes the call has to
+    stream (4 B/id of the w0 plane; SURVEY's contract counts 20 B/id).  The library's batch entry
+    point takes the small-batch path (KS: S1 one pass over w0, S2 one workgroup per target prefix
+    beside the scan roles that answer short subtrees -- none here) for q <= 64; K1 is the plain
+    scan beside it.  Three regimes per q:
+      warm  the cfg-2 set (67 MB w0 plane) stays in the 256 MiB Infinity Cache between calls
+      cold  the same set with the Infinity Cache evicted before every call (512 MiB read): S1
+            streams HBM
+      big   a 2^26-id set (268 MB w0 plane, past the Infinity Cache), warm and cold"""
     out = {}
     oi = torch.empty((64, k), dtype=torch.int32, device=dev)
     oc = torch.empty(64, dtype=torch.int32, device=dev)
-    for q in (1, 8, 32, 64):
+    ebuf = torch.zeros(128 << 20, dtype=torch.int32, device=dev)
+
+    def cold_rows(c, nn, q, reps=9):
+        """per call: evict, then events around the call and its kernels' own dispatches"""
+        lat, s1, s2 = [], [], []
+        for _ in range(reps):
+            l3_evict(ebuf)
+            ev = EvSets(1, tstream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(tstream)
+            ev.arm(c)
+            c.batch_topk_dev(tp.data_ptr(), ts, q, k, oi.data_ptr(), oc.data_ptr(), None, 0, stream)
+            e1.record(tstream)
+            torch.cuda.synchronize()
+            lat.append(e0.elapsed_time(e1))
+            m = ev.mean_ms()
+            s1.append(m[1])
+            s2.append(m[2])
+        ms, s1m, s2m = float(np.median(lat)), float(np.median(s1)), float(np.median(s2))
+        return {"latency_ms": ms, "qps": q / (ms * 1e-3), "kernels_ms": {"k_s1_filter": s1m, "k_s2_answer": s2m},
+                "w0_frac": 4 * nn / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "s1_frac": 4 * nn / (s1m * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "timing": f"median of {reps} calls, each after a 512 MiB read (Infinity Cache evicted); events "
+                          "around the call and on its kernels' own dispatches",
+                "pmc_traffic_bytes_per_launch": {kn: pmc_traffic(f"ks:{nn}x{q}x{k}:cold", kn)
+                                                 for kn in ("k_s1_filter", "k_s2_answer")}}
+
+    def warm_rows(c, nn, q, with_k1):
         row = {}
-        for name, fn in (("batch", ctx.batch_topk_dev), ("k1", ctx.topk_dev)):
+        fns = (("batch", c.batch_topk_dev), ("k1", c.topk_dev)) if with_k1 else (("batch", c.batch_topk_dev),)
+        for name, fn in fns:
             call = lambda: fn(tp.data_ptr(), ts, q, k, oi.data_ptr(), oc.data_ptr(), None, 0, stream)
             call()
-            ms = ev_time(call, 20, tstream)
+            ms = ev_time(call, 20 if name == "batch" else 3, tstream)
             row[name] = {"latency_ms": ms, "qps": q / (ms * 1e-3),
-                         "w0_GBps": 4 * n / (ms * 1e-3) / 1e9, "w0_frac": 4 * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "contract_GBps": (20 * n + 24 * q + 4 * k * q) / (ms * 1e-3) / 1e9}
+                         "w0_GBps": 4 * nn / (ms * 1e-3) / 1e9, "w0_frac": 4 * nn / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "contract_GBps": (20 * nn + 24 * q + 4 * k * q) / (ms * 1e-3) / 1e9}
         ev = EvSets(9, tstream)
-        for _ in range(9):   # serial calls, median per kernel (one call's events were the r03 figure: noisy)
-            ev.arm(ctx)
-            ctx.batch_topk_dev(tp.data_ptr(), ts, q, k, oi.data_ptr(), oc.data_ptr(), None, 0, stream)
+        for _ in range(9):   # serial calls, median per kernel
+            ev.arm(c)
+            c.batch_topk_dev(tp.data_ptr(), ts, q, k, oi.data_ptr(), oc.data_ptr(), None, 0, stream)
         kms = ev.median_ms()
         row["kernels_ms"] = {"k_s1_filter": kms[1], "k_s2_answer (prefix answers + fallback scan roles)": kms[2]}
         row["kernel_timing"] = "median of 9 serial calls (events on the kernels' own dispatches)"
-        row["s1_frac"] = 4 * n / (kms[1] * 1e-3) / 1e9 / HBM_PEAK_GBS
-        # rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes of tools/small_probe.py (profiles/r03)
-        row["pmc_traffic_bytes_per_launch"] = {kn: pmc_traffic(f"ks:{n}x{q}x{k}", kn) for kn in ("k_s1_filter", "k_s2_answer")}
+        row["s1_frac"] = 4 * nn / (kms[1] * 1e-3) / 1e9 / HBM_PEAK_GBS
+        # rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes of tools/small_probe.py (profiles/r0x)
+        row["pmc_traffic_bytes_per_launch"] = {kn: pmc_traffic(f"ks:{nn}x{q}x{k}", kn) for kn in ("k_s1_filter", "k_s2_answer")}
+        return row
+
+    for q in (1, 8, 32, 64):
+        row = warm_rows(ctx, n, q, True)
+        row["cold"] = cold_rows(ctx, n, q)
         out[f"q{q}"] = row
-    out["note"] = ("id set L3-resident (the cfg-2 set); w0_frac = the 4 B/id w0 stream over the whole call's "
-                   "time; s1_frac = the same bytes over the S1 kernel alone")
+    nb = 1 << 26
+    big = opendht_amd.Context(dev.index)
+    try:
+        big.gen_ids(seed + 30, nb)
+        for q in (1, 8, 32, 64):
+            out[f"big_q{q}"] = {"warm": warm_rows(big, nb, q, False), "cold": cold_rows(big, nb, q)}
+    finally:
+        big.close()
+        del ebuf
+        torch.cuda.synchronize()
+    out["note"] = ("q<N>: the cfg-2 set (2^24 ids; warm rows L3-resident, .cold with the Infinity Cache evicted before "
+                   "each call); big_q<N>: a 2^26-id set (268 MB w0 plane > 256 MiB L3). w0_frac = the 4 B/id w0 stream "
+                   "over the whole call's time; s1_frac = the same bytes over the S1 kernel alone")
     return out
 
 
@@ -872,6 +999,101 @@ def cfg5_leg(a, L, dev, stream, tstream):
         return {"workload": f"{q} searches over {n} nodes (10% dead)", "ms_per_batch": ms,
                 "searches_per_s": q / (ms * 1e-3), "rounds_mean": float(o_rd.float().mean().item()),
                 "requests_mean": float(o_qs.float().mean().item()), "net_prepare_s": prep}
+    finally:
+        c.close()
+        torch.cuda.synchronize()
+
+
+def timed_steps(step, steps, warmup, dev):
+    """warmup, then `steps` timed calls of step() between barrier + synchronize pairs; the max
+    over ranks of the wall time, ms per step"""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    tm = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+    return float(tm.item()) * 1e3 / steps
+
+
+def broadcast_leg(a, L, dev, world, rank, exchange, tp, ts, ctx, lo, ref_idx, ref_lo):
+    """The headline's cfg-2 broadcast problem (same shard, same targets) with the other RCCL
+    exchange; steps rotate over --inflight streams as in the headline.  Checked equal to the
+    headline exchange on this rank's targets."""
+    q, k = a.q_total, a.k
+    D = max(1, a.inflight)
+    streams = [torch.cuda.Stream(dev) for _ in range(D)]
+    tlo, thi = sharding.shard_range(q, world, rank) if exchange == "alltoall" else (0, q)
+    qo = thi - tlo
+    recs = [torch.empty((q, k, 6), dtype=torch.int32, device=dev) for _ in range(D)]
+    xb = [torch.empty((world * qo, k, 6), dtype=torch.int32, device=dev) for _ in range(D)]
+    outs = [(torch.empty((max(qo, 1), k), dtype=torch.int32, device=dev),
+             torch.empty(max(qo, 1), dtype=torch.int32, device=dev)) for _ in range(D)]
+    n_call = [0]
+
+    def step():
+        i = n_call[0] % D
+        n_call[0] += 1
+        st = streams[i]
+        with torch.cuda.stream(st):
+            ctx.batch_topk_dev(tp.data_ptr(), ts, q, k, None, None, recs[i].data_ptr(), lo, st.cuda_stream)
+            if exchange == "alltoall":
+                sharding.exchange_records(recs[i], out=xb[i])
+            else:
+                sharding.gather_records(recs[i], out=xb[i])
+            if qo:
+                assert L.dhtgpu_merge_dev(xb[i].data_ptr(), world, qo, k, tp.data_ptr() + 4 * tlo, ts, k,
+                                          outs[i][0].data_ptr(), outs[i][1].data_ptr(), st.cuda_stream) == 0
+    ms = timed_steps(step, a.steps, a.warmup, dev)
+    last = (n_call[0] - 1) % D
+    got = outs[last][0][:qo].cpu().numpy().view(np.uint32)
+    # the rows both runs answered on this rank must agree (same shard, same targets)
+    a0, a1 = max(tlo, ref_lo), min(thi, ref_lo + ref_idx.shape[0])
+    same = bool(np.array_equal(got[a0 - tlo:a1 - tlo], ref_idx[a0 - ref_lo:a1 - ref_lo])) if a1 > a0 else None
+    return {"exchange": exchange, "ms_per_step": ms, "value": q / (ms * 1e-3), "unit": "queries/s",
+            "scaling": "strong (the headline's global batch)",
+            "exchange_bytes_in_per_gpu": (world * q if exchange == "allgather" else q) * k * 24,
+            "results_on_this_rank": f"targets [{tlo}, {thi})",
+            "equals_headline_rank0": same, "rows_compared_rank0": max(0, a1 - a0)}
+
+
+def prefix_weak_leg(a, L, dev, world, rank):
+    """The prefix route beside the headline (labelled): every rank keeps the one-GPU workload
+    (--n ids and --q targets per GPU, weak scaling), ids and targets routed by their top
+    log2(N) bits, no collective on the data path, shard-local result indices."""
+    pbits = world.bit_length() - 1
+    n_tot, q_tot = a.n * world, a.q * world
+    c = opendht_amd.Context(dev.index)
+    try:
+        c.gen_ids_prefix(a.seed + 20, n_tot, pbits, rank)
+        c.set_global_indices(False)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        tp_all, ts = gen_targets(L, a.seed + 21, q_tot, dev, s)
+        tp = torch.empty_like(tp_all)
+        ql = c.select_prefix_dev(tp_all.data_ptr(), ts, q_tot, pbits, rank, tp.data_ptr(), ts, None, s)
+        D = max(1, a.inflight)
+        streams = [torch.cuda.Stream(dev) for _ in range(D)]
+        outs = [(torch.empty((max(ql, 1), a.k), dtype=torch.int32, device=dev),
+                 torch.empty(max(ql, 1), dtype=torch.int32, device=dev)) for _ in range(D)]
+        n_call = [0]
+
+        def step():
+            i = n_call[0] % D
+            n_call[0] += 1
+            c.batch_topk_dev(tp.data_ptr(), ts, ql, a.k, outs[i][0].data_ptr(), outs[i][1].data_ptr(), None, 0,
+                             streams[i].cuda_stream)
+        ms = timed_steps(step, a.steps, a.warmup, dev)
+        return {"route": "prefix", "scaling": "weak", "ms_per_step": ms, "value": q_tot / (ms * 1e-3),
+                "unit": "queries/s", "workload": f"{a.q} targets x {a.n} ids per GPU ({q_tot} x {n_tot} over {world})",
+                "ids_rank": c.num_ids, "targets_rank": ql,
+                "note": "a different (N times larger) problem than the headline's; no data-path collective"}
     finally:
         c.close()
         torch.cuda.synchronize()

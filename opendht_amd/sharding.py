@@ -25,6 +25,12 @@ def shard_range(n, world, rank):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def _host_staged(group, *ts):
+    """gloo moves host tensors only: device tensors are staged through host copies (the
+    one-GPU multi-rank rehearsal); RCCL takes device tensors as they are"""
+    return dist.get_backend(group) == "gloo" and any(t.is_cuda for t in ts)
+
+
 def gather_records(rec, group=None, out=None):
     """All-gather this rank's (q, k, 6) int32 candidate records -> (world, q, k, 6).
     `out` may be a preallocated (world*q, k, 6) buffer (the concatenated form every
@@ -32,7 +38,12 @@ def gather_records(rec, group=None, out=None):
     world = dist.get_world_size(group)
     if out is None:
         out = torch.empty((world * rec.shape[0],) + tuple(rec.shape[1:]), dtype=rec.dtype, device=rec.device)
-    dist.all_gather_into_tensor(out, rec.contiguous(), group=group)
+    if _host_staged(group, rec, out):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(h, rec.contiguous().cpu(), group=group)
+        out.copy_(h)
+    else:
+        dist.all_gather_into_tensor(out, rec.contiguous(), group=group)
     return out.view((world,) + tuple(rec.shape))
 
 
@@ -46,8 +57,14 @@ def exchange_records(rec, group=None, out=None):
     mine = sizes[rank]
     if out is None:
         out = torch.empty((world * mine,) + tuple(rec.shape[1:]), dtype=rec.dtype, device=rec.device)
-    dist.all_to_all_single(out, rec.contiguous(), output_split_sizes=[mine] * world, input_split_sizes=sizes,
-                           group=group)
+    if _host_staged(group, rec, out):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(h, rec.contiguous().cpu(), output_split_sizes=[mine] * world,
+                               input_split_sizes=sizes, group=group)
+        out.copy_(h)
+    else:
+        dist.all_to_all_single(out, rec.contiguous(), output_split_sizes=[mine] * world, input_split_sizes=sizes,
+                               group=group)
     return out.view((world, mine) + tuple(rec.shape[1:]))
 
 

@@ -7,6 +7,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 import oracle as O
 
@@ -43,9 +44,37 @@ def test_gpus_n_launches_n_ranks():
 
 def test_inside_torchrun_no_relaunch():
     (me,) = _run(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1"})
+    me.pop("plan")
     assert me == {"mode": "rank", "gpus": 2, "world_size": 2, "rank": 1, "local_rank": 1}
     (one,) = _run(["--dry-run"])
     assert one["mode"] == "single" and one["world_size"] == 1
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_multi_gpu_default_is_the_metric_workload(world):
+    """N > 1 measures the metric's own workload by default -- the 2^24 cfg-2 ids and
+    65,536 targets in TOTAL, strong scaling, on the north-star broadcast route (range shards, K6
+    record mode, RCCL all-gather, K3) -- and N = 1 is the first point of the same series."""
+    (me,) = _run(["--gpus", str(world), "--dry-run"], {"WORLD_SIZE": str(world), "RANK": "0", "LOCAL_RANK": "0"})
+    assert me["plan"] == {"route": "broadcast", "scaling": "strong", "world": world, "n_total": 16777216,
+                          "q_total": 65536, "exchange": "allgather"}
+    (one,) = _run(["--dry-run"])
+    assert one["plan"] == {"route": "broadcast", "scaling": "strong", "world": 1, "n_total": 16777216,
+                           "q_total": 65536, "exchange": None}
+    # the prefix route stays available, labelled weak
+    (pw,) = _run(["--gpus", str(world), "--dry-run", "--route", "prefix"],
+                 {"WORLD_SIZE": str(world), "RANK": "0", "LOCAL_RANK": "0"})
+    assert pw["plan"]["route"] == "prefix" and pw["plan"]["scaling"] == "weak"
+    assert pw["plan"]["n_total"] == world * 16777216
+
+
+def test_rehearse_plan_two_ranks():
+    """the one-GPU rehearsal (--rehearse-one-gpu --gpus 2) runs the same default plan on each rank"""
+    lines = _run(["--gpus", "2", "--dry-run-ranks", "--rehearse-one-gpu"])
+    assert len(lines) == 2
+    for l in lines:
+        assert l["plan"]["route"] == "broadcast" and l["plan"]["n_total"] == 16777216
+        assert l["plan"]["scaling"] == "strong" and l["plan"]["world"] == 2
 
 
 def test_bench_tables_are_onnewnode_grown():
