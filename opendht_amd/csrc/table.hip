@@ -6,6 +6,8 @@
 #include "dhtgpu_dev.h"
 #include "dhtgpu_internal.h"
 
+#include <type_traits>
+
 namespace dhtgpu {
 namespace {
 
@@ -94,26 +96,87 @@ __global__ __launch_bounds__(256) void k_find_closest(
 }
 
 // ---------------------------------------------------------------------------------
-// K2.  HBM-streaming: each thread classifies 4 consecutive ids per step (5 x 16-B plane
-// loads, one 4-B bucket store), with the next step's 5 loads issued before this step's
-// work (two steps in flight per lane).  The grid is kClsPerCu = 32 workgroups per CU (four
-// rounds of the eight that are resident at once): shorter grid-stride ranges per workgroup
-// end together (measured, profiles/r03/experiments/k2_shapes.txt: 4 per CU 0.468 ms, 8 0.48,
-// 16 0.44, 32 0.42-0.43, 64 without the look-ahead 0.43 ms).  Bucket
-// firsts live in LDS; findBucket is a branch-light binary search.  commonBits is a clz
-// over the first nonzero xor word; the heavy low bins (cb < 8 hold 255/256 of uniform ids)
-// are counted with wave ballots, the rest with LDS atomics, then one global atomic per bin
-// per workgroup.
+// K2.  findBucket + commonBits of every id against one table snapshot, streaming word 0
+// only.  An id's bucket and its commonBits with myid follow from its word 0 alone unless
+// that word equals a bucket first's word 0 or myid's; only then are words 1..4 of the id
+// loaded (rare on hash-distributed ids).  Algorithmic bytes: 4 B/id read + the 1-B bucket
+// written (round 3 streamed all five planes: 21 B/id).
+//   cell table  built in LDS by every workgroup from the firsts: for each value of the top
+//               kClsT bits of word 0, the bucket of the cell's first key and commonBits with
+//               myid (both constant over the cell), or a flag sending the cell's ids to the
+//               exact path: a bucket boundary inside the cell (the binary search over the
+//               firsts' word 0, the full key on a word-0 tie -- the bucket the reference's
+//               linear walk, src/routing_table.cpp:153-166, stops at), or myid's own cell
+//               (commonBits >= kClsT: clz of the word-0 xor, infohash.h:154-176, all five
+//               words when word 0 equals myid's).  A routing table's firsts are prefix
+//               boundaries: on the cfg-4 table they all lie in myid's cell, 1 of 1,024.
+//   histogram   per-lane 4-bit counters of bins 0..kClsT-1 packed in one 64-bit word (one
+//               64-bit add per id; a flagged id adds to a discarded field), flushed into
+//               32-bit counts after every chunk (<= 4 kClsU ids per lane: no overflow); the
+//               exact path counts with LDS atomics; one global atomic per bin per workgroup.
+// Layout: a wave handles chunks of 64 x kClsU uint4 of word 0 (256 x kClsU ids), lane l the
+// uint4s chunk * 64 kClsU + u * 64 + l, so every load and every 4-B bucket store of a wave is
+// one contiguous 1-KB / 256-B run.  Every id's table read is issued before any is used, and
+// the next chunk's loads before this chunk's work (two chunks in flight per lane).
 // ---------------------------------------------------------------------------------
 constexpr int kClsBlock = 256;
 #ifndef DHT_K2_PERCU
-#define DHT_K2_PERCU 32
+#define DHT_K2_PERCU 8
+#endif
+#ifndef DHT_K2_U
+#define DHT_K2_U 3
+#endif
+#ifndef DHT_K2_NT
+#define DHT_K2_NT 1   // non-temporal word-0 loads: 0.125 -> 0.122 ms at cfg 4 (profiles/r04/k2_variants.txt)
 #endif
 #ifndef DHT_K2_AHEAD
 #define DHT_K2_AHEAD 1
 #endif
-constexpr int kClsPerCu = DHT_K2_PERCU;
-constexpr bool kClsAhead = DHT_K2_AHEAD != 0;   // the next step's loads issued before this step's work
+constexpr int kClsPerCu = DHT_K2_PERCU;          // workgroups per CU (one round: 8 x 4 waves fill a CU)
+constexpr uint32_t kClsU = DHT_K2_U;             // uint4 of word 0 per lane per chunk
+static_assert(4 * kClsU <= 15, "4-bit histogram fields flushed once per chunk");
+constexpr uint32_t kClsT = 10, kClsCells = 1u << kClsT;
+constexpr uint32_t kClsExact = 0x8000u;          // table flag: the cell's ids take the exact path
+constexpr uint32_t kClsSkip = 15u;               // histogram field an exact-path id adds to (discarded)
+
+// the reference's findBucket over the firsts in LDS (sf: plane-major, nb entries per plane):
+// the last bucket whose first <= id, bucket 0 when none (a linear walk from the front stops
+// at the same bucket); word 0 decides unless it ties
+__device__ __forceinline__ uint32_t cls_find_bucket(const uint32_t* sf, uint32_t nb, const uint32_t* id) {
+    uint32_t j = 0;
+    for (uint32_t step = 128; step; step >>= 1) {
+        const uint32_t c = j + step;
+        if (c < nb) {
+            const uint32_t f0 = sf[c];
+            bool le = f0 < id[0];
+            if (f0 == id[0]) {
+                uint32_t f[DHT_W];
+#pragma unroll
+                for (int w = 0; w < DHT_W; ++w) f[w] = sf[w * nb + c];
+                le = lex_le(f, id);
+            }
+            if (le) j = c;
+        }
+    }
+    return j;
+}
+
+// the exact path for id i (word 0 = x): {bucket, commonBits}.  Words 1..4 are loaded only when
+// word 0 cannot decide.  One out-of-line copy (inlined at every unrolled id it bloated the
+// loop's code ~10x).
+__device__ __noinline__ uint2 cls_exact(const uint32_t* __restrict__ planes, uint64_t stride, uint64_t i, uint32_t x,
+                                        const uint32_t* sf, uint32_t nb, uint32_t m0, uint32_t m1, uint32_t m2,
+                                        uint32_t m3, uint32_t m4) {
+    uint32_t id[DHT_W] = {x, 0u, 0u, 0u, 0u};
+    bool tie = x == m0;
+    for (uint32_t c = 0; c < nb && !tie; ++c) tie = sf[c] == x;
+    if (tie) {
+#pragma unroll
+        for (int w = 1; w < DHT_W; ++w) id[w] = planes[(uint64_t)w * stride + i];
+    }
+    const uint32_t my[DHT_W] = {m0, m1, m2, m3, m4};
+    return make_uint2(cls_find_bucket(sf, nb, id), tie ? common_bits(id, my) : (uint32_t)__clz(x ^ m0));
+}
 
 __global__ __launch_bounds__(kClsBlock) void k_classify(
     const uint32_t* __restrict__ planes, uint64_t stride, uint64_t n, uint32_t nb,
@@ -121,81 +184,136 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
     uint32_t m4, uint8_t* __restrict__ out_bucket, unsigned long long* __restrict__ hist) {
     __shared__ uint32_t sf[DHT_W * 256];
     __shared__ uint32_t sh[161];
+    __shared__ uint16_t lut[kClsCells];   // bucket | commonBits << 8 | kClsExact
+    constexpr uint32_t CH = 64 * kClsU;   // uint4 per wave chunk
+    constexpr uint32_t NE = 4 * kClsU;    // ids per lane per chunk
     const uint64_t n4 = (n + 3) / 4;
-    const uint64_t G = (uint64_t)gridDim.x * kClsBlock;
-    uint64_t g = (uint64_t)blockIdx.x * kClsBlock + threadIdx.x;
-    // the first step's loads ahead of the setup
-    uint4 v[DHT_W];
+    const uint64_t nch = (n4 + CH - 1) / CH;
+    const uint64_t nfull = n / (4 * CH);  // chunks with every id valid
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint64_t W = (uint64_t)gridDim.x * (kClsBlock / 64);
+    uint64_t c = (uint64_t)blockIdx.x * (kClsBlock / 64) + wv;
+    const uint4* __restrict__ w04 = reinterpret_cast<const uint4*>(planes);
+    // unconditional loads (an address past the set is clamped to its last uint4, whose ids are
+    // masked): a conditional load made the compiler wait for the look-ahead chunk too (vmcnt(0)
+    // at the branch join)
+    auto load = [&](uint64_t ch, uint4* v) {
 #pragma unroll
-    for (int w = 0; w < DHT_W; ++w)
-        v[w] = g < n4 ? reinterpret_cast<const uint4*>(planes + (uint64_t)w * stride)[g] : make_uint4(0u, 0u, 0u, 0u);
+        for (uint32_t u = 0; u < kClsU; ++u) {
+            uint64_t i4 = ch * CH + u * 64 + lane;
+            i4 = i4 < n4 ? i4 : n4 - 1;
+#if DHT_K2_NT
+            typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+            const u4v t = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(w04 + i4));
+            v[u] = make_uint4(t[0], t[1], t[2], t[3]);
+#else
+            v[u] = w04[i4];
+#endif
+        }
+    };
+    // the first chunk's loads ahead of the setup
+    uint4 v[kClsU];
+    load(c, v);
     for (uint32_t i = threadIdx.x; i < DHT_W * nb; i += kClsBlock) sf[i] = fp[i];
     for (uint32_t i = threadIdx.x; i < 161; i += kClsBlock) sh[i] = 0;
     __syncthreads();
-    const uint32_t my[DHT_W] = {m0, m1, m2, m3, m4};
-    const uint32_t lane = lane_id();
-    uint32_t low[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (; g - threadIdx.x < n4; g += G) {   // block-uniform: whole waves stay in the loop for the ballots
-        const bool active = g < n4;
-        const uint64_t gn = g + G;
-        uint4 nx[DHT_W];
-        if (kClsAhead) {
+    const uint32_t mycell = m0 >> (32 - kClsT);
+    for (uint32_t cell = threadIdx.x; cell < kClsCells; cell += kClsBlock) {
+        const uint32_t key[DHT_W] = {cell << (32 - kClsT), 0u, 0u, 0u, 0u};
+        const uint32_t j = cls_find_bucket(sf, nb, key);
+        // the smallest first above the cell's first key decides whether the bucket changes inside it
+        const bool inside = j + 1 < nb && (sf[j + 1] >> (32 - kClsT)) == cell;
+        const uint32_t cb = (uint32_t)__clz((cell ^ mycell) << (32 - kClsT));   // < kClsT off myid's cell
+        lut[cell] = (uint16_t)(inside || cell == mycell ? kClsExact | (kClsSkip << 8) : j | (cb << 8));
+    }
+    __syncthreads();
+    uint32_t low[kClsT];
 #pragma unroll
-            for (int w = 0; w < DHT_W; ++w)
-                nx[w] = gn < n4 ? reinterpret_cast<const uint4*>(planes + (uint64_t)w * stride)[gn] : make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t b = 0; b < kClsT; ++b) low[b] = 0;
+    // one chunk; FULL: every id of the chunk is < n (no per-id bounds test)
+    auto chunk = [&](auto full_c) {
+        constexpr bool FULL = decltype(full_c)::value;
+        uint32_t x[NE], ent[NE];
+#pragma unroll
+        for (uint32_t u = 0; u < kClsU; ++u) {
+            x[4 * u] = v[u].x;
+            x[4 * u + 1] = v[u].y;
+            x[4 * u + 2] = v[u].z;
+            x[4 * u + 3] = v[u].w;
         }
-        uint32_t packed = 0;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const uint64_t i = 4 * g + e;
-            const bool valid = active && i < n;
-            uint32_t id[DHT_W];
+        for (uint32_t e = 0; e < NE; ++e) ent[e] = lut[x[e] >> (32 - kClsT)];
+        unsigned long long pk = 0;   // 4-bit counts of bins 0..kClsT-1 (field kClsSkip: exact-path ids)
+        uint32_t packed[kClsU], exact = 0;
 #pragma unroll
-            for (int w = 0; w < DHT_W; ++w) id[w] = e == 0 ? v[w].x : e == 1 ? v[w].y : e == 2 ? v[w].z : v[w].w;
-            // findBucket by binary search on word 0 of the firsts; words 1..4 only when word 0
-            // ties (a first shares the id's top 32 bits: rare)
-            uint32_t j = 0;
-            for (uint32_t step = 128; step; step >>= 1) {
-                const uint32_t c = j + step;
-                if (c < nb) {
-                    const uint32_t f0 = sf[c];
-                    bool le = f0 < id[0];
-                    if (f0 == id[0]) {
-                        uint32_t f[DHT_W];
+        for (uint32_t u = 0; u < kClsU; ++u) {
+            packed[u] = 0;
 #pragma unroll
-                        for (int w = 0; w < DHT_W; ++w) f[w] = sf[w * nb + c];
-                        le = lex_le(f, id);
-                    }
-                    if (le) j = c;
+            for (uint32_t e = 0; e < 4; ++e) {
+                const uint32_t k = 4 * u + e, en = ent[k];
+                const bool valid = FULL || 4 * (c * CH + u * 64 + lane) + e < n;
+                packed[u] |= (en & 0xFFu) << (8 * e);
+                pk += (unsigned long long)valid << (4 * ((en >> 8) & 0xFu));
+                exact |= (uint32_t)(valid && en >= kClsExact) << k;
+            }
+        }
+        // the exact path: rare ids, one at a time per lane
+        while (exact) {
+            const uint32_t k = (uint32_t)__ffs(exact) - 1;
+            exact &= exact - 1;
+            const uint32_t u = k >> 2, e = k & 3u;
+            const uint64_t i = 4 * (c * CH + u * 64 + lane) + e;
+            uint32_t xk = 0;
+#pragma unroll
+            for (uint32_t kk = 0; kk < NE; ++kk) xk = kk == k ? x[kk] : xk;
+            const uint2 r = cls_exact(planes, stride, i, xk, sf, nb, m0, m1, m2, m3, m4);
+#pragma unroll
+            for (uint32_t uu = 0; uu < kClsU; ++uu)
+                if (uu == u) packed[uu] = (packed[uu] & ~(0xFFu << (8 * e))) | (r.x << (8 * e));
+            atomicAdd(&sh[r.y], 1u);
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kClsT; ++b) low[b] += (uint32_t)(pk >> (4 * b)) & 0xFu;
+        if (out_bucket) {
+#pragma unroll
+            for (uint32_t u = 0; u < kClsU; ++u) {
+                const uint64_t i4 = c * CH + u * 64 + lane;
+                if (FULL || 4 * i4 + 3 < n) {
+                    *reinterpret_cast<uint32_t*>(out_bucket + 4 * i4) = packed[u];
+                } else {
+                    for (uint32_t e = 0; e < 4; ++e)
+                        if (4 * i4 + e < n) out_bucket[4 * i4 + e] = (uint8_t)(packed[u] >> (8 * e));
                 }
             }
-            packed |= j << (8 * e);
-            const uint32_t cb = common_bits(id, my);
-#pragma unroll
-            for (uint32_t b = 0; b < 8; ++b) low[b] += (uint32_t)__popcll(__ballot(valid && cb == b));
-            if (valid && cb >= 8) atomicAdd(&sh[cb], 1u);
         }
-        if (active && out_bucket) {
-            if (4 * g + 3 < n) {
-                *reinterpret_cast<uint32_t*>(out_bucket + 4 * g) = packed;
-            } else {
-                for (int e = 0; e < 4; ++e)
-                    if (4 * g + e < n) out_bucket[4 * g + e] = (uint8_t)(packed >> (8 * e));
-            }
-        }
-        if (kClsAhead) {
+    };
+#if DHT_K2_AHEAD == 2
+    uint4 v2[kClsU];
+    load(c + W, v2);
+    for (; c < nch; c += W) {   // wave-uniform
+        uint4 nx[kClsU];
+        load(c + 2 * W, nx);
+        if (c < nfull) chunk(std::true_type{});
+        else chunk(std::false_type{});
 #pragma unroll
-            for (int w = 0; w < DHT_W; ++w) v[w] = nx[w];
-        } else {
-#pragma unroll
-            for (int w = 0; w < DHT_W; ++w)
-                v[w] = gn < n4 ? reinterpret_cast<const uint4*>(planes + (uint64_t)w * stride)[gn] : make_uint4(0u, 0u, 0u, 0u);
-        }
+        for (uint32_t u = 0; u < kClsU; ++u) { v[u] = v2[u]; v2[u] = nx[u]; }
     }
-    if (lane == 0) {
+#else
+    for (; c < nch; c += W) {   // wave-uniform
+        uint4 nx[kClsU];
+        load(c + W, nx);
+        if (c < nfull) chunk(std::true_type{});
+        else chunk(std::false_type{});
 #pragma unroll
-        for (uint32_t b = 0; b < 8; ++b)
-            if (low[b]) atomicAdd(&sh[b], low[b]);
+        for (uint32_t u = 0; u < kClsU; ++u) v[u] = nx[u];
+    }
+#endif
+#pragma unroll
+    for (uint32_t b = 0; b < kClsT; ++b) {
+        uint32_t s = low[b];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o);
+        if (lane == 0 && s) atomicAdd(&sh[b], s);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < 161; i += kClsBlock)
@@ -284,7 +402,8 @@ hipError_t launch_classify(const uint32_t* planes, uint64_t stride, uint64_t n, 
     const uint64_t n4 = (n + 3) / 4;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    uint64_t grid = (n4 + kClsBlock - 1) / kClsBlock;
+    const uint64_t nch = (n4 + 64 * kClsU - 1) / (64 * kClsU);   // wave chunks
+    uint64_t grid = (nch + kClsBlock / 64 - 1) / (kClsBlock / 64);
     const uint64_t full = (uint64_t)(cus > 0 ? cus : 256) * kClsPerCu;
     if (grid > full) grid = full;
     k_classify<<<(uint32_t)grid, kClsBlock, 0, s>>>(planes, stride, n, nb, fp, myid[0], myid[1],

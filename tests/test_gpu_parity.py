@@ -202,6 +202,35 @@ def test_classify_vs_oracle(ctx):
     assert np.array_equal(hist, wh)
 
 
+@pytest.mark.parametrize("n,nb,seed", [(1, 1, 1), (5, 3, 2), (100003, 200, 3), (262147, 256, 4), (4099, 17, 5)])
+def test_classify_word0_ties_and_flagged_cells(ctx, n, nb, seed):
+    """K2 streams word 0 and loads words 1..4 only where word 0 cannot decide: ids whose word 0
+    equals a bucket first's (findBucket's full-key tie) or myid's (commonBits past 32 bits), ids
+    in cells of the word-0 cell table that hold a bucket boundary (random firsts: most cells),
+    ids equal to a first, a ragged tail -- every bucket and the whole histogram equal the oracle."""
+    rng = np.random.default_rng(seed)
+    firsts = O.gen_ids(seed + 100, nb)
+    firsts[0] = 0                                     # bucket 0 starts at the all-zero hash
+    firsts = firsts[np.lexsort(firsts.T[::-1])]
+    firsts = np.unique(firsts, axis=0)
+    myid = O.gen_ids(seed + 200, 1)[0]
+    ids = O.gen_ids(seed + 300, n)
+    m = n // 8
+    if m:
+        pick = rng.integers(0, firsts.shape[0], size=m)
+        ids[:m, :4] = firsts[pick, :4]                # word-0 ties with firsts
+        ids[m:m + m // 2] = firsts[pick[: m // 2]]    # ids equal to a first
+        ids[2 * m:3 * m, :4] = myid[:4]               # word 0 of myid: commonBits >= 32
+        ids[3 * m:3 * m + 5] = myid                   # myid itself: 160
+        ids[4 * m:5 * m, :3] = myid[:3]               # deep bins 8..31
+    ctx.set_ids(ids)
+    b, hist = ctx.classify(firsts, myid)
+    wb, wh = O.classify(firsts, myid, ids)
+    assert np.array_equal(hist, wh)
+    bad = np.nonzero(b != wb)[0]
+    assert bad.size == 0, f"{bad.size} buckets differ, first {bad[:5]}"
+
+
 def test_cached_nodes_vs_oracle(ctx):
     ids = O.gen_ids(21, 50000)
     s = ids[np.lexsort(ids.T[::-1])]

@@ -1,7 +1,7 @@
 """K2 (findBucket + commonBits classification, cfg 4) driver for profiling: 10^8 splitmix ids
 in HBM, the bucket firsts of a table grown by onNewNode from 10^5 ids (bench.cfg4_firsts),
 --reps stream-ordered calls, then the mean event time of 10 calls and the HBM fraction
-(21 B/id algorithmic: 20 in + 1 out)."""
+(5 B/id algorithmic: word 0 in + the 1-B bucket out; SURVEY's contract counts 20 + 1)."""
 import argparse
 import ctypes
 import os
@@ -53,6 +53,6 @@ for _ in range(10):
 e1.record(st)
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / 10
-b = (20 + (0 if a.no_buckets else 1)) * a.n
+b = (4 + (0 if a.no_buckets else 1)) * a.n   # word 0 streamed + the 1-B bucket (K2 reads words 1..4 only on word-0 ties)
 print(f"K2 n={a.n} buckets={firsts.shape[0]}: {ms:.4f} ms  {b / ms / 1e6:.0f} GB/s  frac {b / ms / 1e6 / 8000:.3f}", flush=True)
 c.close()
