@@ -129,7 +129,7 @@ def run_plan(a, world):
     G = a.simulate_world if a.simulate_world else world
     n_total, q_total = (a.n * G, a.q * G) if scaling == "weak" else (a.n, a.q)
     return {"route": route, "scaling": scaling, "world": G, "n_total": n_total, "q_total": q_total,
-            "exchange": a.exchange if route == "broadcast" and world > 1 else None}
+            "exchange": a.exchange if route == "broadcast" and (world > 1 or a.sharded) else None}
 
 
 def launcher_cmd(gpus, argv):
@@ -398,6 +398,8 @@ def main():
     a.n_total, a.q_total = plan["n_total"], plan["q_total"]
     use_dist = world > 1 or a.sharded
     if use_dist:
+        # RCCL's version banner goes to stdout: keep rank 0's stdout the one JSON line
+        os.environ["NCCL_DEBUG"] = os.environ.get("DHT_BENCH_NCCL_DEBUG", "WARN")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", "0")

@@ -68,6 +68,11 @@ struct dhtgpu_ctx {
     int num_cus = 256;
     hipStream_t stream = nullptr;
     DevBuf planes;          // 5 * stride u32
+    // the set as 24-B records {w0..w4, 0} for record-mode calls (the multi-GPU broadcast route's
+    // candidate records: one 24-B read per candidate instead of five scattered plane reads); built
+    // on the first record-mode call, kept until the set changes
+    DevBuf aos;
+    bool aos_valid = false;
     uint64_t n = 0, stride = 0;
     bool sorted = false;
     DevBuf staging;         // host<->device byte staging
@@ -243,7 +248,7 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
         for (DevBuf* d : {&b.ws, &b.out_idx, &b.out_cnt, &b.sws}) d->release();
     c->invalidate_subs();
     if (c->fb_hint) (void)hipHostFree(c->fb_hint);
-    for (DevBuf* b : {&c->stamps, &c->w0s, &c->sview.planes, &c->sview.perm,
+    for (DevBuf* b : {&c->aos, &c->stamps, &c->w0s, &c->sview.planes, &c->sview.perm,
                       &c->cache.planes, &c->cache.perm, &c->cache_in, &c->sort_scratch, &c->cache_acc, &c->srch})
         b->release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -271,6 +276,20 @@ static int finish_ids(dhtgpu_ctx* c, uint64_t n) {
     return DHTGPU_OK;
 }
 
+// the record-mode gather source (nullptr: gather from the planes, e.g. when the copy cannot be
+// allocated)
+static const uint32_t* rec_aos(dhtgpu_ctx* c, hipStream_t s) {
+    if (!c->aos_valid) {
+        if (c->aos.ensure((size_t)(c->n ? c->n : 1) * 24) != hipSuccess) return nullptr;
+        // built once per set; synchronised, so that calls on other streams may read it at once
+        if (launch_pack_aos(c->planes.as<uint32_t>(), c->stride, c->n, c->aos.as<uint32_t>(), s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return nullptr;
+        c->aos_valid = true;
+    }
+    return c->aos.as<uint32_t>();
+}
+
 static int alloc_ids(dhtgpu_ctx* c, uint64_t n) {
     if (n >= 0xFFFFFFFFull) return DHTGPU_ERANGE;
     c->has_ids = false;
@@ -281,6 +300,7 @@ static int alloc_ids(dhtgpu_ctx* c, uint64_t n) {
     c->has_gidx = false;
     c->invalidate_subs();
     c->sview.valid = false;
+    c->aos_valid = false;
     c->stride = pad_ids(n ? n : 1);
     DHT_TRY(c->planes.ensure((size_t)c->stride * 5 * 4));
     return DHTGPU_OK;
@@ -437,7 +457,7 @@ int dhtgpu_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, 
     }
     if (out_rec)
         DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
-                                    out_rec, s));
+                                    out_rec, s, rec_aos(c, s)));
     else
         DHT_TRY(launch_map_idx(li, (uint64_t)q * k, gidx, idx_base, s));
     return DHTGPU_OK;
@@ -542,7 +562,7 @@ int dhtgpu_index_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
                                li, lc, s));
     if (out_rec)
         DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
-                                    out_rec, s));
+                                    out_rec, s, rec_aos(c, s)));
     else
         DHT_TRY(launch_map_idx(li, (uint64_t)q * k, gidx, idx_base, s));
     return DHTGPU_OK;
@@ -735,7 +755,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     if (r) return r;
     if (out_rec) {
         DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, c->out_map(),
-                                    out_rec, s));
+                                    out_rec, s, rec_aos(c, s)));
     } else if (!global && idx_base) {
         DHT_TRY(launch_map_idx(out_idx, (uint64_t)q * k, nullptr, idx_base, s));
     }
@@ -793,7 +813,8 @@ static int small_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     b.last = s;
     c->last_small = true;
     if (out_rec)
-        DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx, out_rec, s));
+        DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
+                                    out_rec, s, rec_aos(c, s)));
     return DHTGPU_OK;
 }
 
@@ -848,7 +869,7 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     if (r) return r;
     if (out_rec)
         DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
-                                    out_rec, s));
+                                    out_rec, s, rec_aos(c, s)));
     return DHTGPU_OK;
 }
 

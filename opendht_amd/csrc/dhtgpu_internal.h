@@ -73,9 +73,12 @@ hipError_t launch_merge(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_
 hipError_t launch_map_idx(uint32_t* idx, uint64_t m, const uint32_t* gidx, uint32_t base, hipStream_t s);
 // rec[i] = {words of id idx[i], global index} (DHT_NONE record for DHT_NONE); the global
 // index is gidx[idx[i]] when gidx != nullptr, else idx[i] + base
+// aos (nullable): the set as 24-B records (launch_pack_aos), one read per candidate
 hipError_t launch_rec_from_idx(const uint32_t* idx, uint64_t m, const uint32_t* planes,
                                uint64_t stride, uint32_t base, const uint32_t* gidx, uint32_t* rec,
-                               hipStream_t s);
+                               hipStream_t s, const uint32_t* aos = nullptr);
+// aos[i * 6 + w] = word w of id i (w < 5), aos[i * 6 + 5] = 0
+hipError_t launch_pack_aos(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t* aos, hipStream_t s);
 
 // table.hip
 hipError_t launch_find_closest(uint32_t nb, const uint32_t* fp, const uint32_t* off,

@@ -470,6 +470,64 @@ def test_batch_clustered_targets_and_fallback(ctx):
     check_topk(ctx, ids, tg[:100], 14)    # a different batch on the first set again
 
 
+def _shard_records(ids, bounds, tg, k):
+    """(lists, q, k, 6) records {w0..w4, global idx} of each id-range shard's exact top-k (the
+    oracle's, sorted ascending, NONE-padded like every producer in the library)"""
+    q = tg.shape[0]
+    words = ids.view(">u4").reshape(-1, 5).astype(np.uint32)
+    rec = np.full((len(bounds) - 1, q, k, 6), 0xFFFFFFFF, dtype=np.uint32)
+    for s in range(len(bounds) - 1):
+        lo, hi = bounds[s], bounds[s + 1]
+        if hi == lo:
+            continue
+        idx, cnt = O.topk(ids[lo:hi], tg, k)
+        for i in range(q):
+            c = int(cnt[i])
+            rec[s, i, :c, :5] = words[lo + idx[i, :c].astype(np.int64)]
+            rec[s, i, :c, 5] = idx[i, :c] + lo
+    return rec
+
+
+@pytest.mark.parametrize("lists,k,seed", [(1, 8, 1), (2, 8, 2), (3, 14, 3), (8, 8, 4), (8, 32, 5), (13, 1, 6),
+                                          (64, 8, 7), (65, 8, 8), (5, 32, 9)])
+def test_merge_heads_ties_duplicates(ctx, lists, k, seed):
+    """K3 (the k-way heads merge for <= 64 sorted lists, the pairwise rank past 64) over id-range
+    shards whose ids tie on their first 64 bits across shards (the heads' word-0 and word-1
+    distances tie: the five-word path), duplicated ids in different shards (global index
+    decides), shards shorter than k and empty shards == one flat top-k of all ids."""
+    import torch
+    import opendht_amd
+    rng = np.random.default_rng(seed)
+    n, q = 4000, 300
+    ids = O.gen_ids(600 + seed, n)
+    ids[: n // 3, :8] = ids[0, :8]                 # 64-bit prefix cluster, spread over the shards
+    ids[n // 2: n // 2 + 40] = ids[10:50]          # duplicates of cluster ids (other shards)
+    ids = ids[rng.permutation(n)]
+    tg = O.gen_ids(700 + seed, q)
+    tg[: q // 2, :8] = O.gen_ids(600 + seed, 1)[0, :8]   # targets inside the cluster's prefix
+    cuts = np.sort(rng.integers(0, n, size=lists - 1))
+    if lists > 2:
+        cuts[0] = cuts[1]                          # one empty shard
+    bounds = [0] + [int(c) for c in cuts] + [n]
+    rec = _shard_records(ids, bounds, tg, k)
+    dev = torch.device("cuda", 0)
+    ts = (q + 63) // 64 * 64
+    tp = torch.zeros(5 * ts, dtype=torch.int32, device=dev)
+    L = opendht_amd.lib()
+    assert L.dhtgpu_pack_dev(torch.from_numpy(tg.reshape(-1)).to(dev).data_ptr(), q, tp.data_ptr(), ts, None) == 0
+    rd = torch.from_numpy(rec.view(np.int32)).to(dev)
+    out = torch.empty((q, k), dtype=torch.int32, device=dev)
+    cnt = torch.empty(q, dtype=torch.int32, device=dev)
+    assert L.dhtgpu_merge_dev(rd.data_ptr(), lists, q, k, tp.data_ptr(), ts, k, out.data_ptr(), cnt.data_ptr(),
+                              None) == 0
+    torch.cuda.synchronize()
+    want, wcnt = O.topk(ids, tg, k)
+    got = out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(cnt.cpu().numpy().view(np.uint32), wcnt)
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} targets differ, first {bad[:3]}: {got[bad[0]]} vs {want[bad[0]]}"
+
+
 def test_batch_records_merge(ctx):
     """K6 record mode over 3 id shards + K3 merge == one flat top-k."""
     import torch
