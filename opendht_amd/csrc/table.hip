@@ -100,44 +100,50 @@ __global__ __launch_bounds__(256) void k_find_closest(
 // only.  An id's bucket and its commonBits with myid follow from its word 0 alone unless
 // that word equals a bucket first's word 0 or myid's; only then are words 1..4 of the id
 // loaded (rare on hash-distributed ids).  Algorithmic bytes: 4 B/id read + the 1-B bucket
-// written (round 3 streamed all five planes: 21 B/id).
-//   cell table  built in LDS by every workgroup from the firsts: for each value of the top
-//               kClsT bits of word 0, the bucket of the cell's first key and commonBits with
-//               myid (both constant over the cell), or a flag sending the cell's ids to the
-//               exact path: a bucket boundary inside the cell (the binary search over the
-//               firsts' word 0, the full key on a word-0 tie -- the bucket the reference's
-//               linear walk, src/routing_table.cpp:153-166, stops at), or myid's own cell
-//               (commonBits >= kClsT: clz of the word-0 xor, infohash.h:154-176, all five
-//               words when word 0 equals myid's).  A routing table's firsts are prefix
-//               boundaries: on the cfg-4 table they all lie in myid's cell, 1 of 1,024.
-//   histogram   per-lane 4-bit counters of bins 0..kClsT-1 packed in one 64-bit word (one
-//               64-bit add per id; a flagged id adds to a discarded field), flushed into
-//               32-bit counts after every chunk (<= 4 kClsU ids per lane: no overflow); the
-//               exact path counts with LDS atomics; one global atomic per bin per workgroup.
+// written (round 3 streamed all five planes: 21 B/id).  Two ways to the bucket, chosen per
+// workgroup from the firsts (block-uniform):
+//   register path  (routing tables) the ids with commonBits c < kRegT form one key range per c
+//               (myid's top c bits, bit c flipped); when no first lies inside such a range --
+//               a first with commonBits c < kRegT sits at its range's start (the reference's
+//               splits along myid's prefix, src/routing_table.cpp RoutingTable::split, put them
+//               there) -- the bucket is a function of c alone: 15 bytes in four registers,
+//               looked up four ids at a time with v_perm.  f = clz((w0 ^ myid w0) | 2^16)
+//               gives c and the histogram field in two instructions; f = kRegT (commonBits
+//               >= 15, one id in 32,768 on hashes) takes the exact path.  No table read: the
+//               cell table's random LDS reads (bank conflicts) were ~0.035 of its 0.12 ms.
+//   cell table  (any other sorted firsts) built in LDS by every workgroup: for each value of
+//               the top kClsT bits of word 0, the bucket of the cell's first key and
+//               commonBits with myid (both constant over the cell), or a flag sending the
+//               cell's ids to the exact path: a bucket boundary inside the cell (the binary
+//               search over the firsts' word 0, the full key on a word-0 tie -- the bucket the
+//               reference's linear walk, src/routing_table.cpp:153-166, stops at), or myid's
+//               own cell (commonBits >= kClsT: clz of the word-0 xor, infohash.h:154-176, all
+//               five words when word 0 equals myid's).
+//   histogram   per-lane 4-bit counters of bins 0..14 packed in one 64-bit word (one 64-bit
+//               add per id; an exact-path id adds to field 15, discarded), spread into byte
+//               counters (two 64-bit words) after every chunk (<= 4 kClsU ids per lane: no
+//               overflow) and wave-reduced into the block's LDS bins every kClsFlush chunks;
+//               the exact path counts with LDS atomics; one global atomic per bin per workgroup.
 // Layout: a wave handles chunks of 64 x kClsU uint4 of word 0 (256 x kClsU ids), lane l the
 // uint4s chunk * 64 kClsU + u * 64 + l, so every load and every 4-B bucket store of a wave is
-// one contiguous 1-KB / 256-B run.  Every id's table read is issued before any is used, and
-// the next chunk's loads before this chunk's work (two chunks in flight per lane).
+// one contiguous 1-KB / 256-B run; the chunk index is wave-uniform (scalar address math).  The
+// next chunk's loads are issued before this chunk's work (two chunks in flight per lane).
 // ---------------------------------------------------------------------------------
 constexpr int kClsBlock = 256;
 #ifndef DHT_K2_PERCU
-#define DHT_K2_PERCU 8
+#define DHT_K2_PERCU 4
 #endif
 #ifndef DHT_K2_U
 #define DHT_K2_U 3
 #endif
-#ifndef DHT_K2_NT
-#define DHT_K2_NT 1   // non-temporal word-0 loads: 0.125 -> 0.122 ms at cfg 4 (profiles/r04/k2_variants.txt)
-#endif
-#ifndef DHT_K2_AHEAD
-#define DHT_K2_AHEAD 1
-#endif
-constexpr int kClsPerCu = DHT_K2_PERCU;          // workgroups per CU (one round: 8 x 4 waves fill a CU)
+constexpr int kClsPerCu = DHT_K2_PERCU;          // workgroups per CU (4: 0.105 -> 0.096 ms against 8; 117 VGPRs = 4 waves per SIMD, a lower VGPR cap spills)
 constexpr uint32_t kClsU = DHT_K2_U;             // uint4 of word 0 per lane per chunk
 static_assert(4 * kClsU <= 15, "4-bit histogram fields flushed once per chunk");
 constexpr uint32_t kClsT = 10, kClsCells = 1u << kClsT;
 constexpr uint32_t kClsExact = 0x8000u;          // table flag: the cell's ids take the exact path
 constexpr uint32_t kClsSkip = 15u;               // histogram field an exact-path id adds to (discarded)
+constexpr uint32_t kRegT = 15u;                  // register path: commonBits below this from word 0
+constexpr uint32_t kClsFlush = 255u / (4 * kClsU);   // chunks per byte-counter flush
 
 // the reference's findBucket over the firsts in LDS (sf: plane-major, nb entries per plane):
 // the last bucket whose first <= id, bucket 0 when none (a linear walk from the front stops
@@ -185,30 +191,31 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
     __shared__ uint32_t sf[DHT_W * 256];
     __shared__ uint32_t sh[161];
     __shared__ uint16_t lut[kClsCells];   // bucket | commonBits << 8 | kClsExact
+    __shared__ uint32_t s_bad;            // a first inside a commonBits range: no register path
+    __shared__ uint32_t s_map[4];         // register path: bucket of commonBits c in byte c
     constexpr uint32_t CH = 64 * kClsU;   // uint4 per wave chunk
     constexpr uint32_t NE = 4 * kClsU;    // ids per lane per chunk
     const uint64_t n4 = (n + 3) / 4;
     const uint64_t nch = (n4 + CH - 1) / CH;
     const uint64_t nfull = n / (4 * CH);  // chunks with every id valid
-    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t lane = lane_id();
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t W = (uint64_t)gridDim.x * (kClsBlock / 64);
     uint64_t c = (uint64_t)blockIdx.x * (kClsBlock / 64) + wv;
     const uint4* __restrict__ w04 = reinterpret_cast<const uint4*>(planes);
     // unconditional loads (an address past the set is clamped to its last uint4, whose ids are
     // masked): a conditional load made the compiler wait for the look-ahead chunk too (vmcnt(0)
     // at the branch join)
+    // (32-bit index math: the host keeps n < 2^33, so every uint4 index, look-ahead included, < 2^32)
+    const uint32_t last4 = (uint32_t)(n4 - 1);
     auto load = [&](uint64_t ch, uint4* v) {
+        const uint32_t cb = (uint32_t)(ch * CH) + lane;
 #pragma unroll
         for (uint32_t u = 0; u < kClsU; ++u) {
-            uint64_t i4 = ch * CH + u * 64 + lane;
-            i4 = i4 < n4 ? i4 : n4 - 1;
-#if DHT_K2_NT
+            const uint32_t i4 = min(cb + u * 64, last4);
             typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-            const u4v t = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(w04 + i4));
+            const u4v t = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(w04) + i4);
             v[u] = make_uint4(t[0], t[1], t[2], t[3]);
-#else
-            v[u] = w04[i4];
-#endif
         }
     };
     // the first chunk's loads ahead of the setup
@@ -216,24 +223,59 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
     load(c, v);
     for (uint32_t i = threadIdx.x; i < DHT_W * nb; i += kClsBlock) sf[i] = fp[i];
     for (uint32_t i = threadIdx.x; i < 161; i += kClsBlock) sh[i] = 0;
+    if (threadIdx.x < 4) s_map[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) s_bad = 0u;
     __syncthreads();
-    const uint32_t mycell = m0 >> (32 - kClsT);
-    for (uint32_t cell = threadIdx.x; cell < kClsCells; cell += kClsBlock) {
-        const uint32_t key[DHT_W] = {cell << (32 - kClsT), 0u, 0u, 0u, 0u};
-        const uint32_t j = cls_find_bucket(sf, nb, key);
-        // the smallest first above the cell's first key decides whether the bucket changes inside it
-        const bool inside = j + 1 < nb && (sf[j + 1] >> (32 - kClsT)) == cell;
-        const uint32_t cb = (uint32_t)__clz((cell ^ mycell) << (32 - kClsT));   // < kClsT off myid's cell
-        lut[cell] = (uint16_t)(inside || cell == mycell ? kClsExact | (kClsSkip << 8) : j | (cb << 8));
+    // register path test: every first with commonBits c < kRegT starts its range (the bits
+    // below the flipped one, and words 1..4, zero)
+    for (uint32_t j = threadIdx.x; j < nb; j += kClsBlock) {
+        const uint32_t f0 = sf[j], cb = (uint32_t)__clz((f0 ^ m0) | (1u << (31 - kRegT)));
+        if (cb < kRegT) {
+            bool start = (f0 & ((0x80000000u >> cb) - 1u)) == 0u;
+#pragma unroll
+            for (int w = 1; w < DHT_W; ++w) start = start && sf[w * nb + j] == 0u;
+            if (!start) s_bad = 1u;
+        }
+    }
+    if (threadIdx.x < kRegT) {   // the bucket of each commonBits range's first key
+        const uint32_t b = 0x80000000u >> threadIdx.x;
+        const uint32_t key[DHT_W] = {(m0 ^ b) & ~(b - 1u), 0u, 0u, 0u, 0u};
+        atomicOr(&s_map[threadIdx.x >> 2], cls_find_bucket(sf, nb, key) << (8 * (threadIdx.x & 3u)));
     }
     __syncthreads();
-    uint32_t low[kClsT];
+    const bool regs = s_bad == 0u;   // block-uniform
+    const uint32_t ma = s_map[0], mb = s_map[1], mc = s_map[2], md = s_map[3];
+    if (!regs) {
+        const uint32_t mycell = m0 >> (32 - kClsT);
+        for (uint32_t cell = threadIdx.x; cell < kClsCells; cell += kClsBlock) {
+            const uint32_t key[DHT_W] = {cell << (32 - kClsT), 0u, 0u, 0u, 0u};
+            const uint32_t j = cls_find_bucket(sf, nb, key);
+            // the smallest first above the cell's first key decides whether the bucket changes inside it
+            const bool inside = j + 1 < nb && (sf[j + 1] >> (32 - kClsT)) == cell;
+            const uint32_t cb = (uint32_t)__clz((cell ^ mycell) << (32 - kClsT));   // < kClsT off myid's cell
+            lut[cell] = (uint16_t)(inside || cell == mycell ? kClsExact | (kClsSkip << 8) : j | (cb << 8));
+        }
+        __syncthreads();
+    }
+    // per-lane bin counts in bytes: acc_e bins 0, 2, .., 14, acc_o bins 1, 3, .., 15 (<= 12 per
+    // chunk: flushed to the block's LDS bins every kClsFlush chunks, before a byte can wrap)
+    unsigned long long acc_e = 0, acc_o = 0;
+    uint32_t nacc = 0;
+    auto flush_acc = [&]() {   // wave-uniform
 #pragma unroll
-    for (uint32_t b = 0; b < kClsT; ++b) low[b] = 0;
-    // one chunk; FULL: every id of the chunk is < n (no per-id bounds test)
-    auto chunk = [&](auto full_c) {
-        constexpr bool FULL = decltype(full_c)::value;
-        uint32_t x[NE], ent[NE];
+        for (uint32_t b = 0; b < kRegT; ++b) {
+            uint32_t x = (uint32_t)(((b & 1u) ? acc_o : acc_e) >> (8 * (b >> 1))) & 0xFFu;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o);
+            if (lane == 0 && x) atomicAdd(&sh[b], x);
+        }
+        acc_e = acc_o = 0;
+        nacc = 0;
+    };
+    // one chunk; FULL: every id of the chunk is < n (no per-id bounds test); REGS: the register path
+    auto chunk = [&](auto full_c, auto regs_c) {
+        constexpr bool FULL = decltype(full_c)::value, REGS = decltype(regs_c)::value;
+        uint32_t x[NE];
 #pragma unroll
         for (uint32_t u = 0; u < kClsU; ++u) {
             x[4 * u] = v[u].x;
@@ -241,20 +283,48 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
             x[4 * u + 2] = v[u].z;
             x[4 * u + 3] = v[u].w;
         }
-#pragma unroll
-        for (uint32_t e = 0; e < NE; ++e) ent[e] = lut[x[e] >> (32 - kClsT)];
-        unsigned long long pk = 0;   // 4-bit counts of bins 0..kClsT-1 (field kClsSkip: exact-path ids)
+        unsigned long long pk = 0;   // 4-bit counts of bins 0..14 (field kClsSkip: exact-path ids)
         uint32_t packed[kClsU], exact = 0;
+        if constexpr (REGS) {
+            uint32_t fk[NE];
 #pragma unroll
-        for (uint32_t u = 0; u < kClsU; ++u) {
-            packed[u] = 0;
+            for (uint32_t u = 0; u < kClsU; ++u) {
+                uint32_t* f = fk + 4 * u;
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) {
-                const uint32_t k = 4 * u + e, en = ent[k];
-                const bool valid = FULL || 4 * (c * CH + u * 64 + lane) + e < n;
-                packed[u] |= (en & 0xFFu) << (8 * e);
-                pk += (unsigned long long)valid << (4 * ((en >> 8) & 0xFu));
-                exact |= (uint32_t)(valid && en >= kClsExact) << k;
+                for (uint32_t e = 0; e < 4; ++e) f[e] = (uint32_t)__clz((x[4 * u + e] ^ m0) | (1u << (31 - kRegT)));
+                // four byte lookups at once: v_perm over {mb:ma} (c = 0..7) and {md:mc} (8..15)
+                const uint32_t sel = f[0] | f[1] << 8 | f[2] << 16 | f[3] << 24, s7 = sel & 0x07070707u;
+                const uint32_t lo = __builtin_amdgcn_perm(mb, ma, s7), hi = __builtin_amdgcn_perm(md, mc, s7);
+                const uint32_t m = ((sel >> 3) & 0x01010101u) * 0xFFu;
+                packed[u] = (hi & m) | (lo & ~m);
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) {
+                    const bool valid = FULL || 4 * (c * CH + u * 64 + lane) + e < n;
+                    pk += (unsigned long long)valid << (4 * f[e]);
+                }
+            }
+            if (pk >> (4 * kClsSkip)) {   // field 15: this lane holds an id with commonBits >= 15
+#pragma unroll
+                for (uint32_t k = 0; k < NE; ++k) {
+                    const bool valid = FULL || 4 * (c * CH + (k >> 2) * 64 + lane) + (k & 3u) < n;
+                    exact |= (uint32_t)(valid && fk[k] == kRegT) << k;
+                }
+            }
+        } else {
+            uint32_t ent[NE];
+#pragma unroll
+            for (uint32_t e = 0; e < NE; ++e) ent[e] = lut[x[e] >> (32 - kClsT)];
+#pragma unroll
+            for (uint32_t u = 0; u < kClsU; ++u) {
+                packed[u] = 0;
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) {
+                    const uint32_t k = 4 * u + e, en = ent[k];
+                    const bool valid = FULL || 4 * (c * CH + u * 64 + lane) + e < n;
+                    packed[u] |= (en & 0xFFu) << (8 * e);
+                    pk += (unsigned long long)valid << (4 * ((en >> 8) & 0xFu));
+                    exact |= (uint32_t)(valid && en >= kClsExact) << k;
+                }
             }
         }
         // the exact path: rare ids, one at a time per lane
@@ -272,8 +342,9 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
                 if (uu == u) packed[uu] = (packed[uu] & ~(0xFFu << (8 * e))) | (r.x << (8 * e));
             atomicAdd(&sh[r.y], 1u);
         }
-#pragma unroll
-        for (uint32_t b = 0; b < kClsT; ++b) low[b] += (uint32_t)(pk >> (4 * b)) & 0xFu;
+        acc_e += pk & 0x0F0F0F0F0F0F0F0Full;
+        acc_o += (pk >> 4) & 0x0F0F0F0F0F0F0F0Full;
+        if (++nacc == kClsFlush) flush_acc();
         if (out_bucket) {
 #pragma unroll
             for (uint32_t u = 0; u < kClsU; ++u) {
@@ -287,34 +358,19 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
             }
         }
     };
-#if DHT_K2_AHEAD == 2
-    uint4 v2[kClsU];
-    load(c + W, v2);
-    for (; c < nch; c += W) {   // wave-uniform
-        uint4 nx[kClsU];
-        load(c + 2 * W, nx);
-        if (c < nfull) chunk(std::true_type{});
-        else chunk(std::false_type{});
+    auto stream = [&](auto regs_c) {
+        for (; c < nch; c += W) {   // wave-uniform
+            uint4 nx[kClsU];
+            load(c + W, nx);
+            if (c < nfull) chunk(std::true_type{}, regs_c);
+            else chunk(std::false_type{}, regs_c);
 #pragma unroll
-        for (uint32_t u = 0; u < kClsU; ++u) { v[u] = v2[u]; v2[u] = nx[u]; }
-    }
-#else
-    for (; c < nch; c += W) {   // wave-uniform
-        uint4 nx[kClsU];
-        load(c + W, nx);
-        if (c < nfull) chunk(std::true_type{});
-        else chunk(std::false_type{});
-#pragma unroll
-        for (uint32_t u = 0; u < kClsU; ++u) v[u] = nx[u];
-    }
-#endif
-#pragma unroll
-    for (uint32_t b = 0; b < kClsT; ++b) {
-        uint32_t s = low[b];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o);
-        if (lane == 0 && s) atomicAdd(&sh[b], s);
-    }
+            for (uint32_t u = 0; u < kClsU; ++u) v[u] = nx[u];
+        }
+    };
+    if (regs) stream(std::true_type{});
+    else stream(std::false_type{});
+    flush_acc();
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < 161; i += kClsBlock)
         if (sh[i]) atomicAdd(hist + i, (unsigned long long)sh[i]);
@@ -399,6 +455,7 @@ hipError_t launch_classify(const uint32_t* planes, uint64_t stride, uint64_t n, 
                            const uint32_t* fp, const uint32_t* myid, uint8_t* out_bucket,
                            unsigned long long* hist, hipStream_t s) {
     if (!n) return hipSuccess;
+    if (n >= (1ull << 33)) return hipErrorInvalidValue;   // k_classify's 32-bit uint4 indices (look-ahead included)
     const uint64_t n4 = (n + 3) / 4;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

@@ -231,6 +231,48 @@ def test_classify_word0_ties_and_flagged_cells(ctx, n, nb, seed):
     assert bad.size == 0, f"{bad.size} buckets differ, first {bad[:5]}"
 
 
+@pytest.mark.parametrize("shape", ["grown", "grown_deep", "one_bucket", "my_cell_0", "my_cell_last",
+                                   "far_split", "far_split_mid_cell"])
+def test_classify_register_path_shapes(ctx, shape):
+    """K2's register path (bucket and bin from clz(word 0 ^ myid's word 0), no table read) is taken
+    only when every cell but myid's maps to the bucket of its commonBits: routing tables grown by
+    the reference's rule (onNewNode splits myid's bucket), a one-bucket table, myid in the first /
+    last cell. A far bucket split (a boundary off myid's prefix, at a cell edge or inside a cell)
+    must send the workgroups to the cell-table path. Every shape: buckets and histogram = oracle."""
+    rng = np.random.default_rng(sum(map(ord, shape)))
+    myid = O.gen_ids(11, 1)[0]
+    if shape == "my_cell_0":
+        myid[:4] = 0
+    elif shape == "my_cell_last":
+        myid[:4] = 0xFF
+    if shape == "one_bucket":
+        firsts = np.zeros((1, 20), np.uint8)
+    else:
+        grow = 200000 if shape == "grown_deep" else 20000
+        firsts, _, _ = O.Table(myid).grow(O.gen_ids(12, grow)).export()
+    if shape.startswith("far_split"):
+        far = firsts[1].copy() if firsts.shape[0] > 1 else np.zeros(20, np.uint8)
+        far[:] = 0
+        far[0] = (~myid[0]) & 0x80 | 0x20               # off myid's first bit: a far bucket
+        if shape == "far_split_mid_cell":
+            far[1] = 0x11                                # inside its 10-bit cell
+        firsts = np.concatenate([firsts, far[None, :]])
+        firsts = np.unique(firsts[np.lexsort(firsts.T[::-1])], axis=0)
+    ids = O.gen_ids(13, 65539)
+    m = 4096
+    ids[:m, :2] = myid[:2]                               # myid's cell and deep bins
+    ids[m:2 * m, 0] = myid[0] ^ (1 << rng.integers(0, 8, m)).astype(np.uint8)   # every bin 0..7
+    ids[2 * m:2 * m + 64] = myid
+    pick = rng.integers(0, firsts.shape[0], 64)
+    ids[3 * m:3 * m + 64] = firsts[pick]                 # ids equal to a first
+    ctx.set_ids(ids)
+    b, hist = ctx.classify(firsts, myid)
+    wb, wh = O.classify(firsts, myid, ids)
+    assert np.array_equal(hist, wh)
+    bad = np.nonzero(b != wb)[0]
+    assert bad.size == 0, f"{bad.size} buckets differ, first {bad[:5]}"
+
+
 def test_cached_nodes_vs_oracle(ctx):
     ids = O.gen_ids(21, 50000)
     s = ids[np.lexsort(ids.T[::-1])]
