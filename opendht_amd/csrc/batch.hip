@@ -49,13 +49,6 @@ namespace dhtgpu {
 namespace {
 
 constexpr int kF1Threads = 256;                      // one thread per target
-#ifndef DHT_F1_OWNER
-#define DHT_F1_OWNER 0
-#endif
-#ifndef DHT_F1_OWNERS
-#define DHT_F1_OWNERS 16
-#endif
-constexpr uint32_t kF1Owners = DHT_F1_OWNERS;        // owner-form F1: owner workgroups per sub-partition
 constexpr int kF3Threads = 256;
 constexpr uint32_t kF3Cap = 4096;                    // survivors per partition staged in LDS
 constexpr uint32_t kF3Per = kF3Cap / kF3Threads;
@@ -219,70 +212,6 @@ __global__ __launch_bounds__(kF1Threads) void k_f1_targets(F1Args a) {
     if (lane == (uint32_t)__ffsll((long long)sp) - 1) base = atomicAdd(a.ctr + kSpill, (uint32_t)__popcll(sp));
     base = __shfl((int)base, __ffsll((long long)sp) - 1);
     a.tspill[base + (uint32_t)__popcll(sp & ((1ull << lane) - 1ull))] = i;
-}
-
-// ---- F1, owner form: no global atomics ------------------------------------------------------
-// Owner workgroup (sub, o) of nown per sub-partition owns the prefix range [o, o + 1) * 2^Lm /
-// nown of that sub-partition: bitmap words [o * wpo, (o + 1) * wpo) and partitions [o * ppo,
-// (o + 1) * ppo).  It reads every target's word 0 (word 1 too for shifted sets) -- q x 4 B from
-// L2, a range test per target -- marks its own targets' prefixes in an LDS copy of its bitmap
-// words and counts them per partition with LDS atomics, appends them to their partition
-// buckets, then stores its whole bitmap share and its partitions' counts with plain coalesced
-// stores (so nothing needs clearing between calls).  The memory-side atomics of k_f1_targets
-// (a returning slot add per target, then the store) and their 8x write traffic go away.
-constexpr uint32_t kF1OwnThreads = 1024;
-constexpr uint32_t kF1OwnU = 4;   // 16-B target loads per lane in flight
-__global__ __launch_bounds__(kF1OwnThreads) void k_f1_owner(F1Args a, uint32_t nown, uint32_t vec) {
-    extern __shared__ uint32_t shf[];
-    const uint32_t wpo = a.nwords / nown, ppo = a.np / nown;
-    uint32_t* bm = shf;          // [wpo]
-    uint32_t* cnt = shf + wpo;   // [ppo]
-    const uint32_t sub = blockIdx.x / nown, o = blockIdx.x - sub * nown;
-    if (blockIdx.x == 0 && threadIdx.x < 4) a.ctr[threadIdx.x] = 0;   // fallback, survivors, wave path, -
-    for (uint32_t i = threadIdx.x; i < wpo; i += kF1OwnThreads) bm[i] = 0;
-    for (uint32_t i = threadIdx.x; i < ppo; i += kF1OwnThreads) cnt[i] = 0;
-    __syncthreads();
-    const uint32_t p0 = o * ppo, w0base = o * wpo;
-    auto one = [&](uint32_t i, uint32_t w, uint32_t w1) {
-        const uint32_t st = a.sub_bits ? (w << a.sub_shift) >> (32 - a.sub_bits) : 0u;
-        const uint32_t v = a.shift ? (w << a.shift) | (w1 >> (32 - a.shift)) : w;
-        const uint32_t p = top_bits(v, a.b1);
-        if (i >= a.q || st != sub || p - p0 >= ppo) return;   // not this owner's (most targets)
-        const uint32_t pre = top_bits(v, a.Lm);
-        atomicOr(bm + (pre >> 5) - w0base, 1u << (pre & 31));
-        const uint32_t slot = atomicAdd(cnt + (p - p0), 1u);
-        const uint32_t gp = sub * a.np + p;
-        if (slot < a.tcap) a.tbuf[(uint64_t)gp * a.tcap + slot] = make_uint2(v, i);
-        else a.tspill[atomicAdd(a.ctr + kSpill, 1u)] = i;   // a full bucket (rare): F3 lists it for F4
-    };
-    if (vec) {   // 16-B loads, kF1OwnU per lane in flight (clamped past the last target, masked by i < q)
-        const uint32_t q4 = (a.q + 3) / 4;
-        const uint4* t0 = reinterpret_cast<const uint4*>(a.tw0);
-        const uint4* t1 = reinterpret_cast<const uint4*>(a.tw1);
-        for (uint32_t b = 0; b < q4; b += kF1OwnThreads * kF1OwnU) {
-            uint4 x[kF1OwnU], y[kF1OwnU];
-#pragma unroll
-            for (uint32_t u = 0; u < kF1OwnU; ++u) {
-                const uint32_t j = min(b + u * kF1OwnThreads + threadIdx.x, q4 - 1);
-                x[u] = t0[j];
-                y[u] = a.shift ? t1[j] : make_uint4(0u, 0u, 0u, 0u);
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < kF1OwnU; ++u) {
-                const uint32_t i = 4 * (b + u * kF1OwnThreads + threadIdx.x);
-                one(i, x[u].x, y[u].x);
-                one(i + 1, x[u].y, y[u].y);
-                one(i + 2, x[u].z, y[u].z);
-                one(i + 3, x[u].w, y[u].w);
-            }
-        }
-    } else {
-        for (uint32_t i = threadIdx.x; i < a.q; i += kF1OwnThreads) one(i, a.tw0[i], a.shift ? a.tw1[i] : 0u);
-    }
-    __syncthreads();
-    uint32_t* bdst = a.bitmap + sub * a.nwords + w0base;
-    for (uint32_t i = threadIdx.x; i < wpo; i += kF1OwnThreads) bdst[i] = bm[i];
-    for (uint32_t i = threadIdx.x; i < ppo; i += kF1OwnThreads) a.tcount[(sub * a.np + p0 + i) * kCtrStride] = cnt[i];
 }
 
 // ---- F2: stream w0, keep ids in marked subtrees, partition them ----------------------
@@ -1883,17 +1812,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)2 * 8192 * 16 * 8, s);
     const F1Args a1{c.tp, c.tp + c.ts, q, P.Lm, P.b1, c.skip, c.sub_shift, c.nsub ? c.sub_bits : 0u, np, P.nwords,
                     bitmap, tcount, tbuf, P.tcap, ctr, tspill};
-    // owners per sub-partition: kF1Owners, more where an owner's bitmap share would pass 32 KB of
-    // LDS; the atomic form where no power-of-two split fits (np or nwords too small)
-    uint32_t nown = std::max<uint32_t>(1u, std::min<uint32_t>({np, P.nwords, kF1Owners}));
-    while (nown < np && nown < P.nwords && (P.nwords / nown + np / nown) * 4 > 32768) nown *= 2;
-    if (DHT_F1_OWNER && (P.nwords / nown + np / nown) * 4 <= 32768) {
-        const uint32_t vec = (((uintptr_t)c.tp | (uintptr_t)(c.tp + c.ts)) & 15u) == 0 ? 1u : 0u;
-        const size_t l1 = (size_t)(P.nwords / nown + np / nown) * 4;
-        go(0, k_f1_owner, dim3(nsub * nown), dim3(kF1OwnThreads), l1, a1, nown, vec);
-    } else {
-        go(0, k_f1_targets, dim3((q + kF1Threads - 1) / kF1Threads), dim3(kF1Threads), 0, a1);
-    }
+    go(0, k_f1_targets, dim3((q + kF1Threads - 1) / kF1Threads), dim3(kF1Threads), 0, a1);
     if (nblk2) {
         F2Args a2{d_desc, d_blk, hd[0], nsub, NP, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, P.scap, ctr,
                   narrow ? P.nstage : P.stage, dbg, P.sparse, seg, stamps ? stamps + 8192 * 16 : nullptr};
