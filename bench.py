@@ -24,7 +24,8 @@ Multi-GPU (one process per GPU, torch.distributed over RCCL; --route):
              q / N targets), K3 merge.  value = the 65,536 targets / the slowest rank's step.
              Consecutive steps rotate over --inflight streams, so one step's exchange overlaps
              the next step's K6.  The other exchange and the prefix route are measured beside
-             it (extra: broadcast_<exchange>, prefix_weak), each labelled.
+             it (extra: broadcast_<exchange>, prefix_strong -- the same problem on the prefix
+             route -- and prefix_weak), each labelled.
   prefix     ids AND targets are partitioned by their top log2(N) bits; each rank answers only
              its own targets from its own shard.  If every shard holds >= k ids, a target's
              top-k provably lies in its own prefix subtree, so the data path needs no
@@ -683,8 +684,8 @@ def main():
             except Exception as e:  # noqa: BLE001 -- an extra leg must not cost the headline
                 extra[name] = {"error": repr(e)}
     if world > 1 and not a.no_extra and a.algo == "batch" and route == "broadcast" and not a.simulate_world:
-        # the same cfg-2 problem with the other exchange, and the prefix route (weak scaling),
-        # each labelled; measured after the headline, on fresh contexts
+        # the same cfg-2 problem with the other exchange and on the prefix route (strong), and the
+        # prefix route with weak scaling, each labelled; measured after the headline, on fresh contexts
         progress("N > 1 legs: the other exchange, the prefix route")
         other = "alltoall" if plan["exchange"] == "allgather" else "allgather"
         try:
@@ -692,11 +693,12 @@ def main():
                                                         got_idx.reshape(-1, a.k), tlo)
         except Exception as e:  # noqa: BLE001 -- an extra leg must not cost the headline
             extra[f"broadcast_{other}"] = {"error": repr(e)}
-        try:
-            if (world & (world - 1)) == 0:
-                extra["prefix_weak"] = prefix_weak_leg(a, L, dev, world, rank)
-        except Exception as e:  # noqa: BLE001
-            extra["prefix_weak"] = {"error": repr(e)}
+        for name, strong in (("prefix_strong", True), ("prefix_weak", False)):
+            try:
+                if (world & (world - 1)) == 0:
+                    extra[name] = prefix_leg(a, L, dev, world, rank, strong)
+            except Exception as e:  # noqa: BLE001
+                extra[name] = {"error": repr(e)}
     if world > 1 and not a.no_extra and a.algo == "batch" and not a.rehearse_one_gpu:
         progress("cfg3 leg over the ranks")
         try:
@@ -1087,12 +1089,16 @@ def broadcast_leg(a, L, dev, world, rank, exchange, tp, ts, ctx, lo, ref_idx, re
             "equals_headline_rank0": same, "rows_compared_rank0": max(0, a1 - a0)}
 
 
-def prefix_weak_leg(a, L, dev, world, rank):
-    """The prefix route beside the headline (labelled): every rank keeps the one-GPU workload
-    (--n ids and --q targets per GPU, weak scaling), ids and targets routed by their top
-    log2(N) bits, no collective on the data path, shard-local result indices."""
+def prefix_leg(a, L, dev, world, rank, strong):
+    """The prefix route beside the headline (labelled; SURVEY 8(e)'s "better scheme"): ids and
+    targets routed by their top log2(N) bits, no collective on the data path, shard-local result
+    indices.  weak: every rank keeps the one-GPU workload (--n ids and --q targets per GPU);
+    strong: the headline's own problem (--n ids and --q targets in total, every target on every
+    rank as on the broadcast route, each rank answering those of its prefix from its 1/N of the
+    ids) -- exact like the broadcast route (a target's top-k lies in its own prefix subtree when
+    every shard holds >= k ids), with 1/N of its work and no exchange."""
     pbits = world.bit_length() - 1
-    n_tot, q_tot = a.n * world, a.q * world
+    n_tot, q_tot = (a.n, a.q) if strong else (a.n * world, a.q * world)
     c = opendht_amd.Context(dev.index)
     try:
         c.gen_ids_prefix(a.seed + 20, n_tot, pbits, rank)
@@ -1113,6 +1119,12 @@ def prefix_weak_leg(a, L, dev, world, rank):
             c.batch_topk_dev(tp.data_ptr(), ts, ql, a.k, outs[i][0].data_ptr(), outs[i][1].data_ptr(), None, 0,
                              streams[i].cuda_stream)
         ms = timed_steps(step, a.steps, a.warmup, dev)
+        if strong:
+            return {"route": "prefix", "scaling": "strong", "ms_per_step": ms, "value": q_tot / (ms * 1e-3),
+                    "unit": "queries/s", "workload": f"{q_tot} targets x {n_tot} ids in total over {world} (the headline's)",
+                    "ids_rank": c.num_ids, "targets_rank": ql,
+                    "note": "the headline's problem on the prefix route: each rank answers its own prefix's targets "
+                            "from its prefix shard; no data-path collective (results stay on the owning rank)"}
         return {"route": "prefix", "scaling": "weak", "ms_per_step": ms, "value": q_tot / (ms * 1e-3),
                 "unit": "queries/s", "workload": f"{a.q} targets x {a.n} ids per GPU ({q_tot} x {n_tot} over {world})",
                 "ids_rank": c.num_ids, "targets_rank": ql,
