@@ -1905,6 +1905,9 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
 // shards stream their shifted word-0 plane, as K6 does.
 namespace {
 constexpr uint32_t kSmallQ = 64;
+#ifndef DHT_S2_MEAS
+#define DHT_S2_MEAS 0   // measurement builds only (results wrong): 1 no answers, 2 no scan roles
+#endif
 constexpr uint32_t kSmallCap = 512;                   // candidates per prefix bucket
 constexpr uint32_t kS1Queue = 512;                    // matched ids queued in LDS per block
 constexpr uint32_t kSmallFbBlocks = 32;               // K1 fallback scan workgroups (S2's scan roles)
@@ -2168,6 +2171,7 @@ __global__ __launch_bounds__(kS2Threads) void k_s2_answer(F3Args a, SmallArgs sa
     const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
     if (blockIdx.x == 0 && threadIdx.x < kSmallQ) sa.cnt_next[threadIdx.x] = 0;   // the next call's counters
     if (blockIdx.x >= sa.q) {
+        if (DHT_S2_MEAS & 2) return;
         // ---- scan role r: the fallback list, from the final bucket counts (one round trip) ----
         const uint32_t r = blockIdx.x - sa.q;
         uint32_t* list = sa.fb + r * kSmallQ;   // this role's own copy (every role builds the same)
@@ -2197,6 +2201,7 @@ __global__ __launch_bounds__(kS2Threads) void k_s2_answer(F3Args a, SmallArgs sa
     // ---- prefix workgroup s: one round trip for the table, the count, the targets' words and
     // the bucket (one slot per thread) ----
     const uint32_t s = blockIdx.x;
+    const unsigned long long mt0 = (DHT_S2_MEAS & 4) ? __builtin_amdgcn_s_memrealtime() : 0ull;
     uint4* S = reinterpret_cast<uint4*>(lds);
     uint32_t* tl = lds + 4 * kSmallCap;   // this prefix's targets
     uint32_t* tw = tl + kSmallQ;          // [DHT_W][kSmallQ] target words
@@ -2218,6 +2223,8 @@ __global__ __launch_bounds__(kS2Threads) void k_s2_answer(F3Args a, SmallArgs sa
     if (tj < DHT_W) tw[tj * kSmallQ + tq] = twv;
     __syncthreads();
     if (c < want || c > kSmallCap) return;   // the scan roles answer this prefix's targets
+    if (DHT_S2_MEAS & 1) return;
+    const unsigned long long mt1 = (DHT_S2_MEAS & 4) ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint32_t ntl = misc[0];
     for (uint32_t i = wv; i < ntl; i += scan::WAVES) {
         const uint32_t qi = __builtin_amdgcn_readfirstlane(tl[i]);
@@ -2226,6 +2233,10 @@ __global__ __launch_bounds__(kS2Threads) void k_s2_answer(F3Args a, SmallArgs sa
         for (int j = 0; j < DHT_W; ++j) t[j] = __builtin_amdgcn_readfirstlane(tw[j * kSmallQ + qi]);
         const uint32_t t0 = sa.shift ? (t[0] << sa.shift) | (t[1] >> (32 - sa.shift)) : t[0];
         ks_answer(a, S, c, qi, t0, t, want, lane);
+        if (DHT_S2_MEAS & 4) {
+            const unsigned long long mt2 = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0) printf("S2 blk %u q %u c %u ntl %u load+sync %llu answer %llu (x10ns)\n", s, sa.q, c, ntl, mt1 - mt0, mt2 - mt1);
+        }
     }
 }
 
