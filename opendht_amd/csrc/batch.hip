@@ -626,6 +626,23 @@ __device__ __forceinline__ bool key2_less(uint32_t da, uint32_t a1, uint32_t ia,
     return id_less(da, ia, db, ib, planes, stride, t);
 }
 
+// rank of this lane's candidate by (w0 distance md, w1 distance m1) among the mm candidates of
+// lanes [0, mm) (mm wave-uniform): a branch-free count over readlanes.  *tie: another candidate
+// has the same 64-bit distance (only then does the order need words 2..4 and the index).  The
+// branchy form (full-key compare inside the loop) ran ~135 ns per candidate: exec-mask saves and
+// scalar branches around every readlane (S2 stamps, profiles/r04/experiments/s2_stamps.txt).
+__device__ __forceinline__ uint32_t wave_rank64(uint32_t md, uint32_t m1, uint32_t mm, uint32_t lane, bool* tie) {
+    uint32_t rank = 0, eq = 0;
+    for (uint32_t o = 0; o < mm; ++o) {
+        const uint32_t xd = (uint32_t)__builtin_amdgcn_readlane((int)md, (int)o);
+        const uint32_t x1 = (uint32_t)__builtin_amdgcn_readlane((int)m1, (int)o);
+        rank += (uint32_t)(xd < md) | ((uint32_t)(xd == md) & (uint32_t)(x1 < m1));
+        eq |= (uint32_t)(xd == md) & (uint32_t)(x1 == m1) & (uint32_t)(o != lane);
+    }
+    *tie = eq != 0;
+    return rank;
+}
+
 // exact answer for one target from <= 64 candidates, one per lane (lane < mm): its rank is
 // the number of candidates strictly closer by (w0, w1) distance (full key on a double tie).
 // Word 1 and the target are loaded unconditionally (clamped), in one round trip.
@@ -635,13 +652,17 @@ __device__ void wave_rank_loaded(const F3Args& a, uint2 me, uint32_t mm, uint32_
     const bool act = lane < mm;
     const uint32_t md = me.x ^ t0;
     const uint32_t m1 = act ? w1 ^ t[1] : DHT_NONE;
-    uint32_t rank = 0;
-    for (uint32_t o = 0; o < mm; ++o) {
-        const uint32_t xd = __builtin_amdgcn_readlane((int)md, (int)o);
-        const uint32_t x1 = __builtin_amdgcn_readlane((int)m1, (int)o);
-        const uint32_t xi = __builtin_amdgcn_readlane((int)me.y, (int)o);
-        if (xd < md || (xd == md && x1 < m1)) ++rank;
-        else if (xd == md && x1 == m1 && act && o != lane && id_less(xd, xi, md, me.y, a.planes, a.stride, t)) ++rank;
+    bool tie;
+    uint32_t rank = wave_rank64(md, m1, mm, lane, &tie);
+    if (__ballot(act && tie)) {   // a 64-bit distance tie (duplicate ids): the full key decides
+        rank = 0;
+        for (uint32_t o = 0; o < mm; ++o) {
+            const uint32_t xd = __builtin_amdgcn_readlane((int)md, (int)o);
+            const uint32_t x1 = __builtin_amdgcn_readlane((int)m1, (int)o);
+            const uint32_t xi = __builtin_amdgcn_readlane((int)me.y, (int)o);
+            if (xd < md || (xd == md && x1 < m1)) ++rank;
+            else if (xd == md && x1 == m1 && act && o != lane && id_less(xd, xi, md, me.y, a.planes, a.stride, t)) ++rank;
+        }
     }
     uint32_t* orow = a.out_idx + (uint64_t)qi * a.k;
     if (act && rank < want) orow[rank] = map_out(me.y, a.gidx, a.base);
@@ -1905,9 +1926,6 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
 // shards stream their shifted word-0 plane, as K6 does.
 namespace {
 constexpr uint32_t kSmallQ = 64;
-#ifndef DHT_S2_MEAS
-#define DHT_S2_MEAS 0   // measurement builds only (results wrong): 1 no answers, 2 no scan roles
-#endif
 constexpr uint32_t kSmallCap = 512;                   // candidates per prefix bucket
 constexpr uint32_t kS1Queue = 512;                    // matched ids queued in LDS per block
 constexpr uint32_t kSmallFbBlocks = 32;               // K1 fallback scan workgroups (S2's scan roles)
@@ -2117,13 +2135,17 @@ __device__ void ks_answer(const F3Args& a, const uint4* S, uint32_t c, uint32_t 
         const bool act = lane < c;
         const uint4 me = S[act ? lane : 0u];
         const uint32_t md = act ? me.x ^ t0 : DHT_NONE, m1 = act ? me.z ^ t[1] : DHT_NONE;
-        uint32_t rank = 0;
-        for (uint32_t o = 0; o < c; ++o) {
-            const uint32_t xd = __builtin_amdgcn_readlane((int)md, (int)o);
-            const uint32_t x1 = __builtin_amdgcn_readlane((int)m1, (int)o);
-            const uint32_t xi = __builtin_amdgcn_readlane((int)me.y, (int)o);
-            if (xd < md || (xd == md && x1 < m1)) ++rank;
-            else if (xd == md && x1 == m1 && act && o != lane && id_less(xd, xi, md, me.y, a.planes, a.stride, t)) ++rank;
+        bool tie;
+        uint32_t rank = wave_rank64(md, m1, __builtin_amdgcn_readfirstlane(c), lane, &tie);
+        if (__ballot(act && tie)) {   // a 64-bit distance tie (duplicate ids): the full key decides
+            rank = 0;
+            for (uint32_t o = 0; o < c; ++o) {
+                const uint32_t xd = __builtin_amdgcn_readlane((int)md, (int)o);
+                const uint32_t x1 = __builtin_amdgcn_readlane((int)m1, (int)o);
+                const uint32_t xi = __builtin_amdgcn_readlane((int)me.y, (int)o);
+                if (xd < md || (xd == md && x1 < m1)) ++rank;
+                else if (xd == md && x1 == m1 && act && o != lane && id_less(xd, xi, md, me.y, a.planes, a.stride, t)) ++rank;
+            }
         }
         if (act && rank < want) orow[rank] = map_out(me.y, a.gidx, a.base);
     } else {
@@ -2171,7 +2193,6 @@ __global__ __launch_bounds__(kS2Threads) void k_s2_answer(F3Args a, SmallArgs sa
     const uint32_t want = a.n < a.k ? (uint32_t)a.n : a.k;
     if (blockIdx.x == 0 && threadIdx.x < kSmallQ) sa.cnt_next[threadIdx.x] = 0;   // the next call's counters
     if (blockIdx.x >= sa.q) {
-        if (DHT_S2_MEAS & 2) return;
         // ---- scan role r: the fallback list, from the final bucket counts (one round trip) ----
         const uint32_t r = blockIdx.x - sa.q;
         uint32_t* list = sa.fb + r * kSmallQ;   // this role's own copy (every role builds the same)
@@ -2201,7 +2222,6 @@ __global__ __launch_bounds__(kS2Threads) void k_s2_answer(F3Args a, SmallArgs sa
     // ---- prefix workgroup s: one round trip for the table, the count, the targets' words and
     // the bucket (one slot per thread) ----
     const uint32_t s = blockIdx.x;
-    const unsigned long long mt0 = (DHT_S2_MEAS & 4) ? __builtin_amdgcn_s_memrealtime() : 0ull;
     uint4* S = reinterpret_cast<uint4*>(lds);
     uint32_t* tl = lds + 4 * kSmallCap;   // this prefix's targets
     uint32_t* tw = tl + kSmallQ;          // [DHT_W][kSmallQ] target words
@@ -2223,8 +2243,6 @@ __global__ __launch_bounds__(kS2Threads) void k_s2_answer(F3Args a, SmallArgs sa
     if (tj < DHT_W) tw[tj * kSmallQ + tq] = twv;
     __syncthreads();
     if (c < want || c > kSmallCap) return;   // the scan roles answer this prefix's targets
-    if (DHT_S2_MEAS & 1) return;
-    const unsigned long long mt1 = (DHT_S2_MEAS & 4) ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint32_t ntl = misc[0];
     for (uint32_t i = wv; i < ntl; i += scan::WAVES) {
         const uint32_t qi = __builtin_amdgcn_readfirstlane(tl[i]);
@@ -2233,10 +2251,6 @@ __global__ __launch_bounds__(kS2Threads) void k_s2_answer(F3Args a, SmallArgs sa
         for (int j = 0; j < DHT_W; ++j) t[j] = __builtin_amdgcn_readfirstlane(tw[j * kSmallQ + qi]);
         const uint32_t t0 = sa.shift ? (t[0] << sa.shift) | (t[1] >> (32 - sa.shift)) : t[0];
         ks_answer(a, S, c, qi, t0, t, want, lane);
-        if (DHT_S2_MEAS & 4) {
-            const unsigned long long mt2 = __builtin_amdgcn_s_memrealtime();
-            if (lane == 0) printf("S2 blk %u q %u c %u ntl %u load+sync %llu answer %llu (x10ns)\n", s, sa.q, c, ntl, mt1 - mt0, mt2 - mt1);
-        }
     }
 }
 
