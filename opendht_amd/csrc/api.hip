@@ -634,7 +634,7 @@ static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hi
     if (b.zeroed < head) DHT_TRY(hipMemsetAsync(b.ws.p, 0, head, s));
     b.zeroed = 0;   // re-established below once every launch went through
     if (bc.dbg & 256) {
-        DHT_TRY(c->stamps.ensure((size_t)2 * 8192 * 16 * 8));
+        DHT_TRY(c->stamps.ensure((size_t)3 * 8192 * 16 * 8));
         bc.stamps = c->stamps.as<unsigned long long>();
     }
     bc.ws = b.ws.p;

@@ -1037,6 +1037,9 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                 }
             }
         }
+        if (Diag && (a.dbg & 256) && t0i == 0) {   // per wave: the end of its phase-A work
+            if (lane == 0) a.stamps[2ull * 8192 * 16 + (uint64_t)blockIdx.x * 16 + wv] = __builtin_amdgcn_s_memrealtime();
+        }
         sync_lds();
         if (t0i == 0) F3_STAMP(5);
         if (Diag && (a.dbg & 256) && threadIdx.x == 0 && t0i == 0) {
@@ -1546,6 +1549,10 @@ void print_phase_profile(const BatchPlan& P, uint32_t nblk2, uint32_t np, unsign
                     fprintf(stderr, "  A: level %.2f loop %.2f merge %.2f out %.2f",
                             (double)(h[b * 16 + 8] - h[b * 16 + 4]) / 100.0, (double)(h[b * 16 + 9] - h[b * 16 + 8]) / 100.0,
                             (double)(h[b * 16 + 10] - h[b * 16 + 9]) / 100.0, (double)(h[b * 16 + 5] - h[b * 16 + 10]) / 100.0);
+                    std::vector<unsigned long long> hw(16);
+                    (void)hipMemcpy(hw.data(), stamps + 2ull * 8192 * 16 + (uint64_t)b * 16, 16 * 8, hipMemcpyDeviceToHost);
+                    fprintf(stderr, "  waves end");
+                    for (int w = 0; w < 4; ++w) fprintf(stderr, " %.2f", hw[w] ? (double)(hw[w] - t0min) / 100.0 : -1.0);
                     fprintf(stderr, "\n");
                 }
             }
@@ -1830,7 +1837,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         else kern<<<g, b, lds, s>>>(args...);
     };
     unsigned long long* stamps = (dbg & 256) ? c.stamps : nullptr;   // F3 [8192][16] then F2 [8192][16]
-    if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)2 * 8192 * 16 * 8, s);
+    if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)3 * 8192 * 16 * 8, s);
     const F1Args a1{c.tp, c.tp + c.ts, q, P.Lm, P.b1, c.skip, c.sub_shift, c.nsub ? c.sub_bits : 0u, np, P.nwords,
                     bitmap, tcount, tbuf, P.tcap, ctr, tspill};
     go(0, k_f1_targets, dim3((q + kF1Threads - 1) / kF1Threads), dim3(kF1Threads), 0, a1);
