@@ -1,5 +1,5 @@
 # Round-4 K2 (word-0 streaming classify): parity tests, the variants (workgroups per CU x uint4 per
-# lane) three times each, PMC FETCH/WRITE of the in-tree build.   usage: bash tools/gpu_r04_k2.sh [tag]
+# lane) three times each, PMC FETCH/WRITE of the in-tree build.   usage: bash tools/experiments/gpu_r04_k2.sh [tag]
 set -o pipefail
 OUT=gpurun_out/${1:-r04k2}; mkdir -p $OUT
 export TMPDIR=/tmp

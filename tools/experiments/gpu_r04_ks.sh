@@ -1,5 +1,5 @@
 # KS A/B: the small-batch tests on the in-tree build, then S1/S2 per q for builds name=path (rotated x3),
-# on the cfg-2 set and the 2^26 set.   usage: bash tools/gpu_r04_ks.sh tag name=path ...
+# on the cfg-2 set and the 2^26 set.   usage: bash tools/experiments/gpu_r04_ks.sh tag name=path ...
 set -o pipefail
 TAG=$1; shift; OUT=gpurun_out/$TAG; mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "small or kat" > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }

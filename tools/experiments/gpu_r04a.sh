@@ -1,7 +1,7 @@
 # Round-4 pass A: the whole GPU suite + smoke, the driver-shaped bench (20 steps, every leg, CPU
 # baseline; small batches now warm / cold / past the Infinity Cache), a 2-rank rehearsal of the new
 # N > 1 default (broadcast route, strong scaling of cfg 2) on one GPU, PMC traffic for the small-batch
-# cold / 2^26 rows and the per-rank cfg-2 shards (N = 2, 4, 8).   usage: bash tools/gpu_r04a.sh [out-tag]
+# cold / 2^26 rows and the per-rank cfg-2 shards (N = 2, 4, 8).   usage: bash tools/experiments/gpu_r04a.sh [out-tag]
 set -o pipefail
 OUT=gpurun_out/${1:-r04a}; mkdir -p $OUT
 export TMPDIR=/tmp
