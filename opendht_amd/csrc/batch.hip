@@ -341,7 +341,10 @@ constexpr uint32_t kRing = 8;     // S1's ring (two 512-thread workgroups per CU
 // workgroup per CU (tools/experiments/stream_probe.hip, profiles/r03/experiments) takes
 // 13.3 us with 8 (128 KB in flight), 11.7 with 4, 11.1 with 3, 10.3 with 2: a deeper ring only
 // queues longer.  F2 at cfg 2: 21.9 us with 4, 21.3 with 3, 20.7 with 2 (round 2: 8, 24.1 us)
-constexpr uint32_t kF2Ring = 2;
+#ifndef DHT_F2_RING
+#define DHT_F2_RING 2   // (override: ring-depth A/B builds)
+#endif
+constexpr uint32_t kF2Ring = DHT_F2_RING;
 // The ring loads are buffer loads through a descriptor based at the workgroup's first id
 // (f2_rsrc): the plane pointers come from sub-partition descriptors in memory, whose address
 // space the compiler cannot infer -- plain loads through them are FLAT loads, which also count

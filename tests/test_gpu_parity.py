@@ -273,6 +273,30 @@ def test_classify_register_path_shapes(ctx, shape):
     assert bad.size == 0, f"{bad.size} buckets differ, first {bad[:5]}"
 
 
+def test_classify_register_path_every_bin(ctx):
+    """K2's register path takes commonBits c < 15 from clz(word 0 ^ myid's word 0) and sends
+    c >= 15 to the exact path: ids with every commonBits 0..40 (myid with bit c flipped, random
+    bits below), on a grown routing table, bucket and whole histogram = oracle."""
+    rng = np.random.default_rng(4242)
+    myid = O.gen_ids(21, 1)[0]
+    firsts, _, _ = O.Table(myid).grow(O.gen_ids(22, 50000)).export()
+    per = 257
+    ids = O.gen_ids(23, 41 * per)
+    bits = np.unpackbits(myid)
+    for c in range(41):
+        blk = np.unpackbits(ids[c * per:(c + 1) * per], axis=1)
+        blk[:, :c] = bits[:c]
+        blk[:, c] = 1 - bits[c]
+        ids[c * per:(c + 1) * per] = np.packbits(blk, axis=1)
+    ids = ids[rng.permutation(ids.shape[0])]
+    ctx.set_ids(ids)
+    b, hist = ctx.classify(firsts, myid)
+    wb, wh = O.classify(firsts, myid, ids)
+    assert np.array_equal(hist, wh)
+    assert all(int(hist[c]) == per for c in range(41))
+    assert np.array_equal(b, wb)
+
+
 def test_cached_nodes_vs_oracle(ctx):
     ids = O.gen_ids(21, 50000)
     s = ids[np.lexsort(ids.T[::-1])]

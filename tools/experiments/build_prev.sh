@@ -2,7 +2,7 @@
 # the in-tree build (tools/experiments/gpu_ab_lib.sh, tools/experiments/gpu_ab_libs.sh).   usage: bash tools/experiments/build_prev.sh [rev] [name]
 set -e
 REV=${1:-HEAD}; NAME=${2:-prev}
-ROOT=$(cd "$(dirname "$0")/.." && pwd)
+ROOT=$(cd "$(dirname "$0")/../.." && pwd)
 WT=$(mktemp -d /tmp/dhtgpu_wt.XXXXXX)
 git -C "$ROOT" worktree add -q "$WT" "$REV"
 make -C "$WT/opendht_amd/csrc" -j8 >/dev/null
