@@ -479,12 +479,16 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                 const uint32_t rem = hi - sb;
                 bool sv[4];
                 uint64_t bal[4];
+                // the four bitmap words first (one LDS wait for all four: read one at a time, each
+                // read waited before the next issued)
+                uint32_t bw[4];
+#pragma unroll
+                for (uint32_t f = 0; f < 4; ++f) bw[f] = bm[__builtin_amdgcn_ubfe(v4[f], pre_off + 5, lm5)];
 #pragma unroll
                 for (uint32_t f = 0; f < 4; ++f) {
                     // prefix bit: word pre >> 5 of the bitmap, bit pre & 31 (v_bfe masks it)
                     const uint32_t pre = __builtin_amdgcn_ubfe(v4[f], pre_off, a.Lm);
-                    const uint32_t wi = __builtin_amdgcn_ubfe(v4[f], pre_off + 5, lm5);
-                    const bool hit = __builtin_amdgcn_ubfe(bm[wi], pre, 1) != 0, in = tid4 + f < rem;
+                    const bool hit = __builtin_amdgcn_ubfe(bw[f], pre, 1) != 0, in = tid4 + f < rem;
                     sv[f] = hit && in;
                     bal[f] = __builtin_amdgcn_ballot_w64(hit) & __builtin_amdgcn_ballot_w64(in);
                 }
