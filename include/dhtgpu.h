@@ -49,6 +49,8 @@ extern "C" {
 #define DHTGPU_WORDS 5u              /* a 160-bit id = 5 big-endian u32 words */
 #define DHTGPU_MAX_K 32u             /* largest k / count served */
 #define DHTGPU_NONE 0xFFFFFFFFu      /* index padding for short results */
+#define DHTGPU_REC_WORDS 3u          /* candidate record: {w0, w1, global index} (12 B) */
+#define DHTGPU_MAX_LISTS 64u         /* candidate lists one merge takes (ranks of a sharded lookup) */
 
 enum {
     DHTGPU_OK = 0,
@@ -104,18 +106,40 @@ int dhtgpu_topk(dhtgpu_ctx* ctx, const uint8_t* targets20_be, uint32_t q, uint32
 
 /* Device form.  Targets as word planes (t_planes[j*t_stride + i]).  Writes either
  * the final indices (out_idx/out_cnt, offset by idx_base) or, if out_rec != NULL,
- * candidate records out_rec[(qi*k + r)*6 + {w0..w4, idx}] for a cross-shard merge
- * (idx offset by idx_base, DHTGPU_NONE for empty slots). */
+ * candidate records for a cross-shard merge: out_rec[(qi*k + r)*3 + {w0, w1, idx}] = the
+ * first two words of the r-th closest id and its index offset by idx_base (global index
+ * of a prefix shard context), ascending in XOR distance; all DHTGPU_NONE for empty slots. */
 int dhtgpu_topk_dev(dhtgpu_ctx* ctx, const uint32_t* t_planes, uint64_t t_stride, uint32_t q,
                     uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec,
                     uint32_t idx_base, void* stream);
 
-/* K3: merge `lists` candidate-record lists per target (rec[((l*q)+qi)*k_in + r]*6,
- * as written by dhtgpu_topk_dev) into the final top-k.  Used after the RCCL
- * all-gather of per-GPU shards. */
+/* K3: merge `lists` (<= DHTGPU_MAX_LISTS) candidate-record lists per target,
+ * rec[((l*q + qi)*k_in + r)*3] as written by the record forms (each list ascending in XOR
+ * distance, DHTGPU_NONE records after its valid ones), into the final top-k.  Used after the
+ * RCCL all-gather of per-GPU shards.  The records carry 64 bits of each id: a row where two
+ * lists' candidates agree on them (two ids sharing their first 64 bits -- never among the
+ * candidates of hash-distributed ids -- or one id sent by two lists) is answered provisionally
+ * and appended to ties = {count, rows[tie_cap]} (device, zeroed by this call; may be NULL only
+ * when lists == 1); such rows are settled by the second exchange: dhtgpu_tie_words_dev on every
+ * shard, then dhtgpu_merge_ties_dev.  Records equal in all five words and the index are one
+ * candidate; different ids with equal indices are both kept. */
 int dhtgpu_merge_dev(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_t k_in,
                      const uint32_t* t_planes, uint64_t t_stride, uint32_t k,
-                     uint32_t* out_idx, uint32_t* out_cnt, void* stream);
+                     uint32_t* out_idx, uint32_t* out_cnt, uint32_t* ties, uint32_t tie_cap, void* stream);
+/* The second exchange's payload from one shard: words 2..4 of this context's candidates
+ * (rec: its own q x k records from a record-form call with idx_base) in the rows listed by
+ * ties (each row + row_base: the row's place in rec when the merge took a slice of the
+ * targets), out_words[(slot*k + r)*3 + {w2, w3, w4}] for slot < min(count, tie_cap); ties ==
+ * NULL: every row (slot = row), the fallback when count > tie_cap. */
+int dhtgpu_tie_words_dev(dhtgpu_ctx* ctx, const uint32_t* rec, uint32_t q, uint32_t k, uint32_t idx_base,
+                         const uint32_t* ties, uint32_t tie_cap, uint32_t row_base, uint32_t* out_words,
+                         void* stream);
+/* Settle the listed rows (every row when ties == NULL) of a dhtgpu_merge_dev by the full
+ * 160-bit keys: words = the lists' tie-word payloads concatenated in list order (each
+ * tie_cap x k_in x 3 words, or q x k_in x 3 when ties == NULL). */
+int dhtgpu_merge_ties_dev(const uint32_t* rec, const uint32_t* words, uint32_t lists, uint32_t q, uint32_t k_in,
+                          const uint32_t* t_planes, uint64_t t_stride, uint32_t k, const uint32_t* ties,
+                          uint32_t tie_cap, uint32_t* out_idx, uint32_t* out_cnt, void* stream);
 
 /* Device planes -> the ids whose top pbits bits equal pval, compacted in order into
  * out_planes (out_stride >= count) with out_gidx[j] = original index (nullable);

@@ -75,7 +75,11 @@ def lib():
         "dhtgpu_topk_dev": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp,
                              ctypes.c_uint32, _vp], ctypes.c_int),
         "dhtgpu_merge_dev": ([_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _vp, ctypes.c_uint64,
-                              ctypes.c_uint32, _vp, _vp, _vp], ctypes.c_int),
+                              ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_uint32, _vp], ctypes.c_int),
+        "dhtgpu_tie_words_dev": ([_vp, _vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _vp, ctypes.c_uint32,
+                                  ctypes.c_uint32, _vp, _vp], ctypes.c_int),
+        "dhtgpu_merge_ties_dev": ([_vp, _vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _vp, ctypes.c_uint64,
+                                   ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, _vp, _vp], ctypes.c_int),
         "dhtgpu_pack_dev": ([_vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp], ctypes.c_int),
         "dhtgpu_gen_dev": ([ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp],
                            ctypes.c_int),
@@ -134,7 +138,8 @@ def exported_symbols():
     """Names of every entry point declared in include/dhtgpu.h (for the ABI test)."""
     return ["dhtgpu_strerror", "dhtgpu_device_count", "dhtgpu_ctx_create", "dhtgpu_ctx_destroy",
             "dhtgpu_ctx_stream", "dhtgpu_set_ids", "dhtgpu_gen_ids", "dhtgpu_num_ids", "dhtgpu_get_ids",
-            "dhtgpu_ids_dev", "dhtgpu_topk", "dhtgpu_topk_dev", "dhtgpu_merge_dev", "dhtgpu_pack_dev",
+            "dhtgpu_ids_dev", "dhtgpu_topk", "dhtgpu_topk_dev", "dhtgpu_merge_dev", "dhtgpu_tie_words_dev",
+            "dhtgpu_merge_ties_dev", "dhtgpu_pack_dev",
             "dhtgpu_gen_dev", "dhtgpu_find_closest", "dhtgpu_classify", "dhtgpu_classify_dev",
             "dhtgpu_cached_nodes", "dhtgpu_index_build", "dhtgpu_index_topk_dev", "dhtgpu_index_topk",
             "dhtgpu_index_build_timed", "dhtgpu_gen_ids_prefix", "dhtgpu_select_prefix_dev",
@@ -297,6 +302,12 @@ class Context:
         arr = (_vp * 8)(*[e.cuda_event for e in events])
         _check(lib().dhtgpu_batch_events(self._h, arr), "batch_events")
 
+    def tie_words_dev(self, rec_ptr, q, k, idx_base, ties_ptr, tie_cap, row_base, out_words_ptr, stream=None):
+        """Words 2..4 of this context's candidates (its own q x k compact records) in the rows a merge
+        listed as 64-bit ties (ties_ptr None: every row) -- the second exchange's payload."""
+        _check(lib().dhtgpu_tie_words_dev(self._h, rec_ptr, q, k, idx_base, ties_ptr, tie_cap, row_base,
+                                          out_words_ptr, stream), "tie_words_dev")
+
     def topk_dev(self, t_planes_ptr, t_stride, q, k, out_idx_ptr=None, out_cnt_ptr=None, out_rec_ptr=None,
                  idx_base=0, stream=None):
         _check(lib().dhtgpu_topk_dev(self._h, t_planes_ptr, t_stride, q, k, out_idx_ptr, out_cnt_ptr,
@@ -370,20 +381,28 @@ class Context:
         """Requests per search round for later search_batch calls (default 4 =
         MAX_REQUESTED_SEARCH_NODES, include/opendht/dht.h:321)."""
         _check(lib().dhtgpu_set_search_alpha(self._h, int(alpha)), "set_search_alpha")
+        self._alpha = int(alpha)
 
     def search_batch(self, targets, searchers, max_rounds=64, alpha=None):
         """Iterative searches: (idx (q,64), flags (q,64), len (q,), rounds (q,), queries (q,)).
-        alpha (optional): requests per round, set on the context for this and later calls."""
-        if alpha is not None:
-            self.set_search_alpha(alpha)
+        alpha (optional): requests per round for THIS call only (the context's setting,
+        set_search_alpha, default 4 = MAX_REQUESTED_SEARCH_NODES, is restored afterwards)."""
         t = _ids(targets, "targets")
         q = t.shape[0]
         sr = np.ascontiguousarray(searchers, dtype=np.uint32).reshape(q)
         idx = np.empty((q, 64), np.uint32)
         fl = np.empty((q, 64), np.uint8)
         ln, rd, qs = (np.empty(q, np.uint32) for _ in range(3))
-        _check(lib().dhtgpu_search_batch(self._h, _p(t, _u8p), q, _p(sr, _u32p), max_rounds, _p(idx, _u32p),
-                                         _p(fl, _u8p), _p(ln, _u32p), _p(rd, _u32p), _p(qs, _u32p)), "search_batch")
+        saved = getattr(self, "_alpha", 4)
+        if alpha is not None:
+            _check(lib().dhtgpu_set_search_alpha(self._h, int(alpha)), "set_search_alpha")
+        try:
+            _check(lib().dhtgpu_search_batch(self._h, _p(t, _u8p), q, _p(sr, _u32p), max_rounds, _p(idx, _u32p),
+                                             _p(fl, _u8p), _p(ln, _u32p), _p(rd, _u32p), _p(qs, _u32p)),
+                   "search_batch")
+        finally:
+            if alpha is not None:
+                _check(lib().dhtgpu_set_search_alpha(self._h, int(saved)), "set_search_alpha")
         return idx, fl, ln, rd, qs
 
     # ---- K2: classification -------------------------------------------------------

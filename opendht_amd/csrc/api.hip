@@ -68,11 +68,6 @@ struct dhtgpu_ctx {
     int num_cus = 256;
     hipStream_t stream = nullptr;
     DevBuf planes;          // 5 * stride u32
-    // the set as 24-B records {w0..w4, 0} for record-mode calls (the multi-GPU broadcast route's
-    // candidate records: one 24-B read per candidate instead of five scattered plane reads); built
-    // on the first record-mode call, kept until the set changes
-    DevBuf aos;
-    bool aos_valid = false;
     uint64_t n = 0, stride = 0;
     bool sorted = false;
     DevBuf staging;         // host<->device byte staging
@@ -248,7 +243,7 @@ void dhtgpu_ctx_destroy(dhtgpu_ctx* c) {
         for (DevBuf* d : {&b.ws, &b.out_idx, &b.out_cnt, &b.sws}) d->release();
     c->invalidate_subs();
     if (c->fb_hint) (void)hipHostFree(c->fb_hint);
-    for (DevBuf* b : {&c->aos, &c->stamps, &c->w0s, &c->sview.planes, &c->sview.perm,
+    for (DevBuf* b : {&c->stamps, &c->w0s, &c->sview.planes, &c->sview.perm,
                       &c->cache.planes, &c->cache.perm, &c->cache_in, &c->sort_scratch, &c->cache_acc, &c->srch})
         b->release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -276,20 +271,6 @@ static int finish_ids(dhtgpu_ctx* c, uint64_t n) {
     return DHTGPU_OK;
 }
 
-// the record-mode gather source (nullptr: gather from the planes, e.g. when the copy cannot be
-// allocated)
-static const uint32_t* rec_aos(dhtgpu_ctx* c, hipStream_t s) {
-    if (!c->aos_valid) {
-        if (c->aos.ensure((size_t)(c->n ? c->n : 1) * 24) != hipSuccess) return nullptr;
-        // built once per set; synchronised, so that calls on other streams may read it at once
-        if (launch_pack_aos(c->planes.as<uint32_t>(), c->stride, c->n, c->aos.as<uint32_t>(), s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            return nullptr;
-        c->aos_valid = true;
-    }
-    return c->aos.as<uint32_t>();
-}
-
 static int alloc_ids(dhtgpu_ctx* c, uint64_t n) {
     if (n >= 0xFFFFFFFFull) return DHTGPU_ERANGE;
     c->has_ids = false;
@@ -300,7 +281,6 @@ static int alloc_ids(dhtgpu_ctx* c, uint64_t n) {
     c->has_gidx = false;
     c->invalidate_subs();
     c->sview.valid = false;
-    c->aos_valid = false;
     c->stride = pad_ids(n ? n : 1);
     DHT_TRY(c->planes.ensure((size_t)c->stride * 5 * 4));
     return DHTGPU_OK;
@@ -431,7 +411,7 @@ int dhtgpu_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, 
     const ScanPlan p = plan_scan(c->n, q, k, c->num_cus);
     const uint32_t* gidx = c->out_map();
     const bool one = p.splits == 1 || c->n == 0;
-    if (one && !(out_rec && gidx)) {   // one pass writes the final form directly
+    if (one && !out_rec) {   // one pass writes the final form directly
         DHT_TRY(launch_scan(c->planes.as<uint32_t>(), c->stride, c->n, p, tp, ts, q, k, out_idx, out_cnt, out_rec,
                             gidx, idx_base, s));
         return DHTGPU_OK;
@@ -456,8 +436,7 @@ int dhtgpu_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, 
         DHT_TRY(launch_merge(c->rec.as<uint32_t>(), p.splits, q, k, tp, ts, k, li, lc, s));
     }
     if (out_rec)
-        DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
-                                    out_rec, s, rec_aos(c, s)));
+        DHT_TRY(launch_rec3(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx, out_rec, s));
     else
         DHT_TRY(launch_map_idx(li, (uint64_t)q * k, gidx, idx_base, s));
     return DHTGPU_OK;
@@ -465,12 +444,42 @@ int dhtgpu_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, 
 
 int dhtgpu_merge_dev(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_t k_in,
                      const uint32_t* tp, uint64_t ts, uint32_t k, uint32_t* out_idx,
-                     uint32_t* out_cnt, void* stream) {
-    if (!rec || !tp || !out_idx || !out_cnt || k == 0 || k > DHTGPU_MAX_K || lists == 0 || k_in == 0)
+                     uint32_t* out_cnt, uint32_t* ties, uint32_t tie_cap, void* stream) {
+    if (!rec || !tp || !out_idx || !out_cnt || k == 0 || k > DHTGPU_MAX_K || lists == 0 || k_in == 0 ||
+        k_in > DHTGPU_MAX_K)
         return DHTGPU_EINVAL;
-    if ((size_t)lists * k_in * 24 > 160 * 1024) return DHTGPU_ERANGE;
+    if (lists > DHTGPU_MAX_LISTS) return DHTGPU_ERANGE;
+    if (lists > 1 && !ties) return DHTGPU_EINVAL;   // cross-list ties must be listed
     if (!q) return DHTGPU_OK;
-    DHT_TRY(launch_merge(rec, lists, q, k_in, tp, ts, k, out_idx, out_cnt, (hipStream_t)stream));
+    DHT_TRY(launch_merge3(rec, lists, q, k_in, tp, ts, k, out_idx, out_cnt, ties, tie_cap, (hipStream_t)stream));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_tie_words_dev(dhtgpu_ctx* c, const uint32_t* rec, uint32_t q, uint32_t k, uint32_t idx_base,
+                         const uint32_t* ties, uint32_t tie_cap, uint32_t row_base, uint32_t* out_words,
+                         void* stream) {
+    if (!c || !rec || !out_words || k == 0 || k > DHTGPU_MAX_K) return DHTGPU_EINVAL;
+    if (!c->has_ids) return DHTGPU_ENOIDS;
+    if (!q) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    // records name ids by global index: the prefix shard's ascending map, else idx_base + local
+    const uint32_t* gmap = c->out_map();
+    DHT_TRY(launch_tie_words(rec, q, k, ties, tie_cap, row_base, c->planes.as<uint32_t>(), c->stride, c->n, gmap,
+                             gmap ? 0u : idx_base, out_words, s));
+    return DHTGPU_OK;
+}
+
+int dhtgpu_merge_ties_dev(const uint32_t* rec, const uint32_t* words, uint32_t lists, uint32_t q, uint32_t k_in,
+                          const uint32_t* tp, uint64_t ts, uint32_t k, const uint32_t* ties, uint32_t tie_cap,
+                          uint32_t* out_idx, uint32_t* out_cnt, void* stream) {
+    if (!rec || !words || !tp || !out_idx || !out_cnt || k == 0 || k > DHTGPU_MAX_K || lists == 0 || k_in == 0 ||
+        k_in > DHTGPU_MAX_K)
+        return DHTGPU_EINVAL;
+    if (lists > DHTGPU_MAX_LISTS) return DHTGPU_ERANGE;
+    if (!q || (ties && !tie_cap)) return DHTGPU_OK;
+    DHT_TRY(launch_merge_full(rec, words, lists, q, k_in, tp, ts, k, ties, tie_cap, out_idx, out_cnt,
+                              (hipStream_t)stream));
     return DHTGPU_OK;
 }
 
@@ -561,8 +570,7 @@ int dhtgpu_index_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     DHT_TRY(launch_index_query(c->index.p, c->n, c->index_B, c->planes.as<uint32_t>(), c->stride, tp, ts, q, k,
                                li, lc, s));
     if (out_rec)
-        DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
-                                    out_rec, s, rec_aos(c, s)));
+        DHT_TRY(launch_rec3(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx, out_rec, s));
     else
         DHT_TRY(launch_map_idx(li, (uint64_t)q * k, gidx, idx_base, s));
     return DHTGPU_OK;
@@ -754,8 +762,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     r = batch_slot_run(c, si, bc, s, ev);
     if (r) return r;
     if (out_rec) {
-        DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, c->out_map(),
-                                    out_rec, s, rec_aos(c, s)));
+        DHT_TRY(launch_rec3(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, c->out_map(), out_rec, s));
     } else if (!global && idx_base) {
         DHT_TRY(launch_map_idx(out_idx, (uint64_t)q * k, nullptr, idx_base, s));
     }
@@ -813,8 +820,7 @@ static int small_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     b.last = s;
     c->last_small = true;
     if (out_rec)
-        DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
-                                    out_rec, s, rec_aos(c, s)));
+        DHT_TRY(launch_rec3(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx, out_rec, s));
     return DHTGPU_OK;
 }
 
@@ -868,8 +874,7 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     int r = batch_slot_run(c, si, bc, s, ev);
     if (r) return r;
     if (out_rec)
-        DHT_TRY(launch_rec_from_idx(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx,
-                                    out_rec, s, rec_aos(c, s)));
+        DHT_TRY(launch_rec3(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx, out_rec, s));
     return DHTGPU_OK;
 }
 

@@ -60,7 +60,8 @@ struct ScanPlan {
 // splits are capped so that K3 can stage splits * k records (24 B) of a target in LDS
 ScanPlan plan_scan(uint64_t n, uint32_t q, uint32_t k, int num_cus);
 // final form: out_idx/out_cnt mapped through gidx (nullable) or offset by idx_base;
-// record form (out_rec != nullptr): rec[((split * q) + qi) * k + r] * 6, idx offset by idx_base
+// split record form (out_rec != nullptr, internal to the K1 split merge): full 24-B records
+// rec[((split * q) + qi) * k + r] * 6 = {w0..w4, idx + idx_base}
 hipError_t launch_scan(const uint32_t* ids, uint64_t is, uint64_t n, const ScanPlan& p,
                        const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k,
                        uint32_t* out_idx, uint32_t* out_cnt, uint32_t* out_rec,
@@ -71,14 +72,25 @@ hipError_t launch_merge(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_
 
 // valid idx[i] -> gidx ? gidx[idx[i]] : idx[i] + base
 hipError_t launch_map_idx(uint32_t* idx, uint64_t m, const uint32_t* gidx, uint32_t base, hipStream_t s);
-// rec[i] = {words of id idx[i], global index} (DHT_NONE record for DHT_NONE); the global
-// index is gidx[idx[i]] when gidx != nullptr, else idx[i] + base
-// aos (nullable): the set as 24-B records (launch_pack_aos), one read per candidate
-hipError_t launch_rec_from_idx(const uint32_t* idx, uint64_t m, const uint32_t* planes,
-                               uint64_t stride, uint32_t base, const uint32_t* gidx, uint32_t* rec,
-                               hipStream_t s, const uint32_t* aos = nullptr);
-// aos[i * 6 + w] = word w of id i (w < 5), aos[i * 6 + 5] = 0
-hipError_t launch_pack_aos(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t* aos, hipStream_t s);
+// compact candidate records (the public record form): rec[i * 3 ..] = {w0, w1, global index} of
+// local index idx[i] (all DHT_NONE for DHT_NONE); the global index is gidx[idx[i]] when gidx !=
+// nullptr, else idx[i] + base
+hipError_t launch_rec3(const uint32_t* idx, uint64_t m, const uint32_t* planes, uint64_t stride, uint32_t base,
+                       const uint32_t* gidx, uint32_t* rec, hipStream_t s);
+// K3 over compact records (lists <= 64, kin <= 32): rows whose candidates tie on their first 64
+// bits across lists are appended to ties = {count, rows[tie_cap]} (zeroed here; nullable)
+hipError_t launch_merge3(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_t kin, const uint32_t* tp,
+                         uint64_t ts, uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, uint32_t* ties,
+                         uint32_t tie_cap, hipStream_t s);
+// words 2..4 of this set's candidates (rec: its own compact records, q x k) in the listed rows
+// (+ row_base) or every row (ties == nullptr); gmap (nullable, ascending) maps global -> local
+hipError_t launch_tie_words(const uint32_t* rec, uint32_t q, uint32_t k, const uint32_t* ties, uint32_t tie_cap,
+                            uint32_t row_base, const uint32_t* planes, uint64_t stride, uint64_t n,
+                            const uint32_t* gmap, uint32_t base, uint32_t* words, hipStream_t s);
+// the listed rows (every row when ties == nullptr) merged again on the full keys
+hipError_t launch_merge_full(const uint32_t* rec, const uint32_t* words, uint32_t lists, uint32_t q, uint32_t kin,
+                             const uint32_t* tp, uint64_t ts, uint32_t k, const uint32_t* ties, uint32_t tie_cap,
+                             uint32_t* out_idx, uint32_t* out_cnt, hipStream_t s);
 
 // table.hip
 hipError_t launch_find_closest(uint32_t nb, const uint32_t* fp, const uint32_t* off,

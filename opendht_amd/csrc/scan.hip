@@ -129,17 +129,21 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_heads(const uint32_t* _
         for (uint32_t o = 1; o < G; o <<= 1) {
             const uint32_t p0 = (uint32_t)__shfl_xor((int)m0, (int)o), p1 = (uint32_t)__shfl_xor((int)m1, (int)o);
             const uint32_t pi = (uint32_t)__shfl_xor((int)mi, (int)o);
-            tie = tie || (p0 == m0 && p1 == m1 && pi != mi && pi != DHT_NONE && mi != DHT_NONE);
+            // two lists' heads agree on both distance words (the same index or not: lists built
+            // with colliding indices must not be taken for duplicates without the full key)
+            tie = tie || (p0 == m0 && p1 == m1 && pi != DHT_NONE && mi != DHT_NONE);
             const bool less = p0 < m0 || (p0 == m0 && (p1 < m1 || (p1 == m1 && pi < mi)));
             if (less) { m0 = p0; m1 = p1; mi = pi; }
         }
         const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (g * G);
+        bool adv = h0 == m0 && h1 == m1 && hi == mi;
         if (__ballot(tie) & gmask) {
-            // both distances tie between different ids: the group minimum by the full key
-            uint32_t f[DHT_W + 1];
-            f[0] = h0; f[1] = h1; f[DHT_W] = hi;
+            // the group minimum by the full key (words 2..4 from the records), then by index
+            uint32_t f[DHT_W + 1], own[DHT_W + 1];
+            own[0] = h0; own[1] = h1; own[DHT_W] = hi;
             for (int w = 2; w < DHT_W; ++w)
-                f[w] = hi == DHT_NONE ? DHT_NONE : src[p * 6 + w] ^ tp[(uint64_t)w * ts + qc];
+                own[w] = hi == DHT_NONE ? DHT_NONE : src[p * 6 + w] ^ tp[(uint64_t)w * ts + qc];
+            for (int w = 0; w <= DHT_W; ++w) f[w] = own[w];
 #pragma unroll
             for (uint32_t o = 1; o < G; o <<= 1) {
                 uint32_t pf[DHT_W + 1];
@@ -152,11 +156,13 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_heads(const uint32_t* _
                     for (int w = 0; w <= DHT_W; ++w) f[w] = pf[w];
             }
             m0 = f[0]; m1 = f[1]; mi = f[DHT_W];
+            adv = true;   // advance every list whose head IS the winner: the same id and index
+            for (int w = 0; w <= DHT_W; ++w) adv = adv && own[w] == f[w];
         }
         if (mi == DHT_NONE) continue;   // this target's lists are exhausted (group-uniform)
         if (tv && j == 0) out_idx[(uint64_t)qi * k + r] = mi;
         ++cnt;
-        if (hi == mi && lv) {   // the winning list advances (global indices are distinct across lists)
+        if (adv && lv) {   // the winning list advances (and every list holding the same record)
             ++p;
             if (p < kin) { h0 = my[3 * p]; h1 = my[3 * p + 1]; hi = my[3 * p + 2]; }
             else { h0 = DHT_NONE; h1 = DHT_NONE; hi = DHT_NONE; }
@@ -174,42 +180,180 @@ __global__ __launch_bounds__(256) void k_map_idx(uint32_t* __restrict__ idx, uin
     if (i < m && idx[i] != DHT_NONE) idx[i] = gidx ? gidx[idx[i]] : idx[i] + base;
 }
 
-// candidate records {w0..w4, global idx} of local indices.  aos (nullable): the set's ids as 24-B
-// records (k_pack_aos), one 24-B read per candidate instead of five 4-B reads from the planes
-// (each its own 64-B sector: the planes gather of 65,536 x 8 records took 62 us on a 2^24 set)
-__global__ __launch_bounds__(256) void k_rec_from_idx(const uint32_t* __restrict__ idx, uint64_t m,
-                                                      const uint32_t* __restrict__ planes,
-                                                      uint64_t stride, uint32_t base,
-                                                      const uint32_t* __restrict__ gidx,
-                                                      const uint2* __restrict__ aos,
-                                                      uint32_t* __restrict__ rec) {
+// ---- compact candidate records (the public record form, include/dhtgpu.h) --------------------
+// rec[i] = {w0, w1, global idx} of local index idx[i] (12 B; all DHT_NONE for an empty slot): two
+// 4-B reads per candidate from the w0 / w1 planes, which a cfg-2-sized set keeps in the Infinity
+// Cache (the 24-B form's words 2..4 came from a 400 MB copy of the set, i.e. from HBM: 17 us per
+// 65,536 x 8 records).  The global index is gidx[x] (nullable map) or x + base.
+__global__ __launch_bounds__(256) void k_rec3(const uint32_t* __restrict__ idx, uint64_t m,
+                                              const uint32_t* __restrict__ planes, uint64_t stride, uint32_t base,
+                                              const uint32_t* __restrict__ gidx, uint32_t* __restrict__ rec) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= m) return;
     const uint32_t x = idx[i];
     const bool none = x == DHT_NONE;
-    uint2* out = reinterpret_cast<uint2*>(rec + i * 6);
-    if (aos) {
-        const uint2* a = aos + (uint64_t)(none ? 0u : x) * 3;
-        const uint2 r0 = a[0], r1 = a[1], r2 = a[2];
-        out[0] = none ? make_uint2(DHT_NONE, DHT_NONE) : r0;
-        out[1] = none ? make_uint2(DHT_NONE, DHT_NONE) : r1;
-        out[2] = make_uint2(none ? DHT_NONE : r2.x, none ? DHT_NONE : (gidx ? gidx[x] : x + base));
-        return;
-    }
-#pragma unroll
-    for (int w = 0; w < DHT_W; ++w) rec[i * 6 + w] = none ? DHT_NONE : planes[(uint64_t)w * stride + x];
-    rec[i * 6 + 5] = none ? DHT_NONE : (gidx ? gidx[x] : x + base);
+    const uint32_t xc = none ? 0u : x;
+    const uint32_t w0 = planes[xc], w1 = planes[stride + xc];
+    rec[i * 3] = none ? DHT_NONE : w0;
+    rec[i * 3 + 1] = none ? DHT_NONE : w1;
+    rec[i * 3 + 2] = none ? DHT_NONE : (gidx ? gidx[xc] : x + base);
 }
 
-// the id set as 24-B records {w0..w4, 0} (built once per set for record-mode calls)
-__global__ __launch_bounds__(256) void k_pack_aos(const uint32_t* __restrict__ planes, uint64_t stride, uint64_t n,
-                                                  uint2* __restrict__ aos) {
+// K3 over compact records: the heads merge of k_merge_heads on (w0 ^ t0, w1 ^ t1, idx).  When two
+// lists' heads agree on both distance words -- two different ids sharing their first 64 bits, or
+// the same id sent by two lists -- the records cannot order them: the row's answer (ordered by
+// index there) is provisional, and the row is appended to ties = {count, rows[cap]} (nullable when
+// lists == 1: one list is already in order) for the second exchange (words 2..4) and
+// k_merge_full.  Hash-distributed ids never share 64 bits among one target's candidates.
+template <uint32_t G>
+__global__ __launch_bounds__(kMergeThreads) void k_merge3(const uint32_t* __restrict__ rec, uint32_t lists, uint32_t q,
+                                                          uint32_t kin, const uint32_t* __restrict__ tp, uint64_t ts,
+                                                          uint32_t k, uint32_t* __restrict__ out_idx,
+                                                          uint32_t* __restrict__ out_cnt, uint32_t* __restrict__ ties,
+                                                          uint32_t tie_cap) {
+    extern __shared__ uint32_t sm[];   // [thread][kin][3]
+    constexpr uint32_t TPW = 64 / G;
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t g = lane / G, j = lane % G;
+    const uint32_t qi = (blockIdx.x * (kMergeThreads / 64) + wv) * TPW + g;
+    const bool tv = qi < q, lv = tv && j < lists;
+    const uint32_t qc = tv ? qi : 0u;
+    const uint32_t t0 = tp[qc], t1 = tp[ts + qc];
+    uint32_t* my = sm + threadIdx.x * kin * 3;
+    const uint32_t* src = rec + ((uint64_t)(lv ? j : 0u) * q + qc) * kin * 3;
+    for (uint32_t r = 0; r < kin; ++r) {
+        const uint32_t a = src[r * 3], b = src[r * 3 + 1], ix = lv ? src[r * 3 + 2] : DHT_NONE;
+        const bool none = ix == DHT_NONE;
+        my[3 * r] = none ? DHT_NONE : a ^ t0;
+        my[3 * r + 1] = none ? DHT_NONE : b ^ t1;
+        my[3 * r + 2] = ix;
+    }
+    const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (g * G);
+    uint32_t p = 0, cnt = 0;
+    uint32_t h0 = my[0], h1 = my[1], hi = my[2];
+    bool row_tie = false;
+    for (uint32_t r = 0; r < k; ++r) {   // wave-uniform
+        uint32_t m0 = h0, m1 = h1, mi = hi;
+        bool tie = false;
+#pragma unroll
+        for (uint32_t o = 1; o < G; o <<= 1) {
+            const uint32_t p0 = (uint32_t)__shfl_xor((int)m0, (int)o), p1 = (uint32_t)__shfl_xor((int)m1, (int)o);
+            const uint32_t pi = (uint32_t)__shfl_xor((int)mi, (int)o);
+            tie = tie || (p0 == m0 && p1 == m1 && pi != DHT_NONE && mi != DHT_NONE);
+            const bool less = p0 < m0 || (p0 == m0 && (p1 < m1 || (p1 == m1 && pi < mi)));
+            if (less) { m0 = p0; m1 = p1; mi = pi; }
+        }
+        row_tie = row_tie || (__ballot(tie) & gmask) != 0;
+        if (mi == DHT_NONE) continue;   // this target's lists are exhausted (group-uniform)
+        if (tv && j == 0) out_idx[(uint64_t)qi * k + r] = mi;
+        ++cnt;
+        if (lv && h0 == m0 && h1 == m1 && hi == mi) {
+            ++p;
+            if (p < kin) { h0 = my[3 * p]; h1 = my[3 * p + 1]; hi = my[3 * p + 2]; }
+            else { h0 = DHT_NONE; h1 = DHT_NONE; hi = DHT_NONE; }
+        }
+    }
+    if (tv && j == 0) {
+        for (uint32_t r = cnt; r < k; ++r) out_idx[(uint64_t)qi * k + r] = DHT_NONE;
+        out_cnt[qi] = cnt;
+        if (row_tie && ties) {
+            const uint32_t s = atomicAdd(ties, 1u);
+            if (s < tie_cap) ties[1 + s] = qi;
+        }
+    }
+}
+
+// words 2..4 of this rank's candidates in the rows listed by ties = {count, rows[cap]} (rows offset
+// by row_base: an all-to-all slice), or of every row when ties == nullptr: words[(slot * k + r) * 3
+// + {0, 1, 2}].  A record's global index maps back to the set's local index through the sorted
+// index map gmap (prefix shards; nullable) or by subtracting base.
+__global__ __launch_bounds__(256) void k_tie_words(const uint32_t* __restrict__ rec, uint32_t q, uint32_t k,
+                                                   const uint32_t* __restrict__ ties, uint32_t tie_cap,
+                                                   uint32_t row_base, const uint32_t* __restrict__ planes,
+                                                   uint64_t stride, uint64_t n, const uint32_t* __restrict__ gmap,
+                                                   uint32_t base, uint32_t* __restrict__ words) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    uint2* o = aos + i * 3;
-    o[0] = make_uint2(planes[i], planes[stride + i]);
-    o[1] = make_uint2(planes[2 * stride + i], planes[3 * stride + i]);
-    o[2] = make_uint2(planes[4 * stride + i], 0u);
+    const uint64_t slot = i / k, r = i % k;
+    const uint64_t nrows = ties ? (ties[0] < tie_cap ? ties[0] : tie_cap) : q;
+    if (slot >= nrows) return;
+    const uint64_t row = ties ? (uint64_t)ties[1 + slot] + row_base : slot;
+    const uint32_t gi = row < q ? rec[(row * k + r) * 3 + 2] : DHT_NONE;
+    uint32_t* o = words + (slot * k + r) * 3;
+    uint64_t x = n;
+    if (gi != DHT_NONE) {
+        if (gmap) {   // lower_bound in the ascending map
+            uint64_t lo = 0, hi = n;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (gmap[mid] < gi) lo = mid + 1; else hi = mid;
+            }
+            x = lo < n && gmap[lo] == gi ? lo : n;
+        } else if (gi >= base) {
+            x = gi - base;
+        }
+    }
+    const bool ok = x < n;
+#pragma unroll
+    for (int w = 0; w < 3; ++w) o[w] = ok ? planes[(uint64_t)(2 + w) * stride + x] : DHT_NONE;
+}
+
+// The listed rows (or every row when ties == nullptr) merged again by the full key: list j's
+// candidate r of the row is {rec: w0, w1, idx} + {words: w2, w3, w4} (words rows: the tie slots,
+// wrows per list), each list already ascending by the full distance.  Lanes whose head equals the
+// winner in all five words and the index advance together (the same id sent twice); different ids
+// with colliding indices are both kept, ordered by distance.
+template <uint32_t G>
+__global__ __launch_bounds__(256) void k_merge_full(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ words,
+                                                    uint32_t lists, uint32_t q, uint32_t kin, uint32_t wrows,
+                                                    const uint32_t* __restrict__ tp, uint64_t ts, uint32_t k,
+                                                    const uint32_t* __restrict__ ties, uint32_t tie_cap,
+                                                    uint32_t* __restrict__ out_idx, uint32_t* __restrict__ out_cnt) {
+    constexpr uint32_t TPW = 64 / G;
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t g = lane / G, j = lane % G;
+    const uint32_t slot = (blockIdx.x * 4 + wv) * TPW + g;
+    const uint32_t nrows = ties ? (ties[0] < tie_cap ? ties[0] : tie_cap) : q;
+    const bool tv = slot < nrows;
+    const uint32_t row = tv ? (ties ? ties[1 + slot] : slot) : 0u;
+    const bool lv = tv && j < lists && row < q;
+    uint32_t t[DHT_W];
+    for (int w = 0; w < DHT_W; ++w) t[w] = tp[(uint64_t)w * ts + row];
+    auto head = [&](uint32_t p, uint32_t* f) {
+        const bool in = lv && p < kin;   // every address below stays inside the buffers
+        const uint64_t jc = in ? j : 0u, rc = in ? row : 0u, sc = in ? slot : 0u, pc = in ? p : 0u;
+        const uint32_t* r3 = rec + ((jc * q + rc) * kin + pc) * 3;
+        const uint32_t* w3 = words + ((jc * wrows + sc) * kin + pc) * 3;
+        uint32_t v[DHT_W + 1] = {r3[0], r3[1], w3[0], w3[1], w3[2], r3[2]};
+        const bool none = !in || v[DHT_W] == DHT_NONE;
+        for (int w = 0; w < DHT_W; ++w) f[w] = none ? DHT_NONE : v[w] ^ t[w];
+        f[DHT_W] = none ? DHT_NONE : v[DHT_W];
+    };
+    uint32_t h[DHT_W + 1], p = 0, cnt = 0;
+    head(0, h);
+    for (uint32_t r = 0; r < k; ++r) {
+        uint32_t f[DHT_W + 1];
+        for (int w = 0; w <= DHT_W; ++w) f[w] = h[w];
+#pragma unroll
+        for (uint32_t o = 1; o < G; o <<= 1) {
+            uint32_t pf[DHT_W + 1];
+            for (int w = 0; w <= DHT_W; ++w) pf[w] = (uint32_t)__shfl_xor((int)f[w], (int)o);
+            bool less = false, decided = false;
+            for (int w = 0; w <= DHT_W; ++w)
+                if (!decided && pf[w] != f[w]) { less = pf[w] < f[w]; decided = true; }
+            if (less)
+                for (int w = 0; w <= DHT_W; ++w) f[w] = pf[w];
+        }
+        if (f[DHT_W] == DHT_NONE) continue;   // group-uniform
+        if (tv && j == 0) out_idx[(uint64_t)row * k + r] = f[DHT_W];
+        ++cnt;
+        bool adv = lv;
+        for (int w = 0; w <= DHT_W; ++w) adv = adv && h[w] == f[w];
+        if (adv) head(++p, h);
+    }
+    if (tv && j == 0) {
+        for (uint32_t r = cnt; r < k; ++r) out_idx[(uint64_t)row * k + r] = DHT_NONE;
+        out_cnt[row] = cnt;
+    }
 }
 
 template <uint32_t K>
@@ -260,18 +404,80 @@ hipError_t launch_map_idx(uint32_t* idx, uint64_t m, const uint32_t* gidx, uint3
     return hipGetLastError();
 }
 
-hipError_t launch_rec_from_idx(const uint32_t* idx, uint64_t m, const uint32_t* planes,
-                               uint64_t stride, uint32_t base, const uint32_t* gidx, uint32_t* rec,
-                               hipStream_t s, const uint32_t* aos) {
+hipError_t launch_rec3(const uint32_t* idx, uint64_t m, const uint32_t* planes, uint64_t stride, uint32_t base,
+                       const uint32_t* gidx, uint32_t* rec, hipStream_t s) {
     if (!m) return hipSuccess;
-    k_rec_from_idx<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(idx, m, planes, stride, base, gidx,
-                                                               reinterpret_cast<const uint2*>(aos), rec);
+    k_rec3<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(idx, m, planes, stride, base, gidx, rec);
     return hipGetLastError();
 }
 
-hipError_t launch_pack_aos(const uint32_t* planes, uint64_t stride, uint64_t n, uint32_t* aos, hipStream_t s) {
-    if (!n) return hipSuccess;
-    k_pack_aos<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(planes, stride, n, reinterpret_cast<uint2*>(aos));
+hipError_t launch_merge3(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_t kin, const uint32_t* tp,
+                         uint64_t ts, uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, uint32_t* ties,
+                         uint32_t tie_cap, hipStream_t s) {
+    if (lists > 64 || kin > 32) return hipErrorInvalidValue;
+    uint32_t G = 1;
+    while (G < lists) G <<= 1;
+    const uint32_t tpb = (kMergeThreads / 64) * (64 / G);
+    const dim3 grid((q + tpb - 1) / tpb), blk(kMergeThreads);
+    const size_t lds = (size_t)kMergeThreads * kin * 3 * sizeof(uint32_t);
+    static std::once_flag once[kMaxDevices];
+    const hipError_t e = per_device_once(once, [] {
+        const void* fs[] = {(const void*)k_merge3<1>, (const void*)k_merge3<2>, (const void*)k_merge3<4>,
+                            (const void*)k_merge3<8>, (const void*)k_merge3<16>, (const void*)k_merge3<32>,
+                            (const void*)k_merge3<64>};
+        for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    });
+    if (e != hipSuccess) return e;
+    if (ties) {   // the tie count starts at zero for every merge
+        const hipError_t z = hipMemsetAsync(ties, 0, sizeof(uint32_t), s);
+        if (z != hipSuccess) return z;
+    }
+#define DHT_M3(GG) k_merge3<GG><<<grid, blk, lds, s>>>(rec, lists, q, kin, tp, ts, k, out_idx, out_cnt, ties, tie_cap)
+    switch (G) {
+        case 1: DHT_M3(1); break;
+        case 2: DHT_M3(2); break;
+        case 4: DHT_M3(4); break;
+        case 8: DHT_M3(8); break;
+        case 16: DHT_M3(16); break;
+        case 32: DHT_M3(32); break;
+        default: DHT_M3(64); break;
+    }
+#undef DHT_M3
+    return hipGetLastError();
+}
+
+hipError_t launch_tie_words(const uint32_t* rec, uint32_t q, uint32_t k, const uint32_t* ties, uint32_t tie_cap,
+                            uint32_t row_base, const uint32_t* planes, uint64_t stride, uint64_t n,
+                            const uint32_t* gmap, uint32_t base, uint32_t* words, hipStream_t s) {
+    const uint64_t m = (uint64_t)(ties ? tie_cap : q) * k;
+    if (!m) return hipSuccess;
+    k_tie_words<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(rec, q, k, ties, tie_cap, row_base, planes, stride, n,
+                                                            gmap, base, words);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_full(const uint32_t* rec, const uint32_t* words, uint32_t lists, uint32_t q, uint32_t kin,
+                             const uint32_t* tp, uint64_t ts, uint32_t k, const uint32_t* ties, uint32_t tie_cap,
+                             uint32_t* out_idx, uint32_t* out_cnt, hipStream_t s) {
+    if (lists > 64 || kin > 32) return hipErrorInvalidValue;
+    uint32_t G = 1;
+    while (G < lists) G <<= 1;
+    const uint32_t rows = ties ? tie_cap : q, wrows = rows;
+    if (!rows) return hipSuccess;
+    const uint32_t tpb = 4 * (64 / G);
+    const dim3 grid((rows + tpb - 1) / tpb), blk(256);
+#define DHT_MF(GG) k_merge_full<GG><<<grid, blk, 0, s>>>(rec, words, lists, q, kin, wrows, tp, ts, k, ties, tie_cap, \
+                                                         out_idx, out_cnt)
+    switch (G) {
+        case 1: DHT_MF(1); break;
+        case 2: DHT_MF(2); break;
+        case 4: DHT_MF(4); break;
+        case 8: DHT_MF(8); break;
+        case 16: DHT_MF(16); break;
+        case 32: DHT_MF(32); break;
+        default: DHT_MF(64); break;
+    }
+#undef DHT_MF
     return hipGetLastError();
 }
 

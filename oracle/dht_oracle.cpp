@@ -207,6 +207,70 @@ void orc_topk(const uint8_t* ids20, uint64_t n, const uint8_t* targets20, uint32
     });
 }
 
+/* The same top-k (std::partial_sort under xorCmp, equal ids by lower index) over the id stream
+ * [start, start + n) of orc_gen_ids, generated on the fly: no 20-byte array of the whole set is
+ * held (BASELINE cfg 3: 10^9 ids = 20 GB).  Threads take contiguous index ranges and keep, per
+ * target, the k smallest (distance, index) pairs of their range in a sorted array; the per-thread
+ * lists are then merged.  The 160-bit big-endian distance id ^ t compares as the word triple
+ * (bytes 0..7, 8..15, 16..19), which is xorCmp's order (include/opendht/infohash.h:179-194: at the
+ * first byte where two ids differ, the one whose byte XOR t is smaller is closer).  out_idx holds
+ * stream indices (start + i); start + n <= 2^32. */
+void orc_topk_gen(uint64_t seed, uint64_t start, uint64_t n, const uint8_t* targets20, uint32_t q, uint32_t k,
+                  uint32_t* out_idx, uint32_t* out_cnt, int threads) {
+    struct Cand { uint64_t d0, d1; uint32_t d2, idx; };
+    auto less = [](const Cand& a, const Cand& b) {
+        if (a.d0 != b.d0) return a.d0 < b.d0;
+        if (a.d1 != b.d1) return a.d1 < b.d1;
+        if (a.d2 != b.d2) return a.d2 < b.d2;
+        return a.idx < b.idx;
+    };
+    auto be = [](const uint8_t* p, unsigned nb) {
+        uint64_t v = 0;
+        for (unsigned i = 0; i < nb; i++) v = v << 8 | p[i];
+        return v;
+    };
+    std::vector<uint64_t> t0(q), t1(q), t2(q);
+    for (uint32_t j = 0; j < q; j++) {
+        t0[j] = be(targets20 + 20ull * j, 8);
+        t1[j] = be(targets20 + 20ull * j + 8, 8);
+        t2[j] = be(targets20 + 20ull * j + 16, 4);
+    }
+    if (threads < 1) threads = 1;
+    const uint64_t kk = std::min<uint64_t>(k, n);
+    std::vector<std::vector<Cand>> part((size_t)threads * q);
+    parallel_for((uint64_t)threads, threads, [&](uint64_t th) {
+        const uint64_t lo = n * th / threads, hi = n * (th + 1) / threads;
+        std::vector<Cand>* lists = part.data() + th * q;
+        for (uint32_t j = 0; j < q; j++) lists[j].reserve(kk + 1);
+        std::vector<uint64_t> kth(q, ~0ull);   /* d0 of the list's k-th entry: a cheap reject */
+        for (uint64_t i = lo; i < hi; i++) {
+            const uint64_t g = start + i;
+            const uint64_t x0 = splitmix(seed, 3 * g), x1 = splitmix(seed, 3 * g + 1);
+            const uint32_t x2 = (uint32_t)(splitmix(seed, 3 * g + 2) >> 32);   /* top 4 bytes (orc_gen_ids) */
+            for (uint32_t j = 0; j < q; j++) {
+                const uint64_t d0 = x0 ^ t0[j];
+                if (d0 > kth[j]) continue;
+                const Cand c{d0, x1 ^ t1[j], x2 ^ (uint32_t)t2[j], (uint32_t)g};
+                std::vector<Cand>& L = lists[j];
+                if (L.size() == kk && !less(c, L.back())) continue;
+                L.insert(std::upper_bound(L.begin(), L.end(), c, less), c);
+                if (L.size() > kk) L.pop_back();
+                if (L.size() == kk) kth[j] = L.back().d0;
+            }
+        }
+    });
+    for (uint32_t j = 0; j < q; j++) {
+        std::vector<Cand> all;
+        for (int th = 0; th < threads; th++) {
+            const std::vector<Cand>& L = part[(size_t)th * q + j];
+            all.insert(all.end(), L.begin(), L.end());
+        }
+        std::sort(all.begin(), all.end(), less);
+        for (uint32_t i = 0; i < k; i++) out_idx[(uint64_t)j * k + i] = i < kk ? all[i].idx : 0xFFFFFFFFu;
+        out_cnt[j] = (uint32_t)kk;
+    }
+}
+
 orc_table* orc_table_new(const uint8_t* myid20, int is_client) {
     auto* t = new orc_table;
     t->myid = load(myid20);

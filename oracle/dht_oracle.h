@@ -42,6 +42,11 @@ int orc_cmp(const uint8_t* a, const uint8_t* b);                              /*
 void orc_topk(const uint8_t* ids20, uint64_t n, const uint8_t* targets20, uint32_t q,
               uint32_t k, uint32_t* out_idx, uint32_t* out_cnt, int threads);
 
+/* orc_topk over the orc_gen_ids stream [start, start+n) generated on the fly (no id array held:
+ * BASELINE cfg 3's 10^9 ids); out_idx are stream indices start + i (start + n <= 2^32). */
+void orc_topk_gen(uint64_t seed, uint64_t start, uint64_t n, const uint8_t* targets20, uint32_t q, uint32_t k,
+                  uint32_t* out_idx, uint32_t* out_cnt, int threads);
+
 /* RoutingTable growth by onNewNode (src/routing_table.cpp:204-262), used to make
  * realistic table shapes.  All nodes are good when inserted. */
 typedef struct orc_table orc_table;

@@ -68,6 +68,8 @@ def _load(path):
     L.orc_cmp.restype = ctypes.c_int
     L.orc_topk.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint32, ctypes.c_uint32,
                            u32p, u32p, ctypes.c_int]
+    L.orc_topk_gen.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u8p, ctypes.c_uint32,
+                               ctypes.c_uint32, u32p, u32p, ctypes.c_int]
     L.orc_table_new.argtypes = [u8p, ctypes.c_int]
     L.orc_table_new.restype = ctypes.c_void_p
     L.orc_table_free.argtypes = [ctypes.c_void_p]
@@ -148,6 +150,18 @@ def topk(ids, targets, k, threads=None):
     cnt = np.empty(q, dtype=np.uint32)
     lib().orc_topk(_p(ids, u8p), ids.shape[0], _p(targets, u8p), q, k, _p(out, u32p), _p(cnt, u32p),
                    int(threads or default_threads()))
+    return out, cnt
+
+
+def topk_gen(seed, n, targets, k, start=0, threads=None):
+    """topk() over the gen_ids(seed, n, start) stream generated on the fly (no id array: BASELINE
+    cfg 3's 10^9 ids); indices are stream indices start + i."""
+    targets = np.ascontiguousarray(targets, dtype=np.uint8)
+    q = targets.shape[0]
+    out = np.empty((q, k), dtype=np.uint32)
+    cnt = np.empty(q, dtype=np.uint32)
+    lib().orc_topk_gen(seed, start, n, _p(targets, u8p), q, k, _p(out, u32p), _p(cnt, u32p),
+                       int(threads or default_threads()))
     return out, cnt
 
 

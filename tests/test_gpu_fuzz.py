@@ -8,6 +8,7 @@ compared with std::partial_sort(xorCmp) over every target.  Marked gpu."""
 import numpy as np
 import pytest
 
+import merge_util as MU
 import oracle as O
 from test_gpu_parity import check_topk
 
@@ -179,7 +180,7 @@ def test_record_shards_merge_random(ctx, seed):
     torch.cuda.synchronize()
     assert L.dhtgpu_pack_dev(tb.data_ptr(), q, tp.data_ptr(), ts, None) == 0
     torch.cuda.synchronize()
-    rec = torch.empty((nsh, q, k, 6), dtype=torch.int32, device=dev)
+    rec = torch.empty((nsh, q, k, 3), dtype=torch.int32, device=dev)
     for s in range(nsh):
         c = opendht_amd.Context(0)
         c.set_ids(np.ascontiguousarray(ids[bounds[s]:bounds[s + 1]]))
@@ -187,14 +188,10 @@ def test_record_shards_merge_random(ctx, seed):
         fn(tp.data_ptr(), ts, q, k, None, None, rec[s].data_ptr(), bounds[s], c.stream)
         torch.cuda.synchronize()
         c.close()
-    out = torch.empty((q, k), dtype=torch.int32, device=dev)
-    cnt = torch.empty(q, dtype=torch.int32, device=dev)
-    assert L.dhtgpu_merge_dev(rec.data_ptr(), nsh, q, k, tp.data_ptr(), ts, k, out.data_ptr(), cnt.data_ptr(),
-                              None) == 0
-    torch.cuda.synchronize()
+    out, cnt, _ = MU.merge(L, rec, tp, ts, k, ("host", MU.host_words_fn(ids, rec.cpu().numpy().view(np.uint32))))
     want, wcnt = O.topk(ids, tg, k)
-    assert np.array_equal(cnt.cpu().numpy().view(np.uint32), wcnt), seed
-    assert np.array_equal(out.cpu().numpy().view(np.uint32), want), seed
+    assert np.array_equal(cnt, wcnt), seed
+    assert np.array_equal(out, want), seed
 
 
 @pytest.mark.parametrize("seed", range(4))

@@ -3,6 +3,7 @@ All calls go through the C ABI (ctypes).  Marked gpu: run on the MI355X box."""
 import numpy as np
 import pytest
 
+import merge_util as MU
 import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -377,7 +378,7 @@ def test_sharded_records_merge(ctx):
     L = opendht_amd.lib()
     assert L.dhtgpu_pack_dev(tb.data_ptr(), 500, tp.data_ptr(), ts, None) == 0
     bounds = [0, 7000, 19000, 30000]
-    rec = torch.empty((3, 500, k, 6), dtype=torch.int32, device=dev)
+    rec = torch.empty((3, 500, k, 3), dtype=torch.int32, device=dev)
     shards = []
     for s in range(3):
         c = opendht_amd.Context(0)
@@ -385,14 +386,15 @@ def test_sharded_records_merge(ctx):
         c.topk_dev(tp.data_ptr(), ts, 500, k, None, None, rec[s].data_ptr(), bounds[s], c.stream)
         torch.cuda.synchronize()
         shards.append(c)
-    out = torch.empty((500, k), dtype=torch.int32, device=dev)
-    cnt = torch.empty(500, dtype=torch.int32, device=dev)
-    assert L.dhtgpu_merge_dev(rec.data_ptr(), 3, 500, k, tp.data_ptr(), ts, k, out.data_ptr(), cnt.data_ptr(),
-                              None) == 0
-    torch.cuda.synchronize()
+    # the compact records are {w0, w1, global idx} of each shard's ascending top-k
+    words = ids.view(">u4").reshape(-1, 5).astype(np.uint32)
+    r0 = rec[1].cpu().numpy().view(np.uint32)
+    li, _ = O.topk(ids[7000:19000], tg, k)
+    assert np.array_equal(r0[..., 2], li + 7000) and np.array_equal(r0[..., :2], words[li + 7000, :2])
+    out, cnt, nties = MU.merge(L, rec, tp, ts, k, ("ctx", MU.ctx_words_fn(L, shards, rec, bounds, k)))
     want, wcnt = O.topk(ids, tg, k)
-    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
-    assert np.array_equal(cnt.cpu().numpy().view(np.uint32), wcnt)
+    assert nties == 0
+    assert np.array_equal(out, want) and np.array_equal(cnt, wcnt)
     for c in shards:
         c.close()
 
@@ -536,31 +538,15 @@ def test_batch_clustered_targets_and_fallback(ctx):
     check_topk(ctx, ids, tg[:100], 14)    # a different batch on the first set again
 
 
-def _shard_records(ids, bounds, tg, k):
-    """(lists, q, k, 6) records {w0..w4, global idx} of each id-range shard's exact top-k (the
-    oracle's, sorted ascending, NONE-padded like every producer in the library)"""
-    q = tg.shape[0]
-    words = ids.view(">u4").reshape(-1, 5).astype(np.uint32)
-    rec = np.full((len(bounds) - 1, q, k, 6), 0xFFFFFFFF, dtype=np.uint32)
-    for s in range(len(bounds) - 1):
-        lo, hi = bounds[s], bounds[s + 1]
-        if hi == lo:
-            continue
-        idx, cnt = O.topk(ids[lo:hi], tg, k)
-        for i in range(q):
-            c = int(cnt[i])
-            rec[s, i, :c, :5] = words[lo + idx[i, :c].astype(np.int64)]
-            rec[s, i, :c, 5] = idx[i, :c] + lo
-    return rec
-
-
-@pytest.mark.parametrize("lists,k,seed", [(1, 8, 1), (2, 8, 2), (3, 14, 3), (8, 8, 4), (8, 32, 5), (13, 1, 6),
-                                          (64, 8, 7), (65, 8, 8), (5, 32, 9)])
-def test_merge_heads_ties_duplicates(ctx, lists, k, seed):
-    """K3 (the k-way heads merge for <= 64 sorted lists, the pairwise rank past 64) over id-range
-    shards whose ids tie on their first 64 bits across shards (the heads' word-0 and word-1
-    distances tie: the five-word path), duplicated ids in different shards (global index
-    decides), shards shorter than k and empty shards == one flat top-k of all ids."""
+@pytest.mark.parametrize("lists,k,seed,cap", [(1, 8, 1, 256), (2, 8, 2, 256), (3, 14, 3, 256), (8, 8, 4, 256),
+                                              (8, 32, 5, 256), (13, 1, 6, 256), (64, 8, 7, 256), (5, 32, 9, 256),
+                                              (4, 8, 10, 4), (64, 3, 11, 16)])
+def test_merge_heads_ties_duplicates(ctx, lists, k, seed, cap):
+    """K3 over compact records of id-range shards whose ids tie on their first 64 bits across
+    shards (the records cannot order them: the rows are listed and settled by the second
+    exchange of words 2..4 -- cap 4 / 16: more tie rows than one exchange takes, so the every-row
+    settlement runs too), duplicated ids in different shards (global index decides), shards
+    shorter than k and empty shards == one flat top-k of all ids."""
     import torch
     import opendht_amd
     rng = np.random.default_rng(seed)
@@ -575,23 +561,71 @@ def test_merge_heads_ties_duplicates(ctx, lists, k, seed):
     if lists > 2:
         cuts[0] = cuts[1]                          # one empty shard
     bounds = [0] + [int(c) for c in cuts] + [n]
-    rec = _shard_records(ids, bounds, tg, k)
+    rec = MU.host_records(ids, bounds, tg, k, O)
     dev = torch.device("cuda", 0)
     ts = (q + 63) // 64 * 64
     tp = torch.zeros(5 * ts, dtype=torch.int32, device=dev)
     L = opendht_amd.lib()
     assert L.dhtgpu_pack_dev(torch.from_numpy(tg.reshape(-1)).to(dev).data_ptr(), q, tp.data_ptr(), ts, None) == 0
     rd = torch.from_numpy(rec.view(np.int32)).to(dev)
-    out = torch.empty((q, k), dtype=torch.int32, device=dev)
-    cnt = torch.empty(q, dtype=torch.int32, device=dev)
-    assert L.dhtgpu_merge_dev(rd.data_ptr(), lists, q, k, tp.data_ptr(), ts, k, out.data_ptr(), cnt.data_ptr(),
-                              None) == 0
-    torch.cuda.synchronize()
+    got, gcnt, nties = MU.merge(L, rd, tp, ts, k, ("host", MU.host_words_fn(ids, rec)), tie_cap=cap)
     want, wcnt = O.topk(ids, tg, k)
-    got = out.cpu().numpy().view(np.uint32)
-    assert np.array_equal(cnt.cpu().numpy().view(np.uint32), wcnt)
+    assert np.array_equal(gcnt, wcnt)
     bad = np.nonzero((got != want).any(axis=1))[0]
     assert bad.size == 0, f"{bad.size} targets differ, first {bad[:3]}: {got[bad[0]]} vs {want[bad[0]]}"
+    if lists > 1:
+        assert nties > 0, "the 64-bit cluster must produce tie rows"
+        if cap < 64:
+            assert nties > cap
+    if lists == 64:   # more lists than one merge takes
+        assert L.dhtgpu_merge_dev(rd.data_ptr(), 65, 1, k, tp.data_ptr(), ts, k, rd.data_ptr(), rd.data_ptr(),
+                                  rd.data_ptr(), cap, None) == opendht_amd.ERANGE
+
+
+def test_merge_colliding_indices(ctx):
+    """lists built with colliding index bases (every shard's records numbered from 0):
+    different ids that share an index are both kept, ordered by distance; the same id sent by two
+    lists under the same index is one candidate.  Checked against a host merge of (distance,
+    index) with exact duplicates removed."""
+    import torch
+    import opendht_amd
+    n, q, k = 3000, 200, 8
+    ids = O.gen_ids(808, n)
+    ids[1000:1040] = ids[0:40]                     # list 1's first 40 ids == list 0's (same local index)
+    ids[:20, :8] = ids[2000, :8]                   # and 64-bit prefix ties across lists
+    tg = O.gen_ids(809, q)
+    tg[:50, :8] = ids[2000, :8]
+    bounds = [0, 1000, 2000, 3000]
+    rec = MU.host_records(ids, bounds, tg, k, O)
+    for s in range(3):                             # local indices: every list counts from 0
+        m = rec[s, ..., 2] != MU.NONE
+        rec[s, ..., 2][m] -= bounds[s]
+    dev = torch.device("cuda", 0)
+    ts = (q + 63) // 64 * 64
+    tp = torch.zeros(5 * ts, dtype=torch.int32, device=dev)
+    L = opendht_amd.lib()
+    assert L.dhtgpu_pack_dev(torch.from_numpy(tg.reshape(-1)).to(dev).data_ptr(), q, tp.data_ptr(), ts, None) == 0
+    words = ids.view(">u4").reshape(-1, 5).astype(np.uint32)
+
+    def wfn(j, rows, out):
+        g = rec[j][rows][..., 2]
+        w = np.full(g.shape + (3,), MU.NONE, np.uint32)
+        ok = g != MU.NONE
+        w[ok] = words[g[ok].astype(np.int64) + bounds[j], 2:5]
+        return w
+    got, gcnt, nties = MU.merge(L, torch.from_numpy(rec.view(np.int32)).to(dev), tp, ts, k, ("host", wfn))
+    assert nties > 0
+    tw = tg.view(">u4").reshape(-1, 5).astype(np.uint32)
+    for i in range(q):
+        cand = set()
+        for s in range(3):
+            for r in range(k):
+                g = int(rec[s, i, r, 2])
+                if g != MU.NONE:
+                    cand.add(tuple(int(x) for x in (words[g + bounds[s]] ^ tw[i])) + (g,))
+        order = sorted(cand)[:k]
+        assert int(gcnt[i]) == len(order)
+        assert list(got[i, :len(order)]) == [c[-1] for c in order], i
 
 
 def test_batch_records_merge(ctx):
@@ -607,7 +641,7 @@ def test_batch_records_merge(ctx):
     L = opendht_amd.lib()
     assert L.dhtgpu_pack_dev(torch.from_numpy(tg.reshape(-1)).to(dev).data_ptr(), q, tp.data_ptr(), ts, None) == 0
     bounds = [0, 20000, 61000, 90000]
-    rec = torch.empty((3, q, k, 6), dtype=torch.int32, device=dev)
+    rec = torch.empty((3, q, k, 3), dtype=torch.int32, device=dev)
     shards = []
     for s in range(3):
         c = opendht_amd.Context(0)
@@ -615,14 +649,64 @@ def test_batch_records_merge(ctx):
         c.batch_topk_dev(tp.data_ptr(), ts, q, k, None, None, rec[s].data_ptr(), bounds[s], c.stream)
         torch.cuda.synchronize()
         shards.append(c)
-    out = torch.empty((q, k), dtype=torch.int32, device=dev)
-    cnt = torch.empty(q, dtype=torch.int32, device=dev)
-    assert L.dhtgpu_merge_dev(rec.data_ptr(), 3, q, k, tp.data_ptr(), ts, k, out.data_ptr(), cnt.data_ptr(),
-                              None) == 0
+    out, cnt, nties = MU.merge(L, rec, tp, ts, k, ("ctx", MU.ctx_words_fn(L, shards, rec, bounds, k)))
+    want, wcnt = O.topk(ids, tg, k)
+    assert nties == 0 and np.array_equal(out, want) and np.array_equal(cnt, wcnt)
+    for c in shards:
+        c.close()
+
+
+def test_batch_records_tie_words_from_contexts(ctx):
+    """The second exchange's payload from live shard contexts (dhtgpu_tie_words_dev: global index ->
+    the context's own planes; a prefix shard maps it back through its index map): K6 record mode
+    over 3 id-range shards and 2 prefix shards whose ids share their first 64 bits across shards,
+    K3 + tie exchange == one flat top-k (every row settled: cap 2)."""
+    import torch
+    import opendht_amd
+    n, q, k = 60000, 600, 8
+    ids = O.gen_ids(511, n)
+    ids[::3, :8] = ids[1, :8]                      # a third of the ids share 64 bits
+    tg = O.gen_ids(512, q)
+    tg[::2, :8] = ids[1, :8]
+    dev = torch.device("cuda", 0)
+    ts = (q + 63) // 64 * 64
+    tp = torch.zeros(5 * ts, dtype=torch.int32, device=dev)
+    L = opendht_amd.lib()
+    assert L.dhtgpu_pack_dev(torch.from_numpy(tg.reshape(-1)).to(dev).data_ptr(), q, tp.data_ptr(), ts, None) == 0
+    bounds = [0, 11000, 40000, n]
+    rec = torch.empty((3, q, k, 3), dtype=torch.int32, device=dev)
+    shards = []
+    for s in range(3):
+        c = opendht_amd.Context(0)
+        c.set_ids(ids[bounds[s]:bounds[s + 1]])
+        c.batch_topk_dev(tp.data_ptr(), ts, q, k, None, None, rec[s].data_ptr(), bounds[s], c.stream)
+        shards.append(c)
     torch.cuda.synchronize()
     want, wcnt = O.topk(ids, tg, k)
-    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
-    assert np.array_equal(cnt.cpu().numpy().view(np.uint32), wcnt)
+    for cap in (256, 2):
+        out, cnt, nties = MU.merge(L, rec, tp, ts, k, ("ctx", MU.ctx_words_fn(L, shards, rec, bounds, k)),
+                                   tie_cap=cap)
+        assert nties > 2 and np.array_equal(out, want) and np.array_equal(cnt, wcnt), cap
+    for c in shards:
+        c.close()
+    # prefix shards (global indices through the shard's index map) of the generated stream
+    n2 = 200000
+    ids2 = O.gen_ids(513, n2)
+    tg2 = O.gen_ids(514, q)
+    rec2 = torch.empty((2, q, k, 3), dtype=torch.int32, device=dev)
+    tp2 = torch.zeros(5 * ts, dtype=torch.int32, device=dev)
+    assert L.dhtgpu_pack_dev(torch.from_numpy(tg2.reshape(-1)).to(dev).data_ptr(), q, tp2.data_ptr(), ts, None) == 0
+    shards = []
+    for s in range(2):
+        c = opendht_amd.Context(0)
+        c.gen_ids_prefix(513, n2, 1, s)
+        c.batch_topk_dev(tp2.data_ptr(), ts, q, k, None, None, rec2[s].data_ptr(), 0, c.stream)
+        shards.append(c)
+    torch.cuda.synchronize()
+    out, cnt, _ = MU.merge(L, rec2, tp2, ts, k, ("ctx", MU.ctx_words_fn(L, shards, rec2, [0, 0], k)),
+                           force_all=True)
+    want, wcnt = O.topk(ids2, tg2, k)
+    assert np.array_equal(out, want) and np.array_equal(cnt, wcnt)
     for c in shards:
         c.close()
 

@@ -43,7 +43,8 @@ def test_cfg3_shard_2p27(ctx):
     bad = np.nonzero((got != sc).any(axis=1))[0]
     assert bad.size == 0, f"{bad.size} targets differ from the K1 scan, first {bad[:5]}"
     rows = sample_rows(q, 48)
-    want, wcnt = O.topk(O.gen_ids(777, n), tg[rows], k, threads=16)
+    ids = O.gen_ids(777, n)
+    want, wcnt = O.topk(ids, tg[rows], k, threads=16)
     assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
     # device form with candidate records, merged by K3 (the broadcast route's building block)
     dev = torch.device("cuda", 0)
@@ -51,16 +52,76 @@ def test_cfg3_shard_2p27(ctx):
     tp = torch.zeros(5 * ts, dtype=torch.int32, device=dev)
     L = opendht_amd.lib()
     tb = torch.from_numpy(tg.reshape(-1)).to(dev)
-    rec = torch.empty((q, k, 6), dtype=torch.int32, device=dev)
+    rec = torch.empty((q, k, 3), dtype=torch.int32, device=dev)
     out = torch.empty((q, k), dtype=torch.int32, device=dev)
     oc = torch.empty(q, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     s = ctx.stream   # every launch below on the context's stream (stream-ordered)
     assert L.dhtgpu_pack_dev(tb.data_ptr(), q, tp.data_ptr(), ts, s) == 0
     ctx.batch_topk_dev(tp.data_ptr(), ts, q, k, None, None, rec.data_ptr(), 0, s)
-    assert L.dhtgpu_merge_dev(rec.data_ptr(), 1, q, k, tp.data_ptr(), ts, k, out.data_ptr(), oc.data_ptr(), s) == 0
+    assert L.dhtgpu_merge_dev(rec.data_ptr(), 1, q, k, tp.data_ptr(), ts, k, out.data_ptr(), oc.data_ptr(), None, 0,
+                              s) == 0
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), got)
+    r = rec.cpu().numpy().view(np.uint32)
+    assert np.array_equal(r[..., 2], got)
+    w = ids[got[rows].astype(np.int64)].view(">u4").reshape(rows.size, k, 5)
+    assert np.array_equal(r[rows, :, :2], w[..., :2].astype(np.uint32))
+
+
+def test_cfg3_full_1e9_range_shards():
+    """BASELINE cfg 3 at its stated size: 10^9 ids as the 8 range shards of
+    sharding.shard_range(10^9, 8, r), each generated on its own context (one at a time: one GPU's
+    share), 2^20 targets.  Per shard: K6 in record form with idx_base = lo (the library splits each
+    1.25*10^8-id shard into 8 prefix sub-partitions); the 8 record lists concatenated exactly as the
+    all-gather delivers them; K3 with lists = 8.  Checks: every count is 8; no row ties on 64 bits
+    (hash ids; the tie exchange then settles nothing); the whole merged batch == one independent
+    exact route, a single sub-partitioned K6 over all 10^9 ids (64 prefix sub-partitions); 40
+    strided targets == std::partial_sort(xorCmp) over the 10^9-id stream (the generator-fed oracle:
+    no 20-GB host array).  Reference: include/opendht/infohash.h:179-194; SURVEY 8(e)."""
+    import torch
+    import opendht_amd
+    from opendht_amd import sharding
+    n, q, k, world, seed = 10**9, 1 << 20, 8, 8, 1010
+    L = opendht_amd.lib()
+    dev = torch.device("cuda", 0)
+    tg = O.gen_ids(1011, q)
+    ts = q
+    tp = torch.zeros(5 * ts, dtype=torch.int32, device=dev)
+    assert L.dhtgpu_pack_dev(torch.from_numpy(tg.reshape(-1)).to(dev).data_ptr(), q, tp.data_ptr(), ts, None) == 0
+    rec = torch.empty((world, q, k, 3), dtype=torch.int32, device=dev)
+    t0 = time.perf_counter()
+    with opendht_amd.Context(0) as c:
+        for r in range(world):
+            lo, hi = sharding.shard_range(n, world, r)
+            c.gen_ids(seed, hi - lo, start=lo)
+            c.batch_topk_dev(tp.data_ptr(), ts, q, k, None, None, rec[r].data_ptr(), lo, c.stream)
+            torch.cuda.synchronize()
+    t_shards = time.perf_counter() - t0
+    out = torch.empty((q, k), dtype=torch.int32, device=dev)
+    cnt = torch.empty(q, dtype=torch.int32, device=dev)
+    ties = torch.zeros(1 + sharding.TIE_CAP, dtype=torch.int32, device=dev)
+    assert L.dhtgpu_merge_dev(rec.data_ptr(), world, q, k, tp.data_ptr(), ts, k, out.data_ptr(), cnt.data_ptr(),
+                              ties.data_ptr(), sharding.TIE_CAP, None) == 0
+    torch.cuda.synchronize()
+    assert int(ties[0].item()) == 0
+    got = out.cpu().numpy().view(np.uint32)
+    gcnt = cnt.cpu().numpy().view(np.uint32)
+    del rec, out, cnt
+    assert np.all(gcnt == k)
+    t0 = time.perf_counter()
+    with opendht_amd.Context(0) as c:
+        c.gen_ids(seed, n)
+        one, ocnt = c.batch_topk(tg, k)
+    t_one = time.perf_counter() - t0
+    assert np.array_equal(ocnt, gcnt)
+    bad = np.nonzero((one != got).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} targets differ between the routes, first {bad[:5]}"
+    rows = sample_rows(q, 40)
+    t0 = time.perf_counter()
+    want, wcnt = O.topk_gen(seed, n, tg[rows], k, threads=16)
+    print(f"cfg3 full: 8 shards {t_shards:.1f} s, one-set route {t_one:.1f} s, oracle {time.perf_counter() - t0:.1f} s")
+    assert np.array_equal(got[rows], want) and np.array_equal(gcnt[rows], wcnt)
 
 
 def test_subpartition_with_fewer_than_k_ids(ctx):

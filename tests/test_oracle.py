@@ -93,6 +93,22 @@ def test_topk_vs_bigint(n, k):
         assert np.all(out[qi, cnt[qi]:] == 0xFFFFFFFF)
 
 
+@pytest.mark.parametrize("n,k,start", [(5, 8, 0), (20000, 8, 0), (20000, 1, 3), (150000, 32, 10**6)])
+def test_topk_gen_equals_topk(n, k, start):
+    """The generator-fed entry (cfg 3's 10^9-id checker: ids made on the fly, per-thread bounded
+    lists merged) == the array form, on stream indices; targets include exact hits and a target
+    sharing 40 leading bits with an id (word-1 ties)."""
+    ids = O.gen_ids(21, n, start=start)
+    tg = O.gen_ids(22, 24)
+    tg[:3] = ids[[0, n // 2, n - 1]]
+    tg[3, :5] = ids[n // 3, :5]
+    want, wcnt = O.topk(ids, tg, k, threads=4)
+    got, gcnt = O.topk_gen(21, n, tg, k, start=start, threads=3)
+    want = np.where(want == 0xFFFFFFFF, want, want + start)
+    assert np.array_equal(got, want) and np.array_equal(gcnt, wcnt)
+    assert list(got[5, :gcnt[5]]) == [start + i for i in O.py_topk(ids, tg[5], k)]
+
+
 def test_topk_duplicates_tie_by_index():
     base = O.gen_ids(3, 50)
     ids = np.concatenate([base, base[::-1], base[:5]])
