@@ -336,7 +336,10 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
 // Loads are unconditional 16-B loads (no data-dependent branches, so every load of the
 // ring stays in flight): addresses past the id range are clamped into the plane
 // allocation and their words are masked by the caller's range test.
-constexpr uint32_t kRing = 8;     // S1's ring (two 512-thread workgroups per CU: 64 KB each)
+#ifndef DHT_S1_RING
+#define DHT_S1_RING 8   // (override: ring-depth A/B builds)
+#endif
+constexpr uint32_t kRing = DHT_S1_RING;     // S1's ring (two 512-thread workgroups per CU: 64 KB each)
 // F2's ring: 2 sub-steps = 32 KB in flight per CU.  A pure 64 MB stream by one 1024-thread
 // workgroup per CU (tools/experiments/stream_probe.hip, profiles/r03/experiments) takes
 // 13.3 us with 8 (128 KB in flight), 11.7 with 4, 11.1 with 3, 10.3 with 2: a deeper ring only

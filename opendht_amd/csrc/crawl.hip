@@ -9,7 +9,7 @@
 // RoutingTable::findClosestNodes, src/routing_table.cpp:110-150).  One iterative search
 // per target (Dht::Search, src/search.h) with Search::insertNode's ordering and trimming
 // (:636-722, SEARCH_NODES = 14), MAX_REQUESTED_SEARCH_NODES = 4 requests per round
-// (src/dht.h:321, Dht::searchSendGetValues src/dht.cpp:313-378) and the isSynced stop
+// (include/opendht/dht.h:321, Dht::searchSendGetValues src/dht.cpp:313-378) and the isSynced stop
 // rule (:734-747).
 //
 // Kernels:
@@ -24,7 +24,7 @@ namespace dhtgpu {
 namespace {
 
 // kAlphaMax bounds the run-time alpha (requests per round; the reference's MAX_REQUESTED_SEARCH_NODES
-// = 4, src/dht.h:321, is the default; BASELINE cfg 5 states 3)
+// = 4, include/opendht/dht.h:321, is the default; BASELINE cfg 5 states 3)
 constexpr uint32_t kSearchNodes = 14, kTargetNodes = 8, kAlphaMax = 8, kBucket = 8, kLevels = 32;
 constexpr uint32_t kListCap = 64, kDeadCap = 64;
 constexpr uint32_t kQ = 1, kReplied = 2, kBad = 4;

@@ -144,6 +144,7 @@ constexpr uint32_t kClsExact = 0x8000u;          // table flag: the cell's ids t
 constexpr uint32_t kClsSkip = 15u;               // histogram field an exact-path id adds to (discarded)
 constexpr uint32_t kRegT = 15u;                  // register path: commonBits below this from word 0
 constexpr uint32_t kClsFlush = 255u / (4 * kClsU);   // chunks per byte-counter flush
+constexpr uint32_t kClsQCap = 1024;              // queued exact-path ids per wave (> one chunk's 4 * 64 * kClsU)
 
 // the reference's findBucket over the firsts in LDS (sf: plane-major, nb entries per plane):
 // the last bucket whose first <= id, bucket 0 when none (a linear walk from the front stops
@@ -193,6 +194,12 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
     __shared__ uint16_t lut[kClsCells];   // bucket | commonBits << 8 | kClsExact
     __shared__ uint32_t s_bad;            // a first inside a commonBits range: no register path
     __shared__ uint32_t s_map[4];         // register path: bucket of commonBits c in byte c
+    // the exact path, deferred: each wave queues its exact-path ids (index) here during the
+    // stream and answers them between chunks once the queue could not take another chunk's worth,
+    // and at the end -- a call inside the chunk kept the chunk's ids and keys live across it (117
+    // VGPRs, 4 waves per SIMD; without it 95)
+    __shared__ uint32_t s_q[kClsBlock / 64][kClsQCap];
+    __shared__ uint32_t s_qn[kClsBlock / 64];
     constexpr uint32_t CH = 64 * kClsU;   // uint4 per wave chunk
     constexpr uint32_t NE = 4 * kClsU;    // ids per lane per chunk
     const uint64_t n4 = (n + 3) / 4;
@@ -224,6 +231,7 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
     for (uint32_t i = threadIdx.x; i < DHT_W * nb; i += kClsBlock) sf[i] = fp[i];
     for (uint32_t i = threadIdx.x; i < 161; i += kClsBlock) sh[i] = 0;
     if (threadIdx.x < 4) s_map[threadIdx.x] = 0u;
+    if (threadIdx.x < kClsBlock / 64) s_qn[threadIdx.x] = 0u;
     if (threadIdx.x == 0) s_bad = 0u;
     __syncthreads();
     // register path test: every first with commonBits c < kRegT starts its range (the bits
@@ -327,20 +335,13 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
                 }
             }
         }
-        // the exact path: rare ids, one at a time per lane
+        // the exact path's ids (rare) join the wave's queue; their bucket bytes are stored below
+        // as placeholders and rewritten when the queue is answered, their bins are field 15's
         while (exact) {
             const uint32_t k = (uint32_t)__ffs(exact) - 1;
             exact &= exact - 1;
-            const uint32_t u = k >> 2, e = k & 3u;
-            const uint64_t i = 4 * (c * CH + u * 64 + lane) + e;
-            uint32_t xk = 0;
-#pragma unroll
-            for (uint32_t kk = 0; kk < NE; ++kk) xk = kk == k ? x[kk] : xk;
-            const uint2 r = cls_exact(planes, stride, i, xk, sf, nb, m0, m1, m2, m3, m4);
-#pragma unroll
-            for (uint32_t uu = 0; uu < kClsU; ++uu)
-                if (uu == u) packed[uu] = (packed[uu] & ~(0xFFu << (8 * e))) | (r.x << (8 * e));
-            atomicAdd(&sh[r.y], 1u);
+            const uint32_t i = 4 * ((uint32_t)(c * CH) + (k >> 2) * 64 + lane) + (k & 3u);
+            s_q[wv][atomicAdd(&s_qn[wv], 1u)] = i;
         }
         acc_e += pk & 0x0F0F0F0F0F0F0F0Full;
         acc_o += (pk >> 4) & 0x0F0F0F0F0F0F0F0Full;
@@ -358,18 +359,36 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
             }
         }
     };
+    // answer the wave's queued exact-path ids, one per lane: bucket byte (after this wave's
+    // earlier stores of the same words have completed) and commonBits bin
+    auto answer_queue = [&]() {   // wave-uniform
+        const uint32_t nq = __builtin_amdgcn_readfirstlane(s_qn[wv]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (uint32_t b = 0; b < nq; b += 64) {
+            if (b + lane < nq) {
+                const uint32_t i = s_q[wv][b + lane];
+                const uint2 r = cls_exact(planes, stride, i, planes[i], sf, nb, m0, m1, m2, m3, m4);
+                if (out_bucket) out_bucket[i] = (uint8_t)r.x;
+                atomicAdd(&sh[r.y], 1u);
+            }
+        }
+        if (lane == 0) s_qn[wv] = 0u;
+    };
     auto stream = [&](auto regs_c) {
         for (; c < nch; c += W) {   // wave-uniform
             uint4 nx[kClsU];
             load(c + W, nx);
             if (c < nfull) chunk(std::true_type{}, regs_c);
             else chunk(std::false_type{}, regs_c);
+            // room for the next chunk's ids in the queue (wave-uniform)
+            if (__builtin_amdgcn_readfirstlane(s_qn[wv]) > kClsQCap - 4 * CH) answer_queue();
 #pragma unroll
             for (uint32_t u = 0; u < kClsU; ++u) v[u] = nx[u];
         }
     };
     if (regs) stream(std::true_type{});
     else stream(std::false_type{});
+    answer_queue();
     flush_acc();
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < 161; i += kClsBlock)
@@ -455,7 +474,7 @@ hipError_t launch_classify(const uint32_t* planes, uint64_t stride, uint64_t n, 
                            const uint32_t* fp, const uint32_t* myid, uint8_t* out_bucket,
                            unsigned long long* hist, hipStream_t s) {
     if (!n) return hipSuccess;
-    if (n >= (1ull << 33)) return hipErrorInvalidValue;   // k_classify's 32-bit uint4 indices (look-ahead included)
+    if (n >= (1ull << 32)) return hipErrorInvalidValue;   // k_classify's 32-bit id indices (queued exact-path ids)
     const uint64_t n4 = (n + 3) / 4;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
