@@ -759,10 +759,14 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     bc.nsub = S;
     bc.sub_shift = c->shard_pbits;
     bc.sub_bits = sb;
+    bc.out_rec = out_rec;   // F3 writes the records of the targets it answers
+    bc.rec_gidx = c->out_map();
+    bc.rec_base = idx_base;
     r = batch_slot_run(c, si, bc, s, ev);
     if (r) return r;
     if (out_rec) {
-        DHT_TRY(launch_rec3(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, c->out_map(), out_rec, s));
+        DHT_TRY(launch_rec3(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, c->out_map(), out_rec, s,
+                            k));
     } else if (!global && idx_base) {
         DHT_TRY(launch_map_idx(out_idx, (uint64_t)q * k, nullptr, idx_base, s));
     }
@@ -871,10 +875,13 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     bc.num_cus = c->num_cus;
     bc.dbg = c->dbg;
     bc.ev = ev;
+    bc.out_rec = out_rec;   // F3 writes the records of the targets it answers
+    bc.rec_gidx = gidx;
+    bc.rec_base = idx_base;
     int r = batch_slot_run(c, si, bc, s, ev);
     if (r) return r;
     if (out_rec)
-        DHT_TRY(launch_rec3(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx, out_rec, s));
+        DHT_TRY(launch_rec3(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx, out_rec, s, k));
     return DHTGPU_OK;
 }
 

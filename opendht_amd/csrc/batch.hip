@@ -606,6 +606,22 @@ __host__ __device__ inline uint32_t f3_words(uint32_t nsub) {
     return (nsub + 1 + 17 + kF3Threads + 1 + 2 + 1) & ~1u;
 }
 
+// Record form (dhtgpu_batch_topk_dev with out_rec): F3's fast path writes each answered target's
+// compact records {w0, w1, global idx} itself -- word 0 from the LDS stage when the stage holds
+// unshifted words, word 1 (and word 0 of shifted stages) gathered from the context's planes at the
+// context-local index -- and marks the target's local-index row kRecDone; the record kernel
+// (k_rec3) then converts only the other rows (ties, wave-path and fallback targets).  The 65,536 x
+// 8 gathers of a separate conversion pass cost 23 us on the chain at cfg 2 (profiles/r05/b).
+constexpr uint32_t kRecDone = 0xFFFFFFFEu;   // never a local index (sets hold < 2^32 - 1 ids)
+struct RecOut {
+    uint32_t* out;            // nullable: q * k * 3 words
+    const uint32_t* planes;   // the context's (unshifted) planes; record words of context-local indices
+    uint64_t stride;
+    const uint32_t* gidx;     // context-local -> global index (nullable) ...
+    uint32_t base;            // ... or offset
+    uint32_t w0_direct;       // the F3 stage holds unshifted word 0 (one set, no shard shift)
+};
+
 struct F3Args {
     const uint2* pbuf; uint32_t* pcount; uint32_t pcap;
     const uint2* tbuf; uint32_t* tcount; uint32_t tcap;   // F1 target buckets (tcount all-zero between calls)
@@ -626,6 +642,7 @@ struct F3Args {
     uint32_t dbg;
     unsigned long long* stamps;          // dbg & 256: per-block phase timestamps [np][16]
     uint32_t cap;                        // LDS stage entries (the plan's, <= kF3Cap)
+    RecOut rec;                          // record form: F3's fast path writes compact records itself
 };
 
 // (w0 distance, w1 distance, index) order; words 2..4 are read only when both distances tie
@@ -1015,7 +1032,35 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                     // LDS reads first, then (shards) all gidx loads together: one wait before
                     // the stores instead of one per place
                     uint32_t res[K];
-                    if (full_row) {   // k == K == want, 16-B aligned rows (block-uniform)
+                    if (a.rec.out) {   // record form (block-uniform): the target's records here
+                        uint32_t w0[K];
+#pragma unroll
+                        for (int r = 0; r < K; ++r) {
+                            const uint2 e = S[(uint32_t)r < want && ok[r] < a.cap ? ok[r] : 0u];
+                            res[r] = e.y;
+                            w0[r] = e.x;
+                        }
+#pragma unroll
+                        for (int r = 0; r < K; ++r) res[r] = map_out(res[r], a.gidx, a.base);   // context-local
+                        uint32_t w1[K], gi[K];
+#pragma unroll
+                        for (int r = 0; r < K; ++r) {
+                            if (!a.rec.w0_direct) w0[r] = a.rec.planes[res[r]];
+                            w1[r] = a.rec.planes[a.rec.stride + res[r]];
+                            gi[r] = a.rec.gidx ? a.rec.gidx[res[r]] : res[r] + a.rec.base;
+                        }
+                        uint32_t* ro = a.rec.out + (uint64_t)qi * a.k * 3;
+#pragma unroll
+                        for (int r = 0; r < K; ++r) {
+                            if ((uint32_t)r >= a.k) continue;
+                            const bool v = (uint32_t)r < want;
+                            ro[3 * r] = v ? w0[r] : DHT_NONE;
+                            ro[3 * r + 1] = v ? w1[r] : DHT_NONE;
+                            ro[3 * r + 2] = v ? gi[r] : DHT_NONE;
+                        }
+                        orow[0] = kRecDone;
+                        a.out_cnt[qi] = want;
+                    } else if (full_row) {   // k == K == want, 16-B aligned rows (block-uniform)
 #pragma unroll
                         for (int r = 0; r < K; ++r) res[r] = S[ok[r]].y;
                         if (a.gidx) {
@@ -1881,7 +1926,9 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     // the base arguments are the whole set's: F4's scan (fallback targets) runs over all its ids
     F3Args a{pbuf, pcount, P.scap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, c.planes, c.stride,
              c.n, c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, fb_sub, pstat, tie_hdr, tie_cand, tie_cnt,
-             d_desc, np, dbg, stamps, narrow ? P.f3cap : P.f3cap_wide};
+             d_desc, np, dbg, stamps, narrow ? P.f3cap : P.f3cap_wide, RecOut{}};
+    if (c.out_rec)
+        a.rec = RecOut{c.out_rec, c.planes, c.stride, c.rec_gidx, c.rec_base, (nsub == 1 && !c.w0s && !c.skip) ? 1u : 0u};
     // F3 stages the plan's 6-sigma bound only beside F2's narrow stage (which it makes room for)
     size_t l3 = f3_lds(P, a.cap);
     if (dbg & 4096) l3 = l3 > 81920 ? l3 : 81920;   // experiment: 2 F3 blocks per CU

@@ -187,9 +187,10 @@ __global__ __launch_bounds__(256) void k_map_idx(uint32_t* __restrict__ idx, uin
 // 65,536 x 8 records).  The global index is gidx[x] (nullable map) or x + base.
 __global__ __launch_bounds__(256) void k_rec3(const uint32_t* __restrict__ idx, uint64_t m,
                                               const uint32_t* __restrict__ planes, uint64_t stride, uint32_t base,
-                                              const uint32_t* __restrict__ gidx, uint32_t* __restrict__ rec) {
+                                              const uint32_t* __restrict__ gidx, uint32_t* __restrict__ rec, uint32_t k) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= m) return;
+    if (k && idx[i - i % k] == kRecDoneMark) return;   // K6's F3 wrote this row's records itself
     const uint32_t x = idx[i];
     const bool none = x == DHT_NONE;
     const uint32_t xc = none ? 0u : x;
@@ -211,26 +212,36 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge3(const uint32_t* __rest
                                                           uint32_t k, uint32_t* __restrict__ out_idx,
                                                           uint32_t* __restrict__ out_cnt, uint32_t* __restrict__ ties,
                                                           uint32_t tie_cap) {
-    extern __shared__ uint32_t sm[];   // [thread][kin][3]
-    constexpr uint32_t TPW = 64 / G;
+    extern __shared__ uint32_t sm[];   // [list][block target][kin][3]: the block's records as stored
+    constexpr uint32_t TPW = 64 / G, T = (kMergeThreads / 64) * TPW;   // targets per block
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     const uint32_t g = lane / G, j = lane % G;
-    const uint32_t qi = (blockIdx.x * (kMergeThreads / 64) + wv) * TPW + g;
+    const uint32_t qb = blockIdx.x * T, tl = wv * TPW + g;
+    const uint32_t qi = qb + tl;
     const bool tv = qi < q, lv = tv && j < lists;
     const uint32_t qc = tv ? qi : 0u;
     const uint32_t t0 = tp[qc], t1 = tp[ts + qc];
-    uint32_t* my = sm + threadIdx.x * kin * 3;
-    const uint32_t* src = rec + ((uint64_t)(lv ? j : 0u) * q + qc) * kin * 3;
-    for (uint32_t r = 0; r < kin; ++r) {
-        const uint32_t a = src[r * 3], b = src[r * 3 + 1], ix = lv ? src[r * 3 + 2] : DHT_NONE;
-        const bool none = ix == DHT_NONE;
-        my[3 * r] = none ? DHT_NONE : a ^ t0;
-        my[3 * r + 1] = none ? DHT_NONE : b ^ t1;
-        my[3 * r + 2] = ix;
+    // the block's targets' records are one contiguous run per list: copied by all threads with
+    // consecutive lanes on consecutive words (a thread reading its own 12-B records strode 96 B
+    // across the wave), then read from LDS
+    const uint32_t nt = q - qb < T ? q - qb : T, run = nt * kin * 3;
+    for (uint32_t l = 0; l < lists; ++l) {
+        const uint32_t* src = rec + ((uint64_t)l * q + qb) * kin * 3;
+        uint32_t* dst = sm + l * T * kin * 3;
+        for (uint32_t w = threadIdx.x; w < run; w += kMergeThreads) dst[w] = src[w];
     }
+    __syncthreads();
+    const uint32_t* my = sm + ((lv ? j : 0u) * T + (tv ? tl : 0u)) * kin * 3;
+    auto head = [&](uint32_t p, uint32_t& a, uint32_t& b, uint32_t& ix) {
+        ix = lv && p < kin ? my[3 * p + 2] : DHT_NONE;
+        const bool none = ix == DHT_NONE;
+        a = none ? DHT_NONE : my[3 * p] ^ t0;
+        b = none ? DHT_NONE : my[3 * p + 1] ^ t1;
+    };
     const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (g * G);
     uint32_t p = 0, cnt = 0;
-    uint32_t h0 = my[0], h1 = my[1], hi = my[2];
+    uint32_t h0, h1, hi;
+    head(0, h0, h1, hi);
     bool row_tie = false;
     for (uint32_t r = 0; r < k; ++r) {   // wave-uniform
         uint32_t m0 = h0, m1 = h1, mi = hi;
@@ -247,11 +258,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge3(const uint32_t* __rest
         if (mi == DHT_NONE) continue;   // this target's lists are exhausted (group-uniform)
         if (tv && j == 0) out_idx[(uint64_t)qi * k + r] = mi;
         ++cnt;
-        if (lv && h0 == m0 && h1 == m1 && hi == mi) {
-            ++p;
-            if (p < kin) { h0 = my[3 * p]; h1 = my[3 * p + 1]; hi = my[3 * p + 2]; }
-            else { h0 = DHT_NONE; h1 = DHT_NONE; hi = DHT_NONE; }
-        }
+        if (lv && h0 == m0 && h1 == m1 && hi == mi) head(++p, h0, h1, hi);
     }
     if (tv && j == 0) {
         for (uint32_t r = cnt; r < k; ++r) out_idx[(uint64_t)qi * k + r] = DHT_NONE;
@@ -405,9 +412,9 @@ hipError_t launch_map_idx(uint32_t* idx, uint64_t m, const uint32_t* gidx, uint3
 }
 
 hipError_t launch_rec3(const uint32_t* idx, uint64_t m, const uint32_t* planes, uint64_t stride, uint32_t base,
-                       const uint32_t* gidx, uint32_t* rec, hipStream_t s) {
+                       const uint32_t* gidx, uint32_t* rec, hipStream_t s, uint32_t k) {
     if (!m) return hipSuccess;
-    k_rec3<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(idx, m, planes, stride, base, gidx, rec);
+    k_rec3<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(idx, m, planes, stride, base, gidx, rec, k);
     return hipGetLastError();
 }
 

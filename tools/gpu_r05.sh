@@ -4,7 +4,7 @@
 set -o pipefail
 OUT=gpurun_out/${1:-r05}; mkdir -p $OUT
 export TMPDIR=/tmp
-T="python -u -m pytest -q --timeout 300 --timeout-method thread"
+T="python -u -m pytest -q --timeout 300 --timeout-method thread --durations=8"
 timeout -k 10 600 $T tests -m gpu -x -k "merge or records or cfg3 or tie" > $OUT/gpu_new.log 2>&1 || { tail -60 $OUT/gpu_new.log; exit 1; }
 tail -1 $OUT/gpu_new.log
 timeout -k 10 900 $T tests -m gpu --maxfail=3 -k "not (merge or records or cfg3 or tie)" > $OUT/gpu_tests.log 2>&1 || { tail -60 $OUT/gpu_tests.log; exit 1; }
