@@ -1389,7 +1389,22 @@ double poisson_below(double m, uint32_t k) {
     return sum;
 }
 
+BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus);
+
+// plan_batch is a pure function of (n, q, k, CUs), asked three times per call (workspace size,
+// clean head, the launch): the last few plans are kept per host thread
 BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
+    struct Entry { uint64_t n; uint32_t q, k; int cus; BatchPlan P; bool used; };
+    thread_local Entry cache[4] = {};
+    thread_local uint32_t next = 0;
+    for (const Entry& e : cache)
+        if (e.used && e.n == n && e.q == q && e.k == k && e.cus == num_cus) return e.P;
+    Entry& e = cache[next++ & 3u];
+    e = Entry{n, q, k, num_cus, plan_batch_compute(n, q, k, num_cus), true};
+    return e.P;
+}
+
+BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     BatchPlan P;
     // mark level: 4k or more ids per level-Lm subtree -- or one level finer (2k..4k) when, on
     // uniform ids, fewer than 0.01 of the q targets are expected to land in a subtree with

@@ -351,7 +351,11 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
             for (uint32_t u = 0; u < kClsU; ++u) {
                 const uint64_t i4 = c * CH + u * 64 + lane;
                 if (FULL || 4 * i4 + 3 < n) {
+#ifdef DHT_K2_NTSTORE
+                    __builtin_nontemporal_store(packed[u], reinterpret_cast<uint32_t*>(out_bucket + 4 * i4));
+#else
                     *reinterpret_cast<uint32_t*>(out_bucket + 4 * i4) = packed[u];
+#endif
                 } else {
                     for (uint32_t e = 0; e < 4; ++e)
                         if (4 * i4 + e < n) out_bucket[4 * i4 + e] = (uint8_t)(packed[u] >> (8 * e));
