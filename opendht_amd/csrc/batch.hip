@@ -1046,17 +1046,35 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
 #pragma unroll
                         for (int r = 0; r < K; ++r) {
                             if (!a.rec.w0_direct) w0[r] = a.rec.planes[res[r]];
-                            w1[r] = a.rec.planes[a.rec.stride + res[r]];
+                            // 2^16: word 1 not gathered (records wrong; timing only)
+                            w1[r] = (Diag && (a.dbg & (1u << 16))) ? w0[r] : a.rec.planes[a.rec.stride + res[r]];
                             gi[r] = a.rec.gidx ? a.rec.gidx[res[r]] : res[r] + a.rec.base;
                         }
                         uint32_t* ro = a.rec.out + (uint64_t)qi * a.k * 3;
+                        if (Diag && (a.dbg & (1u << 17))) {
+                            // 2^17: records not stored (timing only)
+                        } else if (full_row && ((uintptr_t)a.rec.out & 15) == 0) {
+                            // k == K == want: the row is 3K words from a 16-B boundary (K % 4 == 0),
+                            // 3K / 4 vector stores instead of 3K dword stores
+                            uint32_t wds[3 * K];
 #pragma unroll
-                        for (int r = 0; r < K; ++r) {
-                            if ((uint32_t)r >= a.k) continue;
-                            const bool v = (uint32_t)r < want;
-                            ro[3 * r] = v ? w0[r] : DHT_NONE;
-                            ro[3 * r + 1] = v ? w1[r] : DHT_NONE;
-                            ro[3 * r + 2] = v ? gi[r] : DHT_NONE;
+                            for (int r = 0; r < K; ++r) {
+                                wds[3 * r] = w0[r];
+                                wds[3 * r + 1] = w1[r];
+                                wds[3 * r + 2] = gi[r];
+                            }
+#pragma unroll
+                            for (int r = 0; r < 3 * K; r += 4)
+                                *reinterpret_cast<uint4*>(ro + r) = make_uint4(wds[r], wds[r + 1], wds[r + 2], wds[r + 3]);
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < K; ++r) {
+                                if ((uint32_t)r >= a.k) continue;
+                                const bool v = (uint32_t)r < want;
+                                ro[3 * r] = v ? w0[r] : DHT_NONE;
+                                ro[3 * r + 1] = v ? w1[r] : DHT_NONE;
+                                ro[3 * r + 2] = v ? gi[r] : DHT_NONE;
+                            }
                         }
                         orow[0] = kRecDone;
                         a.out_cnt[qi] = want;
