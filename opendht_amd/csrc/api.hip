@@ -723,7 +723,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     const bool global = c->has_gidx && c->map_global && !out_rec;
     const int si = pick_slot(c, s);
     dhtgpu_ctx::BatchSlot& b = c->bslot[si];
-    // record mode: context-local indices first (then records from the context's planes)
+    // record form: the index rows are scratch (K6 stores the records themselves)
     uint32_t* li = out_idx;
     uint32_t* lc = out_cnt;
     if (out_rec) {
@@ -759,15 +759,12 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     bc.nsub = S;
     bc.sub_shift = c->shard_pbits;
     bc.sub_bits = sb;
-    bc.out_rec = out_rec;   // F3 writes the records of the targets it answers
+    bc.out_rec = out_rec;   // every K6 writer of a row stores its records
     bc.rec_gidx = c->out_map();
     bc.rec_base = idx_base;
     r = batch_slot_run(c, si, bc, s, ev);
     if (r) return r;
-    if (out_rec) {
-        DHT_TRY(launch_rec3(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, c->out_map(), out_rec, s,
-                            k));
-    } else if (!global && idx_base) {
+    if (!out_rec && !global && idx_base) {   // (record form: K6 wrote the records)
         DHT_TRY(launch_map_idx(out_idx, (uint64_t)q * k, nullptr, idx_base, s));
     }
     return DHTGPU_OK;
@@ -851,7 +848,7 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     const uint32_t* gidx = c->out_map();
     uint32_t* li = out_idx;
     uint32_t* lc = out_cnt;
-    if (out_rec) {   // local indices first, then candidate records for a cross-shard merge
+    if (out_rec) {   // record form: the index rows are scratch (K6 stores the records themselves)
         DHT_TRY(b.out_idx.ensure((size_t)q * k * 4));
         DHT_TRY(b.out_cnt.ensure((size_t)q * 4));
         li = b.out_idx.as<uint32_t>();
@@ -875,14 +872,10 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     bc.num_cus = c->num_cus;
     bc.dbg = c->dbg;
     bc.ev = ev;
-    bc.out_rec = out_rec;   // F3 writes the records of the targets it answers
+    bc.out_rec = out_rec;   // every K6 writer of a row stores its records
     bc.rec_gidx = gidx;
     bc.rec_base = idx_base;
-    int r = batch_slot_run(c, si, bc, s, ev);
-    if (r) return r;
-    if (out_rec)
-        DHT_TRY(launch_rec3(li, (uint64_t)q * k, c->planes.as<uint32_t>(), c->stride, idx_base, gidx, out_rec, s, k));
-    return DHTGPU_OK;
+    return batch_slot_run(c, si, bc, s, ev);   // (record form: K6 writes the records itself)
 }
 
 int dhtgpu_batch_topk_dev(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k,

@@ -606,13 +606,13 @@ __host__ __device__ inline uint32_t f3_words(uint32_t nsub) {
     return (nsub + 1 + 17 + kF3Threads + 1 + 2 + 1) & ~1u;
 }
 
-// Record form (dhtgpu_batch_topk_dev with out_rec): F3's fast path writes each answered target's
-// compact records {w0, w1, global idx} itself -- word 0 from the LDS stage when the stage holds
-// unshifted words, word 1 (and word 0 of shifted stages) gathered from the context's planes at the
-// context-local index -- and marks the target's local-index row kRecDone; the record kernel
-// (k_rec3) then converts only the other rows (ties, wave-path and fallback targets).  The 65,536 x
-// 8 gathers of a separate conversion pass cost 23 us on the chain at cfg 2 (profiles/r05/b).
-constexpr uint32_t kRecDone = 0xFFFFFFFEu;   // never a local index (sets hold < 2^32 - 1 ids)
+// Record form (dhtgpu_batch_topk_dev with out_rec): every K6 writer of a result row -- F3's fast
+// path, the wave paths of F3 and F4 (ties, large subtrees), F4's fallback scan and its split merge
+// -- stores the row's compact records {w0, w1, global idx} itself, from the words it already holds
+// (word 0 from the LDS stage when the stage holds unshifted words, word 1 where the wave paths
+// loaded it) and a gather from the planes otherwise.  No conversion pass follows K6: the 65,536 x 8
+// gathers of a separate pass cost 23 us on the chain at cfg 2, the pass over the rows F3 left 2 us
+// (profiles/r05/b, r05/f).
 struct RecOut {
     uint32_t* out;            // nullable: q * k * 3 words
     const uint32_t* planes;   // the context's (unshifted) planes; record words of context-local indices
@@ -621,6 +621,25 @@ struct RecOut {
     uint32_t base;            // ... or offset
     uint32_t w0_direct;       // the F3 stage holds unshifted word 0 (one set, no shard shift)
 };
+
+// place r of target qi's records: the id at index x of the writer's set (a.planes: the context's,
+// or a sub-partition's with a.gidx mapping x to the context-local index); w0 when the caller holds
+// the unshifted word (w0_ok), else read; w1 as loaded by the caller.  x == DHT_NONE: an empty place.
+__device__ __forceinline__ void rec_place(const RecOut& o, const uint32_t* __restrict__ planes, const uint32_t* gidx,
+                                          uint32_t base, uint32_t k, uint32_t qi, uint32_t r, uint32_t x, uint32_t w0,
+                                          bool w0_ok, uint32_t w1) {
+    uint32_t* ro = o.out + ((uint64_t)qi * k + r) * 3;
+    if (x == DHT_NONE) {
+        ro[0] = DHT_NONE;
+        ro[1] = DHT_NONE;
+        ro[2] = DHT_NONE;
+        return;
+    }
+    const uint32_t cl = gidx ? gidx[x] : x + base;   // context-local
+    ro[0] = w0_ok ? w0 : planes[x];
+    ro[1] = w1;
+    ro[2] = o.gidx ? o.gidx[cl] : cl + o.base;
+}
 
 struct F3Args {
     const uint2* pbuf; uint32_t* pcount; uint32_t pcap;
@@ -691,6 +710,11 @@ __device__ void wave_rank_loaded(const F3Args& a, uint2 me, uint32_t mm, uint32_
             else if (xd == md && x1 == m1 && act && o != lane && id_less(xd, xi, md, me.y, a.planes, a.stride, t)) ++rank;
         }
     }
+    if (a.rec.out) {   // record form (the candidates' word 0 as staged)
+        if (act && rank < want) rec_place(a.rec, a.planes, a.gidx, a.base, a.k, qi, rank, me.y, me.x, a.rec.w0_direct, w1);
+        if (lane >= want && lane < a.k) rec_place(a.rec, a.planes, a.gidx, a.base, a.k, qi, lane, DHT_NONE, 0u, true, 0u);
+        return;
+    }
     uint32_t* orow = a.out_idx + (uint64_t)qi * a.k;
     if (act && rank < want) orow[rank] = map_out(me.y, a.gidx, a.base);
     if (lane >= want && lane < a.k) orow[lane] = DHT_NONE;
@@ -746,6 +770,12 @@ __device__ void f3_wave_answer(const F3Args& a, const uint2* S, uint32_t lo, uin
                 w1 = cnt == want ? __builtin_amdgcn_readlane((int)e1, want - 1) : DHT_NONE;
                 wi = cnt == want ? __builtin_amdgcn_readlane((int)ei, want - 1) : DHT_NONE;
             }
+        }
+        if (a.rec.out) {   // record form: word 0 / word 1 back from the distances
+            if (lane < a.k)
+                rec_place(a.rec, a.planes, a.gidx, a.base, a.k, qi, lane, lane < want ? ei : DHT_NONE, ed ^ t0,
+                          a.rec.w0_direct, e1 ^ t[1]);
+            return;
         }
         if (lane < want) orow[lane] = map_out(ei, a.gidx, a.base);
     }
@@ -1076,8 +1106,6 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                                 ro[3 * r + 2] = v ? gi[r] : DHT_NONE;
                             }
                         }
-                        orow[0] = kRecDone;
-                        a.out_cnt[qi] = want;
                     } else if (full_row) {   // k == K == want, 16-B aligned rows (block-uniform)
 #pragma unroll
                         for (int r = 0; r < K; ++r) res[r] = S[ok[r]].y;
@@ -1224,15 +1252,39 @@ __device__ void fb_merge(const F3Args& a, const FbArgs& f, uint32_t g, uint32_t 
                 }
             }
             const uint32_t wi = __builtin_amdgcn_readlane((int)hi, (int)win);
-            if (lane == 0) orow[r] = map_out(wi, a.gidx, a.base);
+            if (lane == 0) {
+                if (a.rec.out)   // record form: word 0 back from the distance, word 1 read
+                    rec_place(a.rec, a.planes, a.gidx, a.base, k, qr, r, wi, m ^ t[0], true, a.planes[a.stride + wi]);
+                else
+                    orow[r] = map_out(wi, a.gidx, a.base);
+            }
             if (lane == win) {
                 ++p;
                 hd = p < k ? buf[2 * (lane * k + p)] : DHT_NONE;
                 hi = p < k ? buf[2 * (lane * k + p) + 1] : DHT_NONE;
             }
         }
-        for (uint32_t x = r + lane; x < k; x += 64) orow[x] = DHT_NONE;
+        for (uint32_t x = r + lane; x < k; x += 64) {
+            if (a.rec.out) rec_place(a.rec, a.planes, a.gidx, a.base, k, qr, x, DHT_NONE, 0u, true, 0u);
+            else orow[x] = DHT_NONE;
+        }
         if (lane == 0) a.out_cnt[qr] = r;
+    }
+}
+
+// Record form after a one-split scan role: the wave converts the rows its role just wrote
+// (context-local indices; its own stores, drained, read back at agent scope past the L1) into
+// records from the context's planes.  Writing the records inside the scan's unrolled result loop
+// took F4 from 135 VGPRs to 221 + 752 B of scratch per lane (F4 7.5 -> 25 us, profiles/r05/g).
+__device__ void fb_rows_to_records(const F3Args& a, uint32_t qb, uint32_t qend) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t lane = lane_id(), k = a.k;
+    const uint32_t nt = qend > qb ? (qend - qb < kScanTargets ? qend - qb : kScanTargets) : 0u;
+    for (uint32_t c = lane; c < nt * k; c += 64) {
+        const uint32_t j = c / k, r = c - j * k;
+        const uint32_t qr = a.fb_list[qb + j];
+        const uint32_t x = ld_sc1(a.out_idx + (uint64_t)qr * k + r);
+        rec_place(a.rec, a.rec.planes, nullptr, 0u, k, qr, r, x, 0u, false, x == DHT_NONE ? 0u : a.rec.planes[a.rec.stride + x]);
     }
 }
 
@@ -1290,7 +1342,10 @@ __device__ __forceinline__ void fb_list_scan(const F3Args& a, const FbArgs& f, u
         const uint32_t qb = single ? (wv == 0 ? g : g + 1) : g * kFbGroup + wv * kScanTargets;
         scan::scan_run<K, kScanTargets>(lds, as.planes, as.stride, lo, hi, as.tp, as.ts, as.fb_list, qb,
                                         single ? g + 1 : cnt, as.k, o);
-        if (S == 1) continue;
+        if (S == 1) {
+            if (a.rec.out) fb_rows_to_records(a, qb, single ? g + 1 : cnt);
+            continue;
+        }
         // hand-off: every wave's sc1 record stores drained, then one agent-scope add per block;
         // the block whose add completes the group merges it (its waves load after the barrier)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1950,7 +2005,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         (void)hipEventRecord(ev[2], s);
         (void)hipEventRecord(ev[3], s);
     }
-    if (dbg & ~(48u | 256u | 512u | 1024u | 2048u | 4096u | 8192u | (1u << 23))) {   // experiments: F1 + F2 only
+    if (dbg & ~(48u | 256u | 512u | 1024u | 2048u | 4096u | 8192u | (7u << 16) | (1u << 23))) {   // experiments: F1 + F2 only
         for (int i = 4; ev && i < 8; ++i) (void)hipEventRecord(ev[i], s);
         if (dirty) *dirty = true;   // F3 (which resets the counters and the bitmap) did not run
         return hipGetLastError();

@@ -76,9 +76,7 @@ hipError_t launch_map_idx(uint32_t* idx, uint64_t m, const uint32_t* gidx, uint3
 // local index idx[i] (all DHT_NONE for DHT_NONE); the global index is gidx[idx[i]] when gidx !=
 // nullptr, else idx[i] + base
 hipError_t launch_rec3(const uint32_t* idx, uint64_t m, const uint32_t* planes, uint64_t stride, uint32_t base,
-                       const uint32_t* gidx, uint32_t* rec, hipStream_t s, uint32_t k = 0);
-// k > 0: rows of k whose first index is kRecDone (F3 wrote their records) are skipped
-constexpr uint32_t kRecDoneMark = 0xFFFFFFFEu;
+                       const uint32_t* gidx, uint32_t* rec, hipStream_t s);
 // K3 over compact records (lists <= 64, kin <= 32): rows whose candidates tie on their first 64
 // bits across lists are appended to ties = {count, rows[tie_cap]} (zeroed here; nullable)
 hipError_t launch_merge3(const uint32_t* rec, uint32_t lists, uint32_t q, uint32_t kin, const uint32_t* tp,
@@ -151,9 +149,9 @@ struct BatchCall {
     uint32_t skip; const uint32_t* w0s;    // w0s = 32 id bits from bit `skip` (every id shares its top skip bits)
     const uint32_t* gidx; uint32_t base;   // result index map (nullable) or offset
     uint32_t* out_idx; uint32_t* out_cnt;  // rows of the ORIGINAL target indices
-    // record form (nullable): F3 writes the compact records of the targets it answers and marks
-    // their out_idx rows kRecDone (launch_rec3 converts the rest); rec_gidx / rec_base map the
-    // context-local index (what out_idx holds) to the record's global index
+    // record form (nullable): every writer of a result row (F3, the wave paths, F4's scan and
+    // merge) stores the row's compact records instead of its indices; rec_gidx / rec_base map the
+    // context-local index to the record's global index
     uint32_t* out_rec; const uint32_t* rec_gidx; uint32_t rec_base;
     int num_cus;
     uint32_t dbg;                          // DHTGPU_DBG diagnostics switches (0 in production)

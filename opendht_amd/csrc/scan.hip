@@ -187,10 +187,9 @@ __global__ __launch_bounds__(256) void k_map_idx(uint32_t* __restrict__ idx, uin
 // 65,536 x 8 records).  The global index is gidx[x] (nullable map) or x + base.
 __global__ __launch_bounds__(256) void k_rec3(const uint32_t* __restrict__ idx, uint64_t m,
                                               const uint32_t* __restrict__ planes, uint64_t stride, uint32_t base,
-                                              const uint32_t* __restrict__ gidx, uint32_t* __restrict__ rec, uint32_t k) {
+                                              const uint32_t* __restrict__ gidx, uint32_t* __restrict__ rec) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= m) return;
-    if (k && idx[i - i % k] == kRecDoneMark) return;   // K6's F3 wrote this row's records itself
     const uint32_t x = idx[i];
     const bool none = x == DHT_NONE;
     const uint32_t xc = none ? 0u : x;
@@ -412,9 +411,9 @@ hipError_t launch_map_idx(uint32_t* idx, uint64_t m, const uint32_t* gidx, uint3
 }
 
 hipError_t launch_rec3(const uint32_t* idx, uint64_t m, const uint32_t* planes, uint64_t stride, uint32_t base,
-                       const uint32_t* gidx, uint32_t* rec, hipStream_t s, uint32_t k) {
+                       const uint32_t* gidx, uint32_t* rec, hipStream_t s) {
     if (!m) return hipSuccess;
-    k_rec3<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(idx, m, planes, stride, base, gidx, rec, k);
+    k_rec3<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(idx, m, planes, stride, base, gidx, rec);
     return hipGetLastError();
 }
 

@@ -34,19 +34,27 @@ def shard_range(n, world, rank):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+_GLOO = {}   # group -> its backend is gloo (looked up once: a per-step lookup costs microseconds)
+
+
 def _host_staged(group, *ts):
     """gloo moves host tensors only: device tensors are staged through host copies (the
     one-GPU multi-rank rehearsal); RCCL takes device tensors as they are"""
-    return dist.get_backend(group) == "gloo" and any(t.is_cuda for t in ts)
+    g = _GLOO.get(group)
+    if g is None:
+        g = _GLOO[group] = dist.get_backend(group) == "gloo"
+    return g and any(t.is_cuda for t in ts)
 
 
 def gather_records(rec, group=None, out=None):
     """All-gather this rank's (q, k, W) int32 records -> (world, q, k, W).  `out` may be a
     preallocated (world*q, k, W) buffer (the concatenated form every backend accepts); list l of
     the result is rank l's shard.  Also moves the tie words ((TIE_CAP, k, 3) per rank)."""
-    world = dist.get_world_size(group)
     if out is None:
+        world = dist.get_world_size(group)
         out = torch.empty((world * rec.shape[0],) + tuple(rec.shape[1:]), dtype=rec.dtype, device=rec.device)
+    else:
+        world = out.shape[0] // rec.shape[0]
     if _host_staged(group, rec, out):
         h = torch.empty(out.shape, dtype=out.dtype)
         dist.all_gather_into_tensor(h, rec.contiguous().cpu(), group=group)

@@ -656,6 +656,74 @@ def test_batch_records_merge(ctx):
         c.close()
 
 
+def _want_records(ids, gidx, tg, k):
+    """(q, k, 3) compact records {w0, w1, global idx} of the exact top-k over `ids` (global index
+    of local i = gidx[i]), NONE-padded."""
+    q = tg.shape[0]
+    words = ids.view(">u4").reshape(-1, 5).astype(np.uint32)
+    idx, cnt = O.topk(ids, tg, k, threads=16)
+    rec = np.full((q, k, 3), MU.NONE, dtype=np.uint32)
+    for i in range(q):
+        c = int(cnt[i])
+        li = idx[i, :c].astype(np.int64)
+        rec[i, :c, :2] = words[li, :2]
+        rec[i, :c, 2] = gidx[li]
+    return rec
+
+
+def _ctx_records(c, tg, k, base):
+    import torch
+    import opendht_amd
+    dev = torch.device("cuda", 0)
+    q = tg.shape[0]
+    ts = (q + 63) // 64 * 64
+    tp = torch.zeros(5 * ts, dtype=torch.int32, device=dev)
+    L = opendht_amd.lib()
+    assert L.dhtgpu_pack_dev(torch.from_numpy(tg.reshape(-1)).to(dev).data_ptr(), q, tp.data_ptr(), ts, None) == 0
+    rec = torch.full((q, k, 3), -7, dtype=torch.int32, device=dev)
+    c.batch_topk_dev(tp.data_ptr(), ts, q, k, None, None, rec.data_ptr(), base, c.stream)
+    torch.cuda.synchronize()
+    return rec.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("case", ["uniform", "w0_ties", "fallback_split", "fallback_list", "prefix_shard"])
+@pytest.mark.parametrize("k", [8, 14, 32])
+def test_batch_records_every_writer(case, k):
+    """K6 in record form stores every row's records from its own writer (round 5: no conversion
+    pass): F3's fast path (uniform), F3's and F4's wave paths (ids pairing on word 0: deferred ties
+    and wave-path targets), F4's fallback scan through its split merge (a short list) and as one
+    split per group (a long list), and a prefix shard (shifted word-0 stage: word 0 read back).
+    Every row == the records of the exact top-k, with the index base."""
+    import opendht_amd
+    base = 1000
+    with opendht_amd.Context(0) as c:
+        if case == "prefix_shard":
+            n = 300000
+            allids = O.gen_ids(611, n)
+            c.gen_ids_prefix(611, n, 2, 1)
+            sel = np.nonzero((allids[:, 0] >> 6) == 1)[0]
+            ids, gidx = allids[sel], sel.astype(np.int64)
+            tg = O.gen_ids(612, 1500)
+            base = 0
+        else:
+            n = {"uniform": 200000, "w0_ties": 120000, "fallback_split": 40000, "fallback_list": 30000}[case]
+            ids = O.gen_ids(600 + len(case), n)
+            q = {"fallback_list": 40000}.get(case, 2000)
+            tg = O.gen_ids(650 + len(case), q)
+            if case == "w0_ties":
+                ids[1::4, :4] = ids[0::4, :4]          # pairs sharing word 0
+                tg[::3] = ids[5::7][: tg[::3].shape[0]]   # targets among them
+            elif case.startswith("fallback"):
+                ids[:, 0] = 0x3C                       # ids in one narrow prefix: most subtrees empty
+                tg[:50] = ids[:50]
+            c.set_ids(ids)
+            gidx = np.arange(n, dtype=np.int64) + base
+        got = _ctx_records(c, tg, k, base)
+    want = _want_records(ids, gidx, tg, k)
+    bad = np.nonzero((got != want).any(axis=(1, 2)))[0]
+    assert bad.size == 0, f"{case} k={k}: {bad.size} rows differ, first {bad[:5]}: {got[bad[0]]} vs {want[bad[0]]}"
+
+
 def test_batch_records_tie_words_from_contexts(ctx):
     """The second exchange's payload from live shard contexts (dhtgpu_tie_words_dev: global index ->
     the context's own planes; a prefix shard maps it back through its index map): K6 record mode

@@ -1,0 +1,65 @@
+"""Register and scratch budget of the hot-path kernels (CPU test: hipcc cross-compiles gfx950).
+
+A kernel that spills to scratch, or whose VGPRs cross an occupancy step, runs several times
+slower without any change in its results: round 5's record-form stores inside the fallback scan's
+unrolled result loop took F4 from 135 VGPRs to 221 + 752 B of scratch per lane and F4 from 7.5 to
+25 us (profiles/r05/g), with every parity test green.  This pins the budget at build time."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "opendht_amd", "csrc")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+FILES = ("batch.hip", "scan.hip", "table.hip")
+# mangled-name fragment -> max VGPRs (the occupancy each kernel is tuned for; measured values in
+# the comments, round 5)
+VGPR_CAPS = {
+    "k_f2_filterI": 128,         # 109-111: 4 waves / SIMD beside its 152 KB of LDS
+    "k_f3_answerILi8E": 96,      # 69-78 (the k <= 8 instantiations)
+    "k_f3_answerILi16E": 136,    # 123-136
+    "k_f4I": 144,                # 139: 3 waves / SIMD
+    "k_s1_filterI": 128,
+    "k_s2_answerI": 144,
+    "k_classifyE": 96,           # K2 87: 5 waves / SIMD
+    "k_merge3I": 64,             # 48-52
+}
+
+
+def _usage(path):
+    out = subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only", "-c",
+                          path, "-o", os.devnull, "-Rpass-analysis=kernel-resource-usage"],
+                         capture_output=True, text=True, cwd=CSRC, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    kern, res = None, {}
+    for line in out.stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            kern = m.group(1)
+            res[kern] = {}
+            continue
+        m = re.search(r"(VGPRs|ScratchSize \[bytes/lane\]): (\d+)", line)
+        if m and kern:
+            res[kern][m.group(1).split()[0]] = int(m.group(2))
+    return res
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_hot_kernels_no_scratch_and_vgpr_budget():
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(len(FILES)) as ex:
+        usage = {}
+        for r in ex.map(_usage, [os.path.join(CSRC, f) for f in FILES]):
+            usage.update(r)
+    assert usage, "no kernel resource remarks parsed"
+    spills = {k: v["ScratchSize"] for k, v in usage.items() if v.get("ScratchSize", 0)}
+    assert not spills, f"kernels spilling to scratch: {spills}"
+    seen = set()
+    for k, v in usage.items():
+        for frag, cap in VGPR_CAPS.items():
+            if re.search(rf"\d{frag}", k):
+                seen.add(frag)
+                assert v["VGPRs"] <= cap, f"{k}: {v['VGPRs']} VGPRs > {cap}"
+    assert seen == set(VGPR_CAPS), f"kernels not found: {set(VGPR_CAPS) - seen}"

@@ -71,6 +71,8 @@ def ctxm():
 
 
 rows.append(timed("stream_context", ctxm))
+rows.append(timed("set_stream", lambda: torch.cuda.set_stream(st0)))
+rows.append(timed("ctypes_num_ids", lambda: L.dhtgpu_num_ids(ctx._h)))
 rows.append(timed("all_gather_into_tensor", lambda: dist.all_gather_into_tensor(xb, rec)))
 rows.append(timed("gather_records", lambda: sharding.gather_records(rec, out=xb)))
 g = xb.view(1, q, k, 3)
@@ -86,6 +88,16 @@ def full():
 
 
 rows.append(timed("full_step_one_stream", full))
+
+
+def full_ss():
+    torch.cuda.set_stream(st0)
+    ctx.batch_topk_dev(tp.data_ptr(), ts, q, k, None, None, rec.data_ptr(), 0, s)
+    dist.all_gather_into_tensor(xb, rec)
+    ops.merge(g, 0, k, oi, oc, None, s)
+
+
+rows.append(timed("full_step_set_stream_direct", full_ss))
 print(json.dumps({"rows": rows}))
 ctx.close()
 dist.destroy_process_group()
