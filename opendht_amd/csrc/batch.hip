@@ -830,6 +830,10 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         a.gidx = d.gidx;
         a.base = d.base;
     }
+#ifdef DHT_F3_NOMAP
+    a.gidx = nullptr;   // measurement build: results left sub-partition-local (no map reads)
+    a.base = 0;
+#endif
     F3_STAMP(0);
     if (Diag && (a.dbg & 1024)) __builtin_amdgcn_s_setprio(3);   // experiment: loads/sort first
     // survivors are sorted by their prefix bits [b1, Lq); a target answers from the deepest
@@ -957,6 +961,10 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         const uint32_t G = a.Lm >= 12 ? (mtr <= kF3Threads / 4 ? 4u : mtr <= kF3Threads / 2 ? 2u : 1u) : 1u;
         const uint32_t slot = G == 4 ? threadIdx.x >> 2 : G == 2 ? threadIdx.x >> 1 : lane * NWV + wv;
         const uint32_t gj = threadIdx.x & (G - 1);
+#ifdef DHT_F3_TIE_INLINE
+        uint32_t tq = 0, tt0 = 0, tlo = 0, thi = 0;   // a group leader's tied target, answered inline
+        bool tinl = false;
+#endif
         if (slot < mtr) {   // group-uniform from here on
             const uint2 te = T[slot];
             const uint32_t t0 = te.x, qi = te.y;
@@ -1040,23 +1048,47 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                 bool tie = rmin == dk[want - 1];
 #pragma unroll
                 for (int r = 0; r + 1 < K; ++r) tie = tie || ((uint32_t)r + 1 <= want && dk[r] == dk[r + 1]);
+#ifdef DHT_F3_NOTIES
+                tie = false;   // measurement build: w0 ties answered as if none (results may be wrong)
+#endif
+#ifdef DHT_F3_TIEDETECT_ONLY
+                tie = tie && a.k == 12345u;   // measurement build: ties detected, never deferred
+#endif
                 if (tie) {
+#ifdef DHT_F3_TIE_INLINE
+                  if (gj == 0) {
+                      tinl = true;
+                      tq = qi;
+                      tt0 = t0;
+                      tlo = lo;
+                      thi = hi;
+                      atomicAdd(ntie + 1, 1u);
+                  }
+                  if (false) {
+#endif
                     // hand the candidates to F4 (one wave per tie, off this block's critical
                     // path) while a slot is free and they fit a wave; else phase B here
                     uint32_t tsl = kTieSlots;
                     if (gj == 0) {
                         atomicAdd(ntie + 1, 1u);
+#ifndef DHT_F3_TIE_INPLACE   // measurement build: every tie answered by F3's own wave path (phase B)
                         if (mm <= 64) tsl = atomicAdd(ntie, 1u);
+#endif
                     }
                     if (G > 1) tsl = (uint32_t)__shfl((int)tsl, (int)(lane & ~(G - 1)));
                     if (tsl < kTieSlots) {
                         const uint32_t g = p * kTieSlots + tsl;
                         uint2* dst = a.tie_cand + (uint64_t)g * 64;
+#ifndef DHT_F3_TIE_NOCOPY   // measurement build: candidates not handed over (F4 answers garbage)
                         for (uint32_t o = gj; o < mm; o += G) dst[o] = S[lo + o];
+#endif
                         if (gj == 0) a.tie_hdr[g] = make_uint4(qi, t0, mm, 0u);
                     } else if (gj == 0) {
                         slow[atomicAdd(slow + kF3Threads, 1u)] = slot;
                     }
+#ifdef DHT_F3_TIE_INLINE
+                  }
+#endif
                 } else if (gj == 0) {
                     uint32_t* orow = a.out_idx + (uint64_t)qi * a.k;
                     // LDS reads first, then (shards) all gidx loads together: one wait before
@@ -1138,6 +1170,16 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                 }
             }
         }
+#ifdef DHT_F3_TIE_INLINE
+        // the wave's tied targets, answered by the whole wave right away (one round trip each:
+        // word 1 of the candidates and the target's words) while the block's other waves finish
+        for (uint64_t tb = __ballot(tinl); tb; tb &= tb - 1) {
+            const int L = __ffsll((long long)tb) - 1;
+            f3_wave_answer(a, S, (uint32_t)__builtin_amdgcn_readlane((int)tlo, L),
+                           (uint32_t)__builtin_amdgcn_readlane((int)thi, L), (uint32_t)__builtin_amdgcn_readlane((int)tq, L),
+                           (uint32_t)__builtin_amdgcn_readlane((int)tt0, L), want, lane);
+        }
+#endif
         if (Diag && (a.dbg & 256) && t0i == 0) {   // per wave: the end of its phase-A work
             if (lane == 0) a.stamps[2ull * 8192 * 16 + (uint64_t)blockIdx.x * 16 + wv] = __builtin_amdgcn_s_memrealtime();
         }

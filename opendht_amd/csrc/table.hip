@@ -129,14 +129,21 @@ __global__ __launch_bounds__(256) void k_find_closest(
 // one contiguous 1-KB / 256-B run; the chunk index is wave-uniform (scalar address math).  The
 // next chunk's loads are issued before this chunk's work (two chunks in flight per lane).
 // ---------------------------------------------------------------------------------
-constexpr int kClsBlock = 256;
+// one 1,024-thread workgroup per CU (16 waves, 4 per SIMD): every workgroup ends with one global
+// atomic per histogram bin it touched, and the 1,024 workgroups of 256 threads ended together with
+// 1,024 atomics on bin 0's address, serialised at the memory side (0.0926 -> 0.088 ms without them,
+// 0.0935 -> 0.0897-0.092 with 256 workgroups of 1,024: profiles/r05/j/k2_blocks.txt)
+#ifndef DHT_K2_BLOCK
+#define DHT_K2_BLOCK 1024
+#endif
+constexpr int kClsBlock = DHT_K2_BLOCK;
 #ifndef DHT_K2_PERCU
-#define DHT_K2_PERCU 4
+#define DHT_K2_PERCU 1
 #endif
 #ifndef DHT_K2_U
 #define DHT_K2_U 3
 #endif
-constexpr int kClsPerCu = DHT_K2_PERCU;          // workgroups per CU (4: 0.105 -> 0.096 ms against 8; 117 VGPRs = 4 waves per SIMD, a lower VGPR cap spills)
+constexpr int kClsPerCu = DHT_K2_PERCU;          // workgroups per CU (16 waves per CU: 0.105 -> 0.096 ms against 32 in r04)
 constexpr uint32_t kClsU = DHT_K2_U;             // uint4 of word 0 per lane per chunk
 static_assert(4 * kClsU <= 15, "4-bit histogram fields flushed once per chunk");
 constexpr uint32_t kClsT = 10, kClsCells = 1u << kClsT;
@@ -395,8 +402,10 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
     answer_queue();
     flush_acc();
     __syncthreads();
+#ifndef DHT_K2_NOHIST   // measurement build: no global histogram atomics (results incomplete)
     for (uint32_t i = threadIdx.x; i < 161; i += kClsBlock)
         if (sh[i]) atomicAdd(hist + i, (unsigned long long)sh[i]);
+#endif
 }
 
 // ---------------------------------------------------------------------------------
