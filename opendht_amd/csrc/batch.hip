@@ -961,10 +961,9 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         const uint32_t G = a.Lm >= 12 ? (mtr <= kF3Threads / 4 ? 4u : mtr <= kF3Threads / 2 ? 2u : 1u) : 1u;
         const uint32_t slot = G == 4 ? threadIdx.x >> 2 : G == 2 ? threadIdx.x >> 1 : lane * NWV + wv;
         const uint32_t gj = threadIdx.x & (G - 1);
-#ifdef DHT_F3_TIE_INLINE
-        uint32_t tq = 0, tt0 = 0, tlo = 0, thi = 0;   // a group leader's tied target, answered inline
+        // one set (no sub-partitions): a group leader's tied target, answered inline by its wave
+        uint32_t tq = 0, tt0 = 0, tlo = 0, thi = 0;
         bool tinl = false;
-#endif
         if (slot < mtr) {   // group-uniform from here on
             const uint2 te = T[slot];
             const uint32_t t0 = te.x, qi = te.y;
@@ -1051,44 +1050,32 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
 #ifdef DHT_F3_NOTIES
                 tie = false;   // measurement build: w0 ties answered as if none (results may be wrong)
 #endif
-#ifdef DHT_F3_TIEDETECT_ONLY
-                tie = tie && a.k == 12345u;   // measurement build: ties detected, never deferred
-#endif
-                if (tie) {
-#ifdef DHT_F3_TIE_INLINE
-                  if (gj == 0) {
-                      tinl = true;
-                      tq = qi;
-                      tt0 = t0;
-                      tlo = lo;
-                      thi = hi;
-                      atomicAdd(ntie + 1, 1u);
-                  }
-                  if (false) {
-#endif
-                    // hand the candidates to F4 (one wave per tie, off this block's critical
-                    // path) while a slot is free and they fit a wave; else phase B here
+                if (tie && !Subs) {
+                    if (gj == 0) {   // answered by the wave below, after the groups' results
+                        tinl = true;
+                        tq = qi;
+                        tt0 = t0;
+                        tlo = lo;
+                        thi = hi;
+                        atomicAdd(ntie + 1, 1u);
+                    }
+                } else if (tie) {
+                    // sub-partitioned calls: hand the candidates to F4 (one wave per tie, off this
+                    // block's critical path) while a slot is free and they fit a wave; else phase B
                     uint32_t tsl = kTieSlots;
                     if (gj == 0) {
                         atomicAdd(ntie + 1, 1u);
-#ifndef DHT_F3_TIE_INPLACE   // measurement build: every tie answered by F3's own wave path (phase B)
                         if (mm <= 64) tsl = atomicAdd(ntie, 1u);
-#endif
                     }
                     if (G > 1) tsl = (uint32_t)__shfl((int)tsl, (int)(lane & ~(G - 1)));
                     if (tsl < kTieSlots) {
                         const uint32_t g = p * kTieSlots + tsl;
                         uint2* dst = a.tie_cand + (uint64_t)g * 64;
-#ifndef DHT_F3_TIE_NOCOPY   // measurement build: candidates not handed over (F4 answers garbage)
                         for (uint32_t o = gj; o < mm; o += G) dst[o] = S[lo + o];
-#endif
                         if (gj == 0) a.tie_hdr[g] = make_uint4(qi, t0, mm, 0u);
                     } else if (gj == 0) {
                         slow[atomicAdd(slow + kF3Threads, 1u)] = slot;
                     }
-#ifdef DHT_F3_TIE_INLINE
-                  }
-#endif
                 } else if (gj == 0) {
                     uint32_t* orow = a.out_idx + (uint64_t)qi * a.k;
                     // LDS reads first, then (shards) all gidx loads together: one wait before
@@ -1170,16 +1157,45 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                 }
             }
         }
-#ifdef DHT_F3_TIE_INLINE
-        // the wave's tied targets, answered by the whole wave right away (one round trip each:
-        // word 1 of the candidates and the target's words) while the block's other waves finish
-        for (uint64_t tb = __ballot(tinl); tb; tb &= tb - 1) {
-            const int L = __ffsll((long long)tb) - 1;
-            f3_wave_answer(a, S, (uint32_t)__builtin_amdgcn_readlane((int)tlo, L),
-                           (uint32_t)__builtin_amdgcn_readlane((int)thi, L), (uint32_t)__builtin_amdgcn_readlane((int)tq, L),
-                           (uint32_t)__builtin_amdgcn_readlane((int)tt0, L), want, lane);
+        // One set: the wave's tied targets, answered by the whole wave right away (one round trip
+        // each: word 1 of the candidates and the target's words) while the block's other waves
+        // finish; ties whose subtrees fit a wave go two at a time (both round trips in flight).
+        // cfg 2: F3 + F4 15.5 + 7.3 -> 18.2 + 4.2 us serial, step 33.9 -> 33.4 us, latency 54 ->
+        // 52 us; the cfg-3 shard keeps the F4 hand-off (F3 38 -> 48 us inline: 0.153 -> 0.162 ms
+        // at two in flight; profiles/r05/o, r05/q)
+        if (!Subs) {
+            uint64_t tb = __ballot(tinl);
+            while (tb) {
+                const int L0 = __ffsll((long long)tb) - 1;
+                tb &= tb - 1;
+                const uint32_t lo0 = (uint32_t)__builtin_amdgcn_readlane((int)tlo, L0);
+                const uint32_t mm0 = (uint32_t)__builtin_amdgcn_readlane((int)thi, L0) - lo0;
+                const uint32_t q0 = (uint32_t)__builtin_amdgcn_readlane((int)tq, L0);
+                const uint32_t t00 = (uint32_t)__builtin_amdgcn_readlane((int)tt0, L0);
+                if (mm0 > 64 || !tb) {
+                    f3_wave_answer(a, S, lo0, lo0 + mm0, q0, t00, want, lane);
+                    continue;
+                }
+                const int L1 = __ffsll((long long)tb) - 1;
+                const uint32_t lo1 = (uint32_t)__builtin_amdgcn_readlane((int)tlo, L1);
+                const uint32_t mm1 = (uint32_t)__builtin_amdgcn_readlane((int)thi, L1) - lo1;
+                if (mm1 > 64) {   // the second one alone, later
+                    f3_wave_answer(a, S, lo0, lo0 + mm0, q0, t00, want, lane);
+                    continue;
+                }
+                tb &= tb - 1;
+                const uint32_t q1 = (uint32_t)__builtin_amdgcn_readlane((int)tq, L1);
+                const uint32_t t01 = (uint32_t)__builtin_amdgcn_readlane((int)tt0, L1);
+                const uint2 c0 = S[lo0 + (lane < mm0 ? lane : 0u)], c1 = S[lo1 + (lane < mm1 ? lane : 0u)];
+                const uint32_t w10 = a.planes[a.stride + (lane < mm0 ? c0.y : 0u)];
+                const uint32_t w11 = a.planes[a.stride + (lane < mm1 ? c1.y : 0u)];
+                uint32_t tw0[DHT_W], tw1[DHT_W];
+                load_target(a.tp, a.ts, q0, tw0);
+                load_target(a.tp, a.ts, q1, tw1);
+                wave_rank_loaded(a, c0, mm0, q0, t00, want, lane, w10, tw0);
+                wave_rank_loaded(a, c1, mm1, q1, t01, want, lane, w11, tw1);
+            }
         }
-#endif
         if (Diag && (a.dbg & 256) && t0i == 0) {   // per wave: the end of its phase-A work
             if (lane == 0) a.stamps[2ull * 8192 * 16 + (uint64_t)blockIdx.x * 16 + wv] = __builtin_amdgcn_s_memrealtime();
         }

@@ -23,7 +23,7 @@ VGPR_CAPS = {
     "k_f4I": 144,                # 139: 3 waves / SIMD
     "k_s1_filterI": 128,
     "k_s2_answerI": 144,
-    "k_classifyE": 96,           # K2 87: 5 waves / SIMD
+    "k_classifyE": 128,          # K2 99: one 1,024-thread workgroup per CU (4 waves / SIMD)
     "k_merge3I": 64,             # 48-52
 }
 
