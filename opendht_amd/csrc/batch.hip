@@ -612,7 +612,7 @@ __host__ __device__ inline uint32_t f3_words(uint32_t nsub) {
 // (word 0 from the LDS stage when the stage holds unshifted words, word 1 where the wave paths
 // loaded it) and a gather from the planes otherwise.  No conversion pass follows K6: the 65,536 x 8
 // gathers of a separate pass cost 23 us on the chain at cfg 2, the pass over the rows F3 left 2 us
-// (profiles/r05/b, r05/f).
+// (profiles/r05/b, r05/g/ablation_f).
 struct RecOut {
     uint32_t* out;            // nullable: q * k * 3 words
     const uint32_t* planes;   // the context's (unshifted) planes; record words of context-local indices
@@ -1162,7 +1162,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         // finish; ties whose subtrees fit a wave go two at a time (both round trips in flight).
         // cfg 2: F3 + F4 15.5 + 7.3 -> 18.2 + 4.2 us serial, step 33.9 -> 33.4 us, latency 54 ->
         // 52 us; the cfg-3 shard keeps the F4 hand-off (F3 38 -> 48 us inline: 0.153 -> 0.162 ms
-        // at two in flight; profiles/r05/o, r05/q)
+        // at two in flight; profiles/r05/experiments/f3_tie_inline*.txt, cfg3_tie_inline.txt)
         if (!Subs) {
             uint64_t tb = __ballot(tinl);
             while (tb) {
@@ -1333,7 +1333,7 @@ __device__ void fb_merge(const F3Args& a, const FbArgs& f, uint32_t g, uint32_t 
 // Record form after a one-split scan role: the wave converts the rows its role just wrote
 // (context-local indices; its own stores, drained, read back at agent scope past the L1) into
 // records from the context's planes.  Writing the records inside the scan's unrolled result loop
-// took F4 from 135 VGPRs to 221 + 752 B of scratch per lane (F4 7.5 -> 25 us, profiles/r05/g).
+// took F4 from 135 VGPRs to 221 + 752 B of scratch per lane (F4 7.5 -> 25 us, profiles/r05/g/probe_scan_rec_stores_221vgpr.json).
 __device__ void fb_rows_to_records(const F3Args& a, uint32_t qb, uint32_t qend) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t lane = lane_id(), k = a.k;

@@ -127,12 +127,12 @@ __global__ __launch_bounds__(256) void k_find_closest(
 // Layout: a wave handles chunks of 64 x kClsU uint4 of word 0 (256 x kClsU ids), lane l the
 // uint4s chunk * 64 kClsU + u * 64 + l, so every load and every 4-B bucket store of a wave is
 // one contiguous 1-KB / 256-B run; the chunk index is wave-uniform (scalar address math).  The
-// next chunk's loads are issued before this chunk's work (two chunks in flight per lane).
+// next two chunks' loads are issued before this chunk's work (three chunks in flight per lane).
 // ---------------------------------------------------------------------------------
 // one 1,024-thread workgroup per CU (16 waves, 4 per SIMD): every workgroup ends with one global
 // atomic per histogram bin it touched, and the 1,024 workgroups of 256 threads ended together with
 // 1,024 atomics on bin 0's address, serialised at the memory side (0.0926 -> 0.088 ms without them,
-// 0.0935 -> 0.0897-0.092 with 256 workgroups of 1,024: profiles/r05/j/k2_blocks.txt)
+// 0.0935 -> 0.0897-0.092 with 256 workgroups of 1,024: profiles/r05/experiments/k2_blocks.txt)
 #ifndef DHT_K2_BLOCK
 #define DHT_K2_BLOCK 1024
 #endif
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
     // unconditional loads (an address past the set is clamped to its last uint4, whose ids are
     // masked): a conditional load made the compiler wait for the look-ahead chunk too (vmcnt(0)
     // at the branch join)
-    // (32-bit index math: the host keeps n < 2^33, so every uint4 index, look-ahead included, < 2^32)
+    // (32-bit index math: the host keeps n < 2^32, so every uint4 index, the two-chunk look-ahead included, < 2^32)
     const uint32_t last4 = (uint32_t)(n4 - 1);
     auto load = [&](uint64_t ch, uint4* v) {
         const uint32_t cb = (uint32_t)(ch * CH) + lane;
@@ -235,6 +235,10 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
     // the first chunk's loads ahead of the setup
     uint4 v[kClsU];
     load(c, v);
+    // three chunks in flight per wave: the next two issued ahead (0.0900-0.0920 -> 0.0893-0.0896
+    // ms against one ahead, profiles/r05/experiments/k2_depth.txt; 6 of the 128 VGPRs the 16 waves per CU allow)
+    uint4 v2[kClsU];
+    load(c + W, v2);
     for (uint32_t i = threadIdx.x; i < DHT_W * nb; i += kClsBlock) sf[i] = fp[i];
     for (uint32_t i = threadIdx.x; i < 161; i += kClsBlock) sh[i] = 0;
     if (threadIdx.x < 4) s_map[threadIdx.x] = 0u;
@@ -388,13 +392,13 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
     auto stream = [&](auto regs_c) {
         for (; c < nch; c += W) {   // wave-uniform
             uint4 nx[kClsU];
-            load(c + W, nx);
+            load(c + 2 * W, nx);
             if (c < nfull) chunk(std::true_type{}, regs_c);
             else chunk(std::false_type{}, regs_c);
             // room for the next chunk's ids in the queue (wave-uniform)
             if (__builtin_amdgcn_readfirstlane(s_qn[wv]) > kClsQCap - 4 * CH) answer_queue();
 #pragma unroll
-            for (uint32_t u = 0; u < kClsU; ++u) v[u] = nx[u];
+            for (uint32_t u = 0; u < kClsU; ++u) { v[u] = v2[u]; v2[u] = nx[u]; }
         }
     };
     if (regs) stream(std::true_type{});
