@@ -1063,11 +1063,18 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                     // sub-partitioned calls: hand the candidates to F4 (one wave per tie, off this
                     // block's critical path) while a slot is free and they fit a wave; else phase B
                     uint32_t tsl = kTieSlots;
-                    if (gj == 0) {
-                        atomicAdd(ntie + 1, 1u);
-                        if (mm <= 64) tsl = atomicAdd(ntie, 1u);
+                    {   // slots for the wave's tied groups at once: one LDS atomic, ranks by ballot
+                        const uint64_t want_slot = __ballot(gj == 0 && mm <= 64), leaders = __ballot(gj == 0);
+                        const uint32_t first = (uint32_t)__ffsll((long long)leaders) - 1;
+                        uint32_t base = 0;
+                        if (lane == first) {
+                            atomicAdd(ntie + 1, (uint32_t)__popcll(leaders));
+                            if (want_slot) base = atomicAdd(ntie, (uint32_t)__popcll(want_slot));
+                        }
+                        base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
+                        const uint32_t leader = lane & ~(G - 1);
+                        if (mm <= 64) tsl = base + (uint32_t)__popcll(want_slot & ((1ull << leader) - 1ull));
                     }
-                    if (G > 1) tsl = (uint32_t)__shfl((int)tsl, (int)(lane & ~(G - 1)));
                     if (tsl < kTieSlots) {
                         const uint32_t g = p * kTieSlots + tsl;
                         uint2* dst = a.tie_cand + (uint64_t)g * 64;
