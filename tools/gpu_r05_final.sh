@@ -2,9 +2,13 @@
 # baseline), the 1,000-step headline, the 2-rank rehearsal of the N > 1 default (gloo, one GPU), the
 # RCCL collective path as a world of one, rocprofv3 kernel traces (driver-shaped bench, K2, cfg-3
 # shard) and PMC FETCH/WRITE passes (cfg 2 warm / cold, cfg-3 shard, K2).   usage: bash tools/gpu_r05_final.sh [tag]
+# PART=a: suite, smoke, benches, rehearsals, shard probe; PART=b: kernel traces + PMC passes
+# (two gpurun calls, each well inside one call's limit).
 set -o pipefail
 OUT=gpurun_out/${1:-r05final}; mkdir -p $OUT
 export TMPDIR=/tmp
+PART=${PART:-a}
+if [ "$PART" = a ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations=12 > $OUT/gpu_tests.log 2>&1 || { tail -40 $OUT/gpu_tests.log; exit 1; }
 tail -1 $OUT/gpu_tests.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
@@ -16,6 +20,20 @@ timeout -k 10 300 python bench.py --sharded --steps 20 --warmup 5 --verify 64 > 
 timeout -k 10 300 python bench.py --sharded --steps 1000 --warmup 100 --no-cpu --no-extra --verify 64 > $OUT/sharded_1000.json 2> $OUT/sharded_1000.err || { tail -20 $OUT/sharded_1000.err; exit 1; }
 timeout -k 10 400 python tools/experiments/rehearse_cfg3.py > $OUT/rehearse_cfg3.json 2> $OUT/rehearse_cfg3.err || { tail -20 $OUT/rehearse_cfg3.err; exit 1; }
 timeout -k 10 300 python tools/shard_probe.py > $OUT/shard_probe.json 2> $OUT/shard_probe.err || { tail -20 $OUT/shard_probe.err; exit 1; }
+python3 - $OUT <<'PY'
+import json, sys
+o = sys.argv[1]
+for f in ("bench_driver", "bench1000", "sharded_allgather", "sharded_1000"):
+    d = json.loads([l for l in open(f"{o}/{f}.json") if l.startswith("{")][-1])
+    print(f, round(d["ms_per_step"] * 1e3, 2), "us/step", round(d["value"] / 1e9, 4), "G q/s, F2 frac",
+          round(d["roofline"]["frac"], 3), "lat", round(d["latency_ms_per_batch"] * 1e3, 1), "verified", d.get("verified_exact"))
+r = [json.loads(l) for l in open(f"{o}/rehearse_2ranks.json") if l.startswith("{")]
+print("rehearsal", [(x.get("n_gpus"), x["config"]["route"], x["config"]["n_ids"], x["scaling"], x.get("verified_exact"),
+                     {k: (v.get("ms_per_step"), v.get("equals_headline_rank0")) for k, v in x.items() if k in ("broadcast_alltoall", "prefix_weak")}) for x in r])
+PY
+echo all-ok
+exit 0
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt_bench20 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-extra --no-scan > $OUT/kt_bench20.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt_k2 -o run --output-format csv -- python3 tools/classify_probe.py --reps 20 > $OUT/kt_k2.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt_cfg3 -o run --output-format csv -- python3 tools/batch_probe.py --reps 20 --n 134217728 --q 131072 > $OUT/kt_cfg3.log 2>&1 || exit 1
@@ -33,13 +51,6 @@ pmc k2 "cfg4:100000000" python3 tools/classify_probe.py --reps 3 || exit 1
 python3 - $OUT <<'PY'
 import csv, glob, json, sys
 o = sys.argv[1]
-for f in ("bench_driver", "bench1000", "sharded_allgather", "sharded_1000"):
-    d = json.loads([l for l in open(f"{o}/{f}.json") if l.startswith("{")][-1])
-    print(f, round(d["ms_per_step"] * 1e3, 2), "us/step", round(d["value"] / 1e9, 4), "G q/s, F2 frac",
-          round(d["roofline"]["frac"], 3), "lat", round(d["latency_ms_per_batch"] * 1e3, 1), "verified", d.get("verified_exact"))
-r = [json.loads(l) for l in open(f"{o}/rehearse_2ranks.json") if l.startswith("{")]
-print("rehearsal", [(x.get("n_gpus"), x["config"]["route"], x["config"]["n_ids"], x["scaling"], x.get("verified_exact"),
-                     {k: (v.get("ms_per_step"), v.get("equals_headline_rank0")) for k, v in x.items() if k in ("broadcast_alltoall", "prefix_weak")}) for x in r])
 for k in ("kt_bench20", "kt_k2", "kt_cfg3"):
     f = glob.glob(f"{o}/{k}/**/*kernel_stats.csv", recursive=True)[0]
     for row in csv.DictReader(open(f)):
