@@ -208,7 +208,7 @@ HBM_PEAK_GBS = 8000.0
 # 64-bit lane; both fractions are reported (the packed prefilter is an algorithmic win).
 OPS_PER_PAIR = 1.0
 SURVEY_OPS_PER_PAIR = 3.0
-PMC_FILE = "profiles/r04/pmc_traffic.json"
+PMC_FILE = "profiles/r05/pmc_traffic.json"
 
 
 def oracle():
