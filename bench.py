@@ -977,10 +977,39 @@ def cfg3_shard_leg(a, L, dev, stream, tstream):
                "persistent_state": "the 8 prefix sub-partitions (compacted copies with their shifted word-0 planes "
                                    "and index maps, 28 B/id) are built by the first call (setup_first_call_s) and kept "
                                    "across calls; every timed call streams all 2^27 word-0 entries"}
+        got_idx = outs[(steps - 1) % 2][0].clone()
+        # the same calls returning sub-partition handles (dhtgpu_set_sub_handles: no index-map read
+        # per result), mapped back to global indices after the window for the check
+        c.set_sub_handles(True)
+        for i in range(4):
+            c.batch_topk_dev(tp.data_ptr(), ts, q, k, outs[i % 2][0].data_ptr(), outs[i % 2][1].data_ptr(), None, 0,
+                             st2[i % 2].cuda_stream)
+        ms_h = window(2)
+        evh = EvSets(reps, tstream)
+        for i in range(reps):
+            evh.arm(c)
+            c.batch_topk_dev(tp.data_ptr(), ts, q, k, outs[0][0].data_ptr(), outs[0][1].data_ptr(), None, 0,
+                             tstream.cuda_stream)
+        torch.cuda.synchronize()
+        hk = evh.mean_ms()
+        mapped = torch.empty_like(outs[0][0])
+        c.handles_to_indices_dev(outs[0][0].data_ptr(), q * k, mapped.data_ptr(), 0, stream)
+        torch.cuda.synchronize()
+        c.set_sub_handles(False)
+        f3alg = kern["k_f3_answer"][1]
+        res["handles"] = {"ms_per_step": ms_h, "qps": q / (ms_h * 1e-3), "inflight": 2,
+                          "kernels_ms": dict(zip(["k_f1_targets", "k_f2_filter", "k_f3_answer", "k_f4_fallback"], hk)),
+                          "f3_alg_bytes_per_launch": f3alg,
+                          "f3_traffic_bytes_per_launch": pmc_traffic(f"cfg3shard:{n}x{q}x{k}:handles", "k_f3_answer"),
+                          "f3_traffic_bytes_per_launch_indices": pmc_traffic(f"cfg3shard:{n}x{q}x{k}", "k_f3_answer"),
+                          "mapped_equal_indices": bool(torch.equal(mapped, got_idx)),
+                          "note": "results as sub-partition handles (offset of the id's sub-partition + its place "
+                                  "there), mapped to global indices on request (dhtgpu_handles_to_indices_dev); "
+                                  "ms_per_step above returns indices"}
         if not a.no_cpu:
             O = oracle()
             rows = np.arange(0, q, q // 16)
-            got = outs[(steps - 1) % 2][0].cpu().numpy().view(np.uint32)[rows]
+            got = got_idx.cpu().numpy().view(np.uint32)[rows]
             want, _ = O.topk(O.gen_ids(a.seed + 3, n), O.gen_ids(a.seed + 4, q)[rows], k, threads=usable_cpus())
             res["verified_targets"] = int(rows.size)
             res["verified_exact"] = bool(np.array_equal(got, want))

@@ -91,6 +91,20 @@ int dhtgpu_gen_ids_prefix(dhtgpu_ctx* ctx, uint64_t seed, uint64_t start, uint64
  * (positions in get_ids order) -- the handle a rank that owns its shard's node table
  * keeps, without the per-result gather through the index map. */
 int dhtgpu_set_global_indices(dhtgpu_ctx* ctx, int on);
+/* Sets too large for one K6 plan (e.g. a 2^27-id shard) are answered over prefix
+ * sub-partitions, compacted copies in id order.  on != 0 makes such calls return
+ * sub-partition handles instead of indices: handle = the sub-partition's offset + the id's
+ * position in it (one handle per id, in [0, n)), saving the per-result read of the index map
+ * (10 us of the cfg-3 shard's 0.15 ms).  Record form (out_rec) is unaffected.
+ * dhtgpu_sub_handles_active tells whether a call of q targets at k returns handles (only
+ * sub-partitioned calls do); dhtgpu_handles_to_indices_dev maps m handles to the indices the
+ * call would have returned (global stream indices per dhtgpu_set_global_indices, else
+ * context-local + idx_base); DHTGPU_NONE stays.  The handle space is the one the last
+ * sub-partitioned call used (it changes with the id set). */
+int dhtgpu_set_sub_handles(dhtgpu_ctx* ctx, int on);
+int dhtgpu_sub_handles_active(dhtgpu_ctx* ctx, uint32_t q, uint32_t k);
+int dhtgpu_handles_to_indices_dev(dhtgpu_ctx* ctx, const uint32_t* handles, uint64_t m, uint32_t* out_idx,
+                                  uint32_t idx_base, void* stream);
 uint64_t dhtgpu_num_ids(const dhtgpu_ctx* ctx);
 /* Read back ids [first, first+n) as 20-byte big-endian. */
 int dhtgpu_get_ids(dhtgpu_ctx* ctx, uint64_t first, uint64_t n, uint8_t* out20_be);

@@ -68,6 +68,9 @@ def lib():
         "dhtgpu_gen_ids": ([_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64], ctypes.c_int),
         "dhtgpu_num_ids": ([_vp], ctypes.c_uint64),
         "dhtgpu_set_global_indices": ([_vp, ctypes.c_int], ctypes.c_int),
+        "dhtgpu_set_sub_handles": ([_vp, ctypes.c_int], ctypes.c_int),
+        "dhtgpu_sub_handles_active": ([_vp, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
+        "dhtgpu_handles_to_indices_dev": ([_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp], ctypes.c_int),
         "dhtgpu_set_search_alpha": ([_vp, ctypes.c_uint32], ctypes.c_int),
         "dhtgpu_get_ids": ([_vp, ctypes.c_uint64, ctypes.c_uint64, _u8p], ctypes.c_int),
         "dhtgpu_ids_dev": ([_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
@@ -145,7 +148,8 @@ def exported_symbols():
             "dhtgpu_index_build_timed", "dhtgpu_gen_ids_prefix", "dhtgpu_select_prefix_dev",
             "dhtgpu_batch_topk_dev", "dhtgpu_batch_topk_timed", "dhtgpu_batch_topk", "dhtgpu_table_depth",
             "dhtgpu_buffer_nodes_dev", "dhtgpu_buffer_nodes", "dhtgpu_deserialize_nodes", "dhtgpu_net_prepare",
-            "dhtgpu_search_batch", "dhtgpu_search_batch_dev", "dhtgpu_set_global_indices", "dhtgpu_set_search_alpha", "dhtgpu_cache_set",
+            "dhtgpu_search_batch", "dhtgpu_search_batch_dev", "dhtgpu_set_global_indices", "dhtgpu_set_sub_handles",
+            "dhtgpu_sub_handles_active", "dhtgpu_handles_to_indices_dev", "dhtgpu_set_search_alpha", "dhtgpu_cache_set",
             "dhtgpu_cache_nodes", "dhtgpu_cache_sorted", "dhtgpu_buffer_nodes_ids", "dhtgpu_batch_events",
             "dhtgpu_search_insert", "dhtgpu_table_stats"]
 
@@ -214,6 +218,20 @@ class Context:
     def set_global_indices(self, on):
         """Prefix shards: results as global stream indices (True, default) or shard-local."""
         _check(lib().dhtgpu_set_global_indices(self._h, int(bool(on))), "set_global_indices")
+
+    def set_sub_handles(self, on):
+        """Sub-partitioned calls (sets one K6 plan cannot serve) return sub-partition handles
+        instead of indices (no per-result index-map read); see include/dhtgpu.h."""
+        _check(lib().dhtgpu_set_sub_handles(self._h, int(bool(on))), "set_sub_handles")
+
+    def sub_handles_active(self, q, k):
+        """True when a call of q targets at k returns handles."""
+        return bool(lib().dhtgpu_sub_handles_active(self._h, q, k))
+
+    def handles_to_indices_dev(self, handles_ptr, m, out_ptr, idx_base=0, stream=None):
+        """m handles -> the indices the call would have returned (device pointers)."""
+        _check(lib().dhtgpu_handles_to_indices_dev(self._h, handles_ptr, m, out_ptr, idx_base, stream),
+               "handles_to_indices_dev")
 
     def select_prefix_dev(self, planes_ptr, stride, n, pbits, pval, out_planes_ptr, out_stride, out_gidx_ptr=None,
                           stream=None):

@@ -126,6 +126,10 @@ struct dhtgpu_ctx {
     std::vector<SubPart> subs;
     uint32_t sub_bits = 0;
     bool subs_valid = false;
+    // dhtgpu_set_sub_handles: sub-partitioned calls return handles (a sub-partition's offset +
+    // its compacted index), no index-map read per result; sub_tab maps them back on request
+    bool sub_handles = false;
+    DevBuf sub_tab;   // HandleSub[subs.size()], built with the sub-partitions
     uint32_t shard_pval = 0;
     // lexicographically sorted views (sort.hip): of the main set when it was uploaded unsorted
     // (built on the first cached_nodes call), and the NodeCache mirror (dhtgpu_cache_set)
@@ -154,6 +158,7 @@ struct dhtgpu_ctx {
         for (auto& sp : subs)
             for (DevBuf* b : {&sp.planes, &sp.map, &sp.gmap, &sp.w0s}) b->release();
         subs.clear();
+        sub_tab.release();
         sub_bits = 0;
     }
 
@@ -353,6 +358,31 @@ int dhtgpu_gen_ids_prefix(dhtgpu_ctx* c, uint64_t seed, uint64_t start, uint64_t
 int dhtgpu_set_global_indices(dhtgpu_ctx* c, int on) {
     if (!c) return DHTGPU_EINVAL;
     c->map_global = on != 0;
+    return DHTGPU_OK;
+}
+
+int dhtgpu_set_sub_handles(dhtgpu_ctx* c, int on) {
+    if (!c) return DHTGPU_EINVAL;
+    c->sub_handles = on != 0;
+    return DHTGPU_OK;
+}
+
+static bool needs_subs(const dhtgpu_ctx* c, uint32_t q, uint32_t k);
+
+int dhtgpu_sub_handles_active(dhtgpu_ctx* c, uint32_t q, uint32_t k) {
+    if (!c || !c->has_ids) return 0;
+    return c->sub_handles && !(small_supported(c->n, q, k) && !(c->dbg & (1u << 23))) && needs_subs(c, q, k) ? 1 : 0;
+}
+
+int dhtgpu_handles_to_indices_dev(dhtgpu_ctx* c, const uint32_t* handles, uint64_t m, uint32_t* out_idx,
+                                  uint32_t idx_base, void* stream) {
+    if (!c || (m && (!handles || !out_idx))) return DHTGPU_EINVAL;
+    if (!c->subs_valid) return DHTGPU_EINVAL;   // no sub-partitioned call has built the handle space
+    if (!m) return DHTGPU_OK;
+    DHT_TRY(c->bind());
+    const bool global = c->has_gidx && c->map_global;
+    DHT_TRY(launch_handles_to_idx(c->sub_tab.as<HandleSub>(), (uint32_t)c->subs.size(), handles, m, out_idx, global,
+                                  global ? 0u : idx_base, stream ? (hipStream_t)stream : c->stream));
     return DHTGPU_OK;
 }
 
@@ -697,6 +727,15 @@ static int build_subs(dhtgpu_ctx* c) {
             DHT_TRY(launch_map_idx(sp.gmap.as<uint32_t>(), m, c->gidx.as<uint32_t>(), 0, s));
         }
     }
+    std::vector<HandleSub> tab(c->subs.size());
+    uint64_t off = 0;
+    for (size_t i = 0; i < tab.size(); ++i) {
+        const dhtgpu_ctx::SubPart& sp = c->subs[i];
+        tab[i] = HandleSub{sp.n, sp.map.as<uint32_t>(), c->has_gidx ? sp.gmap.as<uint32_t>() : nullptr, (uint32_t)off, 0u};
+        off += sp.n;
+    }
+    DHT_TRY(c->sub_tab.ensure(tab.size() * sizeof(HandleSub)));
+    DHT_TRY(hipMemcpyAsync(c->sub_tab.p, tab.data(), tab.size() * sizeof(HandleSub), hipMemcpyHostToDevice, s));
     DHT_TRY(hipStreamSynchronize(s));
     c->sub_bits = sb;
     c->subs_valid = true;
@@ -718,9 +757,20 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     const uint32_t q_plan = std::max<uint32_t>(1u, (uint32_t)(((uint64_t)q + S - 1) >> sb));
     uint64_t n_max = 0;
     for (const auto& sp : c->subs) n_max = std::max<uint64_t>(n_max, sp.n);
-    if (!batch_supported(n_max, q_plan, k, c->num_cus, S))
-        return dhtgpu_topk_dev(c, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s);
-    const bool global = c->has_gidx && c->map_global && !out_rec;
+    const bool handles = c->sub_handles && !out_rec;
+    if (!batch_supported(n_max, q_plan, k, c->num_cus, S)) {
+        if (!handles) return dhtgpu_topk_dev(c, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s);
+        // handles on the K1 route: context-local indices, then their handles
+        const bool mg = c->map_global;
+        c->map_global = false;
+        r = dhtgpu_topk_dev(c, tp, ts, q, k, out_idx, out_cnt, nullptr, 0, s);
+        c->map_global = mg;
+        if (r) return r;
+        DHT_TRY(launch_idx_to_handles(c->sub_tab.as<HandleSub>(), c->planes.as<uint32_t>(), c->shard_pbits, sb, out_idx,
+                                      (uint64_t)q * k, s));
+        return DHTGPU_OK;
+    }
+    const bool global = !handles && c->has_gidx && c->map_global && !out_rec;
     const int si = pick_slot(c, s);
     dhtgpu_ctx::BatchSlot& b = c->bslot[si];
     // record form: the index rows are scratch (K6 stores the records themselves)
@@ -733,10 +783,13 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
         lc = b.out_cnt.as<uint32_t>();
     }
     std::vector<SubSpec> specs(S);
+    uint64_t off = 0;
     for (uint32_t i = 0; i < S; ++i) {
         const dhtgpu_ctx::SubPart& sp = c->subs[i];
         specs[i] = SubSpec{sp.planes.as<uint32_t>(), sp.w0s.as<uint32_t>(), sp.stride, sp.n,
-                           global ? sp.gmap.as<uint32_t>() : sp.map.as<uint32_t>(), 0u};
+                           handles ? nullptr : global ? sp.gmap.as<uint32_t>() : sp.map.as<uint32_t>(),
+                           handles ? (uint32_t)off : 0u, sp.map.as<uint32_t>()};
+        off += sp.n;
     }
     BatchCall bc{};
     bc.planes = c->planes.as<uint32_t>();   // F4's scan: the whole set
@@ -762,9 +815,10 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     bc.out_rec = out_rec;   // every K6 writer of a row stores its records
     bc.rec_gidx = c->out_map();
     bc.rec_base = idx_base;
+    bc.handles = handles ? 1u : 0u;
     r = batch_slot_run(c, si, bc, s, ev);
     if (r) return r;
-    if (!out_rec && !global && idx_base) {   // (record form: K6 wrote the records)
+    if (!out_rec && !handles && !global && idx_base) {   // (record form: K6 wrote the records)
         DHT_TRY(launch_map_idx(out_idx, (uint64_t)q * k, nullptr, idx_base, s));
     }
     return DHTGPU_OK;

@@ -178,6 +178,7 @@ struct SubDesc {
     uint32_t lim;             // last 16-B aligned word offset loadable inside w0's allocation
     uint32_t blk0, nblk;      // its F2 workgroups
     uint64_t per_blk;         // F2 ids per workgroup
+    const uint32_t* cmap;     // sub-local -> context-local index, ascending (handle conversion)
 };
 
 struct F1Args {
@@ -581,6 +582,22 @@ __device__ __forceinline__ uint32_t map_out(uint32_t x, const uint32_t* __restri
     return gidx ? gidx[x] : x + base;
 }
 
+// Sub-partition handles: the handle of context-local index x (what F4's whole-set scans write) --
+// its sub-partition from its word 0, its place there by a binary search in that sub-partition's
+// ascending index map (rare rows: targets whose own sub-partition holds fewer than k ids)
+__device__ uint32_t to_handle(const uint32_t* __restrict__ planes, const SubDesc* subs, uint32_t hshift, uint32_t hbits,
+                              uint32_t x) {
+    if (x == DHT_NONE) return x;
+    const uint32_t s = __builtin_amdgcn_ubfe(planes[x], 32u - hshift - hbits, hbits);
+    const uint32_t* __restrict__ m = subs[s].cmap;
+    uint64_t lo = 0, hi = subs[s].n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (m[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    return subs[s].base + (uint32_t)lo;
+}
+
 __device__ __forceinline__ void load_target(const uint32_t* __restrict__ tp, uint64_t ts, uint32_t qi, uint32_t* t) {
 #pragma unroll
     for (int j = 0; j < DHT_W; ++j) t[j] = __builtin_amdgcn_readfirstlane(tp[(uint64_t)j * ts + qi]);
@@ -662,6 +679,8 @@ struct F3Args {
     unsigned long long* stamps;          // dbg & 256: per-block phase timestamps [np][16]
     uint32_t cap;                        // LDS stage entries (the plan's, <= kF3Cap)
     RecOut rec;                          // record form: F3's fast path writes compact records itself
+    uint32_t h_conv;                     // sub-partition handles: convert context-local results (whole-set roles)
+    uint32_t hshift, hbits;              // an id's sub-partition: word-0 bits [hshift, hshift + hbits)
 };
 
 // (w0 distance, w1 distance, index) order; words 2..4 are read only when both distances tie
@@ -1320,6 +1339,8 @@ __device__ void fb_merge(const F3Args& a, const FbArgs& f, uint32_t g, uint32_t 
             if (lane == 0) {
                 if (a.rec.out)   // record form: word 0 back from the distance, word 1 read
                     rec_place(a.rec, a.planes, a.gidx, a.base, k, qr, r, wi, m ^ t[0], true, a.planes[a.stride + wi]);
+                else if (a.h_conv)   // a whole-set role under sub-partition handles
+                    orow[r] = to_handle(a.planes, a.subs, a.hshift, a.hbits, map_out(wi, a.gidx, a.base));
                 else
                     orow[r] = map_out(wi, a.gidx, a.base);
             }
@@ -1350,6 +1371,19 @@ __device__ void fb_rows_to_records(const F3Args& a, uint32_t qb, uint32_t qend) 
         const uint32_t qr = a.fb_list[qb + j];
         const uint32_t x = ld_sc1(a.out_idx + (uint64_t)qr * k + r);
         rec_place(a.rec, a.rec.planes, nullptr, 0u, k, qr, r, x, 0u, false, x == DHT_NONE ? 0u : a.rec.planes[a.rec.stride + x]);
+    }
+}
+
+// Sub-partition handles after a one-split whole-set scan role: the wave converts the rows its
+// role just wrote (context-local indices, its own stores drained, read back at agent scope).
+__device__ void fb_rows_to_handles(const F3Args& a, uint32_t qb, uint32_t qend) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t lane = lane_id(), k = a.k;
+    const uint32_t nt = qend > qb ? (qend - qb < kScanTargets ? qend - qb : kScanTargets) : 0u;
+    for (uint32_t c = lane; c < nt * k; c += 64) {
+        const uint32_t j = c / k, r = c - j * k;
+        uint32_t* p = a.out_idx + (uint64_t)a.fb_list[qb + j] * k + r;
+        *p = to_handle(a.planes, a.subs, a.hshift, a.hbits, ld_sc1(p));
     }
 }
 
@@ -1393,6 +1427,7 @@ __device__ __forceinline__ void fb_list_scan(const F3Args& a, const FbArgs& f, u
                     as.n = d.n;
                     as.gidx = d.gidx;
                     as.base = d.base;
+                    as.h_conv = 0;   // a sub-partition's own results are handles already
                 }
             }
         }
@@ -1409,6 +1444,7 @@ __device__ __forceinline__ void fb_list_scan(const F3Args& a, const FbArgs& f, u
                                         single ? g + 1 : cnt, as.k, o);
         if (S == 1) {
             if (a.rec.out) fb_rows_to_records(a, qb, single ? g + 1 : cnt);
+            else if (as.h_conv) fb_rows_to_handles(as, qb, single ? g + 1 : cnt);
             continue;
         }
         // hand-off: every wave's sc1 record stores drained, then one agent-scope add per block;
@@ -1892,7 +1928,8 @@ uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, 
         const uint64_t nb = n ? (n + per - 1) / per : 0;
         const uint64_t lim = (subs[i].w0s ? subs[i].stride : 5 * subs[i].stride) - 4;
         d[i] = SubDesc{subs[i].w0s ? subs[i].w0s : subs[i].planes, subs[i].planes, subs[i].stride, n, subs[i].gidx,
-                       subs[i].base, (uint32_t)(lim < 0xFFFFFFF0ull ? lim : 0xFFFFFFF0ull), blk, (uint32_t)nb, per};
+                       subs[i].base, (uint32_t)(lim < 0xFFFFFFF0ull ? lim : 0xFFFFFFF0ull), blk, (uint32_t)nb, per,
+                       subs[i].cmap};
         blk += (uint32_t)nb;
     }
     return blk;
@@ -1943,6 +1980,56 @@ __global__ void k_shift_w0(const uint32_t* __restrict__ planes, uint64_t stride,
 hipError_t launch_shift_w0(const uint32_t* planes, uint64_t stride, uint32_t shift, uint32_t* out, hipStream_t s) {
     if (shift == 0 || shift >= 32) return hipErrorInvalidValue;
     k_shift_w0<<<dim3((uint32_t)((stride + 255) / 256)), dim3(256), 0, s>>>(planes, stride, shift, out);
+    return hipGetLastError();
+}
+
+// Sub-partition handles <-> indices (dhtgpu_handles_to_indices_dev; the K1 route of a
+// sub-partitioned call under handles).  tab: the context's sub-partitions, offsets ascending.
+__global__ void k_handles_to_idx(const HandleSub* __restrict__ tab, uint32_t nsub, const uint32_t* __restrict__ h,
+                                 uint64_t m, uint32_t* __restrict__ out, uint32_t global, uint32_t base) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t x = h[i];
+    uint32_t r = DHT_NONE;
+    if (x != DHT_NONE) {
+        uint32_t lo = 0, hi = nsub;   // the last sub-partition whose offset <= x
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (tab[mid].off <= x) lo = mid; else hi = mid;
+        }
+        const HandleSub t = tab[lo];
+        const uint64_t j = x - t.off;
+        if (j < t.n) r = global ? t.gmap[j] : t.map[j] + base;
+    }
+    out[i] = r;
+}
+
+__global__ void k_idx_to_handles(const HandleSub* __restrict__ tab, const uint32_t* __restrict__ planes, uint32_t hshift,
+                                 uint32_t hbits, uint32_t* __restrict__ idx, uint64_t m) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t x = idx[i];
+    if (x == DHT_NONE) return;
+    const HandleSub t = tab[__builtin_amdgcn_ubfe(planes[x], 32u - hshift - hbits, hbits)];
+    uint64_t lo = 0, hi = t.n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (t.map[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    idx[i] = t.off + (uint32_t)lo;
+}
+
+hipError_t launch_handles_to_idx(const HandleSub* tab, uint32_t nsub, const uint32_t* h, uint64_t m, uint32_t* out,
+                                 bool global, uint32_t base, hipStream_t s) {
+    if (!m) return hipSuccess;
+    k_handles_to_idx<<<dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s>>>(tab, nsub, h, m, out, global ? 1u : 0u, base);
+    return hipGetLastError();
+}
+
+hipError_t launch_idx_to_handles(const HandleSub* tab, const uint32_t* planes, uint32_t hshift, uint32_t hbits,
+                                 uint32_t* idx, uint64_t m, hipStream_t s) {
+    if (!m) return hipSuccess;
+    k_idx_to_handles<<<dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s>>>(tab, planes, hshift, hbits, idx, m);
     return hipGetLastError();
 }
 
@@ -2082,6 +2169,9 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
              d_desc, np, dbg, stamps, narrow ? P.f3cap : P.f3cap_wide, RecOut{}};
     if (c.out_rec)
         a.rec = RecOut{c.out_rec, c.planes, c.stride, c.rec_gidx, c.rec_base, (nsub == 1 && !c.w0s && !c.skip) ? 1u : 0u};
+    a.h_conv = (c.handles && nsub > 1 && !c.out_rec) ? 1u : 0u;
+    a.hshift = c.sub_shift;
+    a.hbits = c.sub_bits;
     // F3 stages the plan's 6-sigma bound only beside F2's narrow stage (which it makes room for)
     size_t l3 = f3_lds(P, a.cap);
     if (dbg & 4096) l3 = l3 > 81920 ? l3 : 81920;   // experiment: 2 F3 blocks per CU

@@ -134,7 +134,22 @@ struct SubSpec {
     const uint32_t* planes; const uint32_t* w0s;   // unshifted planes; shifted word-0 plane (nullable)
     uint64_t stride, n;
     const uint32_t* gidx; uint32_t base;           // result index map (nullable) or offset
+    const uint32_t* cmap;                          // sub-local -> context-local index, ascending (nullable)
 };
+
+// One sub-partition in handle space: handles [off, off + n) name its ids in its compacted order.
+struct HandleSub {
+    uint64_t n;
+    const uint32_t* map;    // sub-local -> context-local, ascending
+    const uint32_t* gmap;   // sub-local -> global stream index (nullable: no global map)
+    uint32_t off, pad;
+};
+// out[i] = the index handle h[i] names: gmap (global) or map + base; DHT_NONE stays
+hipError_t launch_handles_to_idx(const HandleSub* tab, uint32_t nsub, const uint32_t* h, uint64_t m, uint32_t* out,
+                                 bool global, uint32_t base, hipStream_t s);
+// idx[i] (context-local) -> its handle in place (its sub-partition from word-0 bits [hshift, +hbits))
+hipError_t launch_idx_to_handles(const HandleSub* tab, const uint32_t* planes, uint32_t hshift, uint32_t hbits,
+                                 uint32_t* idx, uint64_t m, hipStream_t s);
 
 struct BatchCall {
     void* ws;                              // workspace (batch_bytes), head zero (batch_clean_bytes)
@@ -153,6 +168,10 @@ struct BatchCall {
     // merge) stores the row's compact records instead of its indices; rec_gidx / rec_base map the
     // context-local index to the record's global index
     uint32_t* out_rec; const uint32_t* rec_gidx; uint32_t rec_base;
+    // sub-partition handles (nsub > 1, dhtgpu_set_sub_handles): every sub-partition's results are
+    // its base + sub-local index (SubSpec gidx null, base = the sub-partition's offset), and rows
+    // F4 answers from the whole set (context-local indices) are converted to handles in place
+    uint32_t handles;
     int num_cus;
     uint32_t dbg;                          // DHTGPU_DBG diagnostics switches (0 in production)
     const volatile uint32_t* fb_hint;      // nullable: the slot's last fallback-list length (mapped host memory)

@@ -18,6 +18,7 @@ ap.add_argument("--algo", default="batch")
 ap.add_argument("--prefix", type=int, default=0, help="prefix shard: keep ids with top PREFIX bits == 0 of 2^PREFIX x n")
 ap.add_argument("--evict", action="store_true", help="write 512 MiB before every call (Infinity Cache evicted)")
 ap.add_argument("--inflight", type=int, default=1, help="calls alternate over this many streams")
+ap.add_argument("--handles", action="store_true", help="sub-partitioned calls return sub-partition handles")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
@@ -31,6 +32,8 @@ if a.prefix:
 else:
     ctx.gen_ids(2024, a.n)
 print("ids", ctx.num_ids, flush=True)
+if a.handles:
+    ctx.set_sub_handles(True)
 ts = (a.q + 63) // 64 * 64
 tp = torch.empty(5 * ts, dtype=torch.int32, device=dev)
 assert L.dhtgpu_gen_dev(2025, 0, a.q, tp.data_ptr(), ts, s) == 0
