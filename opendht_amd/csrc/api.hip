@@ -788,7 +788,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
         const dhtgpu_ctx::SubPart& sp = c->subs[i];
         specs[i] = SubSpec{sp.planes.as<uint32_t>(), sp.w0s.as<uint32_t>(), sp.stride, sp.n,
                            handles ? nullptr : global ? sp.gmap.as<uint32_t>() : sp.map.as<uint32_t>(),
-                           handles ? (uint32_t)off : 0u, sp.map.as<uint32_t>()};
+                           handles ? (uint32_t)off : 0u};
         off += sp.n;
     }
     BatchCall bc{};
@@ -816,6 +816,8 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     bc.rec_gidx = c->out_map();
     bc.rec_base = idx_base;
     bc.handles = handles ? 1u : 0u;
+    bc.htab = c->sub_tab.as<HandleSub>();
+    if (handles) bc.base = kHandleMark;   // whole-set fallback rows, marked for the pass after F4
     r = batch_slot_run(c, si, bc, s, ev);
     if (r) return r;
     if (!out_rec && !handles && !global && idx_base) {   // (record form: K6 wrote the records)

@@ -178,7 +178,6 @@ struct SubDesc {
     uint32_t lim;             // last 16-B aligned word offset loadable inside w0's allocation
     uint32_t blk0, nblk;      // its F2 workgroups
     uint64_t per_blk;         // F2 ids per workgroup
-    const uint32_t* cmap;     // sub-local -> context-local index, ascending (handle conversion)
 };
 
 struct F1Args {
@@ -582,21 +581,6 @@ __device__ __forceinline__ uint32_t map_out(uint32_t x, const uint32_t* __restri
     return gidx ? gidx[x] : x + base;
 }
 
-// Sub-partition handles: the handle of context-local index x (what F4's whole-set scans write) --
-// its sub-partition from its word 0, its place there by a binary search in that sub-partition's
-// ascending index map (rare rows: targets whose own sub-partition holds fewer than k ids)
-__device__ uint32_t to_handle(const uint32_t* __restrict__ planes, const SubDesc* subs, uint32_t hshift, uint32_t hbits,
-                              uint32_t x) {
-    if (x == DHT_NONE) return x;
-    const uint32_t s = __builtin_amdgcn_ubfe(planes[x], 32u - hshift - hbits, hbits);
-    const uint32_t* __restrict__ m = subs[s].cmap;
-    uint64_t lo = 0, hi = subs[s].n;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (m[mid] < x) lo = mid + 1; else hi = mid;
-    }
-    return subs[s].base + (uint32_t)lo;
-}
 
 __device__ __forceinline__ void load_target(const uint32_t* __restrict__ tp, uint64_t ts, uint32_t qi, uint32_t* t) {
 #pragma unroll
@@ -679,8 +663,6 @@ struct F3Args {
     unsigned long long* stamps;          // dbg & 256: per-block phase timestamps [np][16]
     uint32_t cap;                        // LDS stage entries (the plan's, <= kF3Cap)
     RecOut rec;                          // record form: F3's fast path writes compact records itself
-    uint32_t h_conv;                     // sub-partition handles: convert context-local results (whole-set roles)
-    uint32_t hshift, hbits;              // an id's sub-partition: word-0 bits [hshift, hshift + hbits)
 };
 
 // (w0 distance, w1 distance, index) order; words 2..4 are read only when both distances tie
@@ -1339,8 +1321,6 @@ __device__ void fb_merge(const F3Args& a, const FbArgs& f, uint32_t g, uint32_t 
             if (lane == 0) {
                 if (a.rec.out)   // record form: word 0 back from the distance, word 1 read
                     rec_place(a.rec, a.planes, a.gidx, a.base, k, qr, r, wi, m ^ t[0], true, a.planes[a.stride + wi]);
-                else if (a.h_conv)   // a whole-set role under sub-partition handles
-                    orow[r] = to_handle(a.planes, a.subs, a.hshift, a.hbits, map_out(wi, a.gidx, a.base));
                 else
                     orow[r] = map_out(wi, a.gidx, a.base);
             }
@@ -1371,19 +1351,6 @@ __device__ void fb_rows_to_records(const F3Args& a, uint32_t qb, uint32_t qend) 
         const uint32_t qr = a.fb_list[qb + j];
         const uint32_t x = ld_sc1(a.out_idx + (uint64_t)qr * k + r);
         rec_place(a.rec, a.rec.planes, nullptr, 0u, k, qr, r, x, 0u, false, x == DHT_NONE ? 0u : a.rec.planes[a.rec.stride + x]);
-    }
-}
-
-// Sub-partition handles after a one-split whole-set scan role: the wave converts the rows its
-// role just wrote (context-local indices, its own stores drained, read back at agent scope).
-__device__ void fb_rows_to_handles(const F3Args& a, uint32_t qb, uint32_t qend) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t lane = lane_id(), k = a.k;
-    const uint32_t nt = qend > qb ? (qend - qb < kScanTargets ? qend - qb : kScanTargets) : 0u;
-    for (uint32_t c = lane; c < nt * k; c += 64) {
-        const uint32_t j = c / k, r = c - j * k;
-        uint32_t* p = a.out_idx + (uint64_t)a.fb_list[qb + j] * k + r;
-        *p = to_handle(a.planes, a.subs, a.hshift, a.hbits, ld_sc1(p));
     }
 }
 
@@ -1427,7 +1394,6 @@ __device__ __forceinline__ void fb_list_scan(const F3Args& a, const FbArgs& f, u
                     as.n = d.n;
                     as.gidx = d.gidx;
                     as.base = d.base;
-                    as.h_conv = 0;   // a sub-partition's own results are handles already
                 }
             }
         }
@@ -1444,7 +1410,6 @@ __device__ __forceinline__ void fb_list_scan(const F3Args& a, const FbArgs& f, u
                                         single ? g + 1 : cnt, as.k, o);
         if (S == 1) {
             if (a.rec.out) fb_rows_to_records(a, qb, single ? g + 1 : cnt);
-            else if (as.h_conv) fb_rows_to_handles(as, qb, single ? g + 1 : cnt);
             continue;
         }
         // hand-off: every wave's sc1 record stores drained, then one agent-scope add per block;
@@ -1928,8 +1893,7 @@ uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, 
         const uint64_t nb = n ? (n + per - 1) / per : 0;
         const uint64_t lim = (subs[i].w0s ? subs[i].stride : 5 * subs[i].stride) - 4;
         d[i] = SubDesc{subs[i].w0s ? subs[i].w0s : subs[i].planes, subs[i].planes, subs[i].stride, n, subs[i].gidx,
-                       subs[i].base, (uint32_t)(lim < 0xFFFFFFF0ull ? lim : 0xFFFFFFF0ull), blk, (uint32_t)nb, per,
-                       subs[i].cmap};
+                       subs[i].base, (uint32_t)(lim < 0xFFFFFFF0ull ? lim : 0xFFFFFFF0ull), blk, (uint32_t)nb, per};
         blk += (uint32_t)nb;
     }
     return blk;
@@ -2017,6 +1981,30 @@ __global__ void k_idx_to_handles(const HandleSub* __restrict__ tab, const uint32
         if (t.map[mid] < x) lo = mid + 1; else hi = mid;
     }
     idx[i] = t.off + (uint32_t)lo;
+}
+
+// Sub-partition handles: the rows F4 answered from the whole set (targets whose own sub-partition
+// holds fewer than k ids, long fallback lists) hold context-local index | kHandleMark (the
+// whole-set roles' result offset); this pass, after F4 and only under handles, turns them into
+// handles.  The fallback list and its count (ctr[0]) are the call's own, F1 of the next call
+// resets them.
+__global__ void k_fb_handles(uint32_t* __restrict__ out_idx, uint32_t k, const uint32_t* __restrict__ fb_list,
+                             const uint32_t* __restrict__ ctr, const HandleSub* __restrict__ tab,
+                             const uint32_t* __restrict__ planes, uint32_t hshift, uint32_t hbits) {
+    const uint64_t m = (uint64_t)ctr[0] * k;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
+        uint32_t* p = out_idx + (uint64_t)fb_list[i / k] * k + i % k;
+        const uint32_t x = *p;
+        if (x == DHT_NONE || !(x & kHandleMark)) continue;
+        const uint32_t cl = x & ~kHandleMark;
+        const HandleSub t = tab[__builtin_amdgcn_ubfe(planes[cl], 32u - hshift - hbits, hbits)];
+        uint64_t lo = 0, hi = t.n;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (t.map[mid] < cl) lo = mid + 1; else hi = mid;
+        }
+        *p = t.off + (uint32_t)lo;
+    }
 }
 
 hipError_t launch_handles_to_idx(const HandleSub* tab, uint32_t nsub, const uint32_t* h, uint64_t m, uint32_t* out,
@@ -2169,9 +2157,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
              d_desc, np, dbg, stamps, narrow ? P.f3cap : P.f3cap_wide, RecOut{}};
     if (c.out_rec)
         a.rec = RecOut{c.out_rec, c.planes, c.stride, c.rec_gidx, c.rec_base, (nsub == 1 && !c.w0s && !c.skip) ? 1u : 0u};
-    a.h_conv = (c.handles && nsub > 1 && !c.out_rec) ? 1u : 0u;
-    a.hshift = c.sub_shift;
-    a.hbits = c.sub_bits;
+
     // F3 stages the plan's 6-sigma bound only beside F2's narrow stage (which it makes room for)
     size_t l3 = f3_lds(P, a.cap);
     if (dbg & 4096) l3 = l3 > 81920 ? l3 : 81920;   // experiment: 2 F3 blocks per CU
@@ -2211,6 +2197,9 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     if (k <= 8) go(3, k_f4<8>, g4, b4, 0, a, fa);
     else if (k <= 16) go(3, k_f4<16>, g4, b4, 0, a, fa);
     else go(3, k_f4<32>, g4, b4, 0, a, fa);
+    if (c.handles && nsub > 1 && !c.out_rec)   // the whole-set fallback rows -> handles
+        k_fb_handles<<<dim3(64), dim3(256), 0, s>>>(c.out_idx, k, fb_list, ctr, c.htab, c.planes, c.sub_shift,
+                                                   c.sub_bits);
     return hipGetLastError();
 }
 

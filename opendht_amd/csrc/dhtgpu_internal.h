@@ -134,9 +134,9 @@ struct SubSpec {
     const uint32_t* planes; const uint32_t* w0s;   // unshifted planes; shifted word-0 plane (nullable)
     uint64_t stride, n;
     const uint32_t* gidx; uint32_t base;           // result index map (nullable) or offset
-    const uint32_t* cmap;                          // sub-local -> context-local index, ascending (nullable)
 };
 
+constexpr uint32_t kHandleMark = 0x80000000u;   // sets hold < 2^31 ids (batch_supported)
 // One sub-partition in handle space: handles [off, off + n) name its ids in its compacted order.
 struct HandleSub {
     uint64_t n;
@@ -169,9 +169,10 @@ struct BatchCall {
     // context-local index to the record's global index
     uint32_t* out_rec; const uint32_t* rec_gidx; uint32_t rec_base;
     // sub-partition handles (nsub > 1, dhtgpu_set_sub_handles): every sub-partition's results are
-    // its base + sub-local index (SubSpec gidx null, base = the sub-partition's offset), and rows
-    // F4 answers from the whole set (context-local indices) are converted to handles in place
-    uint32_t handles;
+    // its base + sub-local index (SubSpec gidx null, base = the sub-partition's offset); rows F4
+    // answers from the whole set carry context-local index | kHandleMark (gidx null, base =
+    // kHandleMark) and a pass after F4 turns them into handles through htab
+    uint32_t handles; const HandleSub* htab;
     int num_cus;
     uint32_t dbg;                          // DHTGPU_DBG diagnostics switches (0 in production)
     const volatile uint32_t* fb_hint;      // nullable: the slot's last fallback-list length (mapped host memory)
