@@ -2191,8 +2191,12 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     // fallback scan's parallelism).  Measured at three in flight: step -1.3 µs, latency +1.5.
     // (a sub-partitioned call fills the chip alone and defers ~1 tie per partition over 2,048+
     // partitions: the full grid keeps them at about one per wave)
-    const uint32_t nfb = (c.fb_hint && *c.fb_hint == 0u && nsub == 1) ? kFbBlocks / 2 : kFbBlocks;
-    const FbArgs fa{fb_rec, fb_done, nfb, NP, c.fb_hint_dev};
+#ifndef DHT_F4_IDLE_GRID
+#define DHT_F4_IDLE_GRID (kFbBlocks / 2)
+#endif
+    const uint32_t nfb = (c.fb_hint && *c.fb_hint == 0u && nsub == 1) ? (uint32_t)DHT_F4_IDLE_GRID : kFbBlocks;
+    // one set: F3 answers its ties inline, so F4 reads no deferred-tie counts (np_ties 0)
+    const FbArgs fa{fb_rec, fb_done, nfb, nsub > 1 ? NP : 0u, c.fb_hint_dev};
     const dim3 g4(nfb), b4(kF4Threads);
     if (k <= 8) go(3, k_f4<8>, g4, b4, 0, a, fa);
     else if (k <= 16) go(3, k_f4<16>, g4, b4, 0, a, fa);
