@@ -2185,14 +2185,16 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
 #undef F3_GO
     if (dbg & 256) print_phase_profile(P, nblk2, NP, stamps, s);
     // F4's grid: its workgroups (50 KB of LDS each) hold CUs the other batches' F2 / F3 want,
-    // and with an empty fallback list only the deferred ties use them -- half the grid when the
-    // context's last completed call listed no target (a hint F4 leaves in mapped host memory;
-    // read without a sync, so possibly a call or two old), the full grid otherwise (the
-    // fallback scan's parallelism).  Measured at three in flight: step -1.3 µs, latency +1.5.
-    // (a sub-partitioned call fills the chip alone and defers ~1 tie per partition over 2,048+
-    // partitions: the full grid keeps them at about one per wave)
+    // and on one set (ties answered inline by F3) an empty fallback list leaves them nothing to
+    // do -- 32 workgroups when the context's last completed call listed no target (a hint F4
+    // leaves in mapped host memory; read without a sync, so possibly a call or two old; a list
+    // that appears then is scanned by those 32, still exactly), the full grid otherwise (the
+    // fallback scan's parallelism).  Round 5: 128 -> 32 with the tie-count reads gone, cfg-2 step
+    // 33.6 -> 31.7-31.9 us (profiles/r05/experiments/f4_idle_ab.txt, f4_idle_grid_ab.txt; 16 and
+    // 8 equal).  (a sub-partitioned call fills the chip alone and defers ~1 tie per partition over
+    // 2,048+ partitions: the full grid keeps them at about one per wave)
 #ifndef DHT_F4_IDLE_GRID
-#define DHT_F4_IDLE_GRID (kFbBlocks / 2)
+#define DHT_F4_IDLE_GRID 32
 #endif
     const uint32_t nfb = (c.fb_hint && *c.fb_hint == 0u && nsub == 1) ? (uint32_t)DHT_F4_IDLE_GRID : kFbBlocks;
     // one set: F3 answers its ties inline, so F4 reads no deferred-tie counts (np_ties 0)
