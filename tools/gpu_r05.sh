@@ -13,7 +13,7 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 tail -1 $OUT/smoke.log
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_driver.json 2> $OUT/bench_driver.err || { tail -20 $OUT/bench_driver.err; exit 1; }
 timeout -k 10 300 python bench.py --sharded --steps 20 --warmup 5 --verify 64 > $OUT/sharded_allgather.json 2> $OUT/sharded_allgather.err || { tail -20 $OUT/sharded_allgather.err; exit 1; }
-timeout -k 10 300 python bench.py --sharded --steps 1000 --warmup 100 --no-cpu --no-extra --verify 64 > $OUT/sharded_1000.json 2> $OUT/sharded_1000.err || { tail -20 $OUT/sharded_1000.err; exit 1; }
+timeout -k 10 300 python bench.py --sharded --steps 1000 --warmup 100 --no-extra --verify 64 > $OUT/sharded_1000.json 2> $OUT/sharded_1000.err || { tail -20 $OUT/sharded_1000.err; exit 1; }
 if [ "$2" != quick ]; then
   timeout -k 10 400 python bench.py --steps 1000 --warmup 100 --no-cpu --no-extra > $OUT/bench1000.json 2> $OUT/bench1000.err || { tail -20 $OUT/bench1000.err; exit 1; }
   timeout -k 10 400 python tools/experiments/rehearse_cfg3.py > $OUT/rehearse_cfg3.json 2> $OUT/rehearse_cfg3.err || { tail -20 $OUT/rehearse_cfg3.err; exit 1; }
