@@ -1612,8 +1612,11 @@ BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     const double mu = (double)q / (double)(1u << P.b1);
     P.tcap = ((uint32_t)(mu + 6.0 * std::sqrt(mu) + 64.0) + 63u) & ~63u;
     // F2: one persistent workgroup per CU, ranges in whole chunks
+#ifndef DHT_F2_WG_PER_CU   // experiment: more, shorter F2 workgroups (dispatched as CUs free up)
+#define DHT_F2_WG_PER_CU 1
+#endif
     const uint64_t chunks = (n + kF2Step - 1) / kF2Step;
-    const uint64_t g = num_cus > 0 ? (uint64_t)num_cus : 256;
+    const uint64_t g = (num_cus > 0 ? (uint64_t)num_cus : 256) * DHT_F2_WG_PER_CU;
     const uint64_t cpb = (chunks + g - 1) / g;
     P.per_blk = (cpb ? cpb : 1) * kF2Step;
     P.nblk2 = (uint32_t)((n + P.per_blk - 1) / P.per_blk);
