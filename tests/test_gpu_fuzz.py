@@ -260,3 +260,35 @@ def test_search_batch_random(ctx, seed):
     for g, w, nm in zip(got, want, ["idx", "flags", "len", "rounds", "queries"]):
         bad = np.nonzero((g != w).reshape(g.shape[0], -1).any(axis=1))[0]
         assert bad.size == 0, f"seed {seed} {nm}: {bad.size} searches differ, first {bad[:5]}"
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_subpartitioned_random_handles(ctx, seed):
+    """Random sub-partitioned shapes with sub-partition handles on: when the call returns handles,
+    mapping them back (dhtgpu_handles_to_indices_dev) gives exactly the K1 scan's indices."""
+    import torch
+    rng = np.random.default_rng(61_000 + seed)
+    n = int(rng.integers((1 << 25) + 1, (1 << 26) + 1))
+    q = int(rng.integers(1 << 17, (1 << 18) + 1))
+    k = int(rng.integers(1, 33))
+    ctx.gen_ids(710 + seed, n)
+    tg = rng.integers(0, 256, size=(q, 20), dtype=np.uint8)
+    sc, scnt = ctx.topk(tg, k)
+    ctx.set_sub_handles(True)
+    try:
+        active = ctx.sub_handles_active(q, k)
+        h, cnt = ctx.batch_topk(tg, k)
+    finally:
+        ctx.set_sub_handles(False)
+    assert np.array_equal(cnt, scnt), (seed, n, q, k)
+    if not active:   # one K6 plan served it: ordinary indices
+        assert np.array_equal(h, sc)
+        return
+    dev = torch.device("cuda", 0)
+    hd = torch.from_numpy(h.reshape(-1).view(np.int32)).to(dev)
+    out = torch.empty_like(hd)
+    ctx.handles_to_indices_dev(hd.data_ptr(), hd.numel(), out.data_ptr(), 0, None)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32).reshape(h.shape)
+    bad = np.nonzero((got != sc).any(axis=1))[0]
+    assert bad.size == 0, (seed, n, q, k, bad[:4])
