@@ -13,7 +13,9 @@ Algorithms (--algo):
   index  K4 bucket-index build + K5 trie-descent query; the index is REBUILT from the raw
          id planes inside every timed step
   scan   K1 brute-force streaming scan (the north-star kernel design)
-Nothing is cached between steps in any algorithm.
+No result or intermediate of a step is reused by the next one.  Persistent per-set state (built
+once per id set, outside the timed steps): the w0..w4 planes (20 B/id) and, for sets
+one K6 plan cannot serve (the cfg-3 shard), their prefix sub-partitions (28 B/id).
 
 Multi-GPU (one process per GPU, torch.distributed over RCCL; --route):
   broadcast  (default for N > 1; SURVEY §8(e) north-star scheme) the metric's own workload,
@@ -36,13 +38,14 @@ totals) or "weak" (default with the prefix route: every rank keeps the one-GPU w
 targets / the slowest rank's time).  N = 1 runs the one-GPU K6 over the whole set.
 
 Beside the headline (`value`) the line carries, measured in the same run:
-  roofline        F2 (the dominant K6 kernel) timed by events its own dispatches record in
-                  every timed step; roofline_hbm: the same kernel with the Infinity Cache
+  roofline        F2 (the dominant K6 kernel) timed by events its own dispatches record over
+                  serial calls after the timed steps; roofline_hbm: the same kernel with the Infinity Cache
                   evicted before each call (the cfg-2 working set otherwise stays in L3)
   small_batch     Q = 1 / 8 / 32 / 64 targets over the same ids (HBM-bound latency mode, KS path)
   find_closest    RoutingTable::findClosestNodes drop-in on a cfg-1-shaped table
   cfg3_shard      one GPU's shard of BASELINE cfg 3 (2^27 ids, 131,072 targets; the library
-                  splits it into prefix sub-partitions) -- its w0 planes (537 MB) exceed L3
+                  splits it into prefix sub-partitions) -- its w0 planes (537 MB) exceed L3;
+                  `handles`: the same calls returning sub-partition handles
   cfg4 / cfg5     classification of 10^8 ids; iterative searches over 5*10^7 nodes
   cfg3 (N > 1)    BASELINE cfg 3 itself over the ranks: 10^9 ids, 2^20 targets, both routes
   cpu_baseline    the oracle port on the host cores (rank 0, N = 1): every host CPU and 1 core;
