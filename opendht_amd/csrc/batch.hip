@@ -2364,8 +2364,9 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
                     }
                     if (__ballot((m[0] | m[1] | m[2] | m[3]) != 0)) {   // rare
 #pragma unroll
-                        for (uint32_t f = 0; f < 4; ++f)
+                        for (uint32_t f = 0; f < 4; ++f) {
                             if (m[f]) emit(v4[f], sb + tid4 + f, (uint32_t)__ffs(m[f]) - 1);
+                        }
                     }
                     ring[r] = load(sb + kRing * kS1Sub);
                     continue;
@@ -2377,10 +2378,14 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
                     hit[f] = ((b16[h >> 5] >> (h & 31)) & 1u) && tid4 + f < rem;
                 }
 #ifdef DHT_S1_MEASURE_NOFILTER
-                if (v4[0] == 0x12345678u && v4[1] == 0x9abcdef0u) nhit = hit[0];   // measurement build: stream only
+                if (v4[0] == 0x12345678u && v4[1] == 0x9abcdef0u) nhit = hit[0] | hit[1] | hit[2] | hit[3];   // measurement build: stream + filter only
                 if (false)
 #endif
+#ifdef DHT_S1_MEASURE_HITS_NEVER   // measurement build: the hit block kept, never entered (results incomplete)
+                if (__ballot(hit[0] || hit[1] || hit[2] || hit[3]) && a.lim == 0xFFFFFFF7u) {
+#else
                 if (__ballot(hit[0] || hit[1] || hit[2] || hit[3])) {   // rare
+#endif
                     // the 16-bit hits go to the LDS queue as they are (one LDS atomic per wave, no
                     // search in the stream: the dependent binary search per hit held the whole wave
                     // at q = 64, S1 18.6 us against 10.6 for the bare stream); the level-Ls match
@@ -2398,6 +2403,9 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
                             if (qi < kS1Queue) {
                                 hitq[qi] = make_uint4(v4[f], sb + tid4 + f, DHT_NONE, 0u);
                             } else {   // past the queue (strongly clustered ids): matched and appended here
+#ifdef DHT_S1_MEASURE_NO_OVERFLOW   // measurement build (results incomplete past the queue)
+                                continue;
+#endif
                                 const uint32_t sl = match(v4[f]);
                                 if (sl != DHT_NONE) {
                                     const uint32_t j = sb + tid4 + f;
@@ -2423,8 +2431,16 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
         const uint4 e = hitq[i];
         const uint32_t sl = e.z != DHT_NONE ? e.z : match(e.x);
         if (sl == DHT_NONE) continue;
+#ifdef DHT_S1_MEASURE_TAIL_NOW1   // measurement builds (results wrong): the tail without its word-1 load / its atomic
+        const uint32_t w1 = 0u;
+#else
         const uint32_t w1 = a.w1[e.y];
+#endif
+#ifdef DHT_S1_MEASURE_TAIL_NOATOM
+        const uint32_t pos = i % kSmallCap;
+#else
         const uint32_t pos = atomicAdd(a.cnt + sl, 1u);
+#endif
         if (pos < kSmallCap) a.cand[sl * kSmallCap + pos] = make_uint4(e.x, e.y, w1, 0u);
     }
 }
