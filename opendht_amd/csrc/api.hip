@@ -369,6 +369,14 @@ int dhtgpu_set_sub_handles(dhtgpu_ctx* c, int on) {
 
 static bool needs_subs(const dhtgpu_ctx* c, uint32_t q, uint32_t k);
 
+// measurement only (not in include/): the phase-stamp / residency-log buffer of DHTGPU_DBG runs
+int dhtgpu_debug_stamps(dhtgpu_ctx* c, void** dev_ptr, uint64_t* bytes) {
+    if (!c || !dev_ptr || !bytes) return DHTGPU_EINVAL;
+    *dev_ptr = c->stamps.p;
+    *bytes = c->stamps.cap;
+    return 0;
+}
+
 int dhtgpu_sub_handles_active(dhtgpu_ctx* c, uint32_t q, uint32_t k) {
     if (!c || !c->has_ids) return 0;
     return c->sub_handles && !(small_supported(c->n, q, k) && !(c->dbg & (1u << 23))) && needs_subs(c, q, k) ? 1 : 0;
@@ -671,8 +679,10 @@ static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hi
     bc.fb_hint_dev = c->fb_hint_dev;
     if (b.zeroed < head) DHT_TRY(hipMemsetAsync(b.ws.p, 0, head, s));
     b.zeroed = 0;   // re-established below once every launch went through
-    if (bc.dbg & 256) {
+    if (bc.dbg & (256u | (1u << 24))) {   // phase stamps / the residency log (zeroed when allocated)
+        const bool fresh = !c->stamps.p;
         DHT_TRY(c->stamps.ensure((size_t)3 * 8192 * 16 * 8));
+        if (fresh) DHT_TRY(hipMemsetAsync(c->stamps.p, 0, (size_t)3 * 8192 * 16 * 8, s));
         bc.stamps = c->stamps.as<unsigned long long>();
     }
     bc.ws = b.ws.p;

@@ -247,6 +247,32 @@ struct F2Args {
 #define F2_STAMP(i) \
     do { if ((a.dbg & 256) && threadIdx.x == 0) a.stamps[(uint64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
+// DHTGPU_DBG bit 2^24 (measurement build): a workgroup residency log of F2 and F3 -- thread 0 appends
+// {kernel | phase, HW_ID | XCC_ID << 32, s_memrealtime, blockIdx} at the workgroup's start and
+// end to stamps[4 + 4 i] (stamps[0]: the record count), across calls (tools/experiments/
+// residency_probe.py: do the two kernels of different batches in flight share CUs?)
+constexpr uint32_t kDbgResLog = 1u << 24;
+constexpr uint32_t kResLogCap = (3u * 8192 * 16 - 4) / 4;
+__device__ __forceinline__ void res_log(unsigned long long* log, uint32_t tag) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+    const unsigned long long i = atomicAdd(log, 1ull);
+    if (i < kResLogCap) {
+        unsigned long long* r = log + 4 + 4 * i;
+        r[0] = tag;
+        r[1] = hw | ((unsigned long long)xcc << 32);
+        r[2] = t;
+        r[3] = blockIdx.x;
+    }
+}
+#ifdef DHT_RESLOG   // the log's code only in the measurement build (build_variant.sh ... -DDHT_RESLOG)
+#define RES_LOG(tag) \
+    do { if ((a.dbg & kDbgResLog) && threadIdx.x == 0) res_log(a.stamps, (tag)); } while (0)
+#else
+#define RES_LOG(tag) do { } while (0)
+#endif
+
 // Flush the stage: the entries move to registers, are counting-sorted by partition back
 // into the stage, and every partition's run is then written with consecutive lanes on
 // consecutive addresses of its bucket pbuf[p][...], whose slots one returning global
@@ -406,6 +432,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     const uint64_t lo64 = (uint64_t)(blockIdx.x - d.blk0) * d.per_blk;
     if (lo64 >= d.n) return;
     F2_STAMP(0);
+    RES_LOG(0x20);
     const uint32_t* const w0 = d.w0;
     const uint32_t poff = sub * np;   // this sub-partition's first partition
     const uint32_t lo = (uint32_t)lo64;
@@ -563,6 +590,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
         }
     }
     F2_STAMP(5);
+    RES_LOG(0x21);
 }
 
 // ---- candidate order ------------------------------------------------------------------
@@ -836,6 +864,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     a.base = 0;
 #endif
     F3_STAMP(0);
+    if (Diag) RES_LOG(0x30);
     if (Diag && (a.dbg & 1024)) __builtin_amdgcn_s_setprio(3);   // experiment: loads/sort first
     // survivors are sorted by their prefix bits [b1, Lq); a target answers from the deepest
     // level L in [Lm, Lq] whose subtree sub(t, L) holds >= want ids (a contiguous range)
@@ -1236,6 +1265,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     // this partition's deferred ties for F4 (a plain store: no shared counter to serialise on)
     if (threadIdx.x == 0 && ntie[0]) a.tie_cnt[p] = ntie[0] < kTieSlots ? ntie[0] : kTieSlots;
     F3_STAMP(7);
+    if (Diag) RES_LOG(0x31);
 }
 
 // ---- F4: the fallback targets (K1 scan, run-time roles) and the deferred ties -------------
@@ -1606,6 +1636,22 @@ BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
             if (lq == P.Lm) break;
         }
     }
+#ifdef DHT_F3_FIVE   // experiment: five F3 workgroups per CU (the cfg-2 period is LDS x time bound)
+    if (P.fits) {
+        const double sub = (double)(1ull << (P.Lm - P.b1)), mu1 = (double)n / (double)(1ull << P.Lm);
+        const double mean = sub * f * mu1, sd = std::sqrt(sub * f * (1.0 - f) * mu1 * mu1 + sub * f * mu1);
+        const double minc = mean + (double)DHT_F3_FIVE * 0.1 * sd + 64.0;
+        constexpr size_t kF3Lds5 = kLdsMax / 5;
+        for (uint32_t lq = P.Lq; lq >= P.Lm && lq > P.b1; --lq) {
+            const size_t fw = (size_t)f3_words(1u << (lq - P.b1)) * 4;
+            if (fw + (size_t)(kF3Threads + 64) * 8 > kF3Lds5) continue;
+            uint32_t c5 = (uint32_t)((kF3Lds5 - fw) / 8 - kF3Threads) & ~63u;
+            c5 = std::min(c5, P.f3cap);
+            if ((double)c5 >= minc) { P.Lq = lq; P.f3cap = c5; break; }
+            if (lq == P.Lm) break;
+        }
+    }
+#endif
     P.nwords = P.Lm >= 5 ? (1u << (P.Lm - 5)) : 1u;
     P.nblk1 = (q + kF1Threads - 1) / kF1Threads;
     // target buckets: mean + 6 sigma + 64 (uniform targets); overflow spills to F4
@@ -2122,14 +2168,15 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         if (ev) hipExtLaunchKernelGGL(kern, g, b, (uint32_t)lds, s, ev[2 * i], ev[2 * i + 1], 0, args...);
         else kern<<<g, b, lds, s>>>(args...);
     };
-    unsigned long long* stamps = (dbg & 256) ? c.stamps : nullptr;   // F3 [8192][16] then F2 [8192][16]
-    if (stamps) (void)hipMemsetAsync(stamps, 0, (size_t)3 * 8192 * 16 * 8, s);
+    if (dbg & 256) dbg &= ~kDbgResLog;
+    unsigned long long* stamps = (dbg & (256u | kDbgResLog)) ? c.stamps : nullptr;   // F3 [8192][16] then F2 [8192][16]
+    if (dbg & 256) (void)hipMemsetAsync(stamps, 0, (size_t)3 * 8192 * 16 * 8, s);
     const F1Args a1{c.tp, c.tp + c.ts, q, P.Lm, P.b1, c.skip, c.sub_shift, c.nsub ? c.sub_bits : 0u, np, P.nwords,
                     bitmap, tcount, tbuf, P.tcap, ctr, tspill};
     go(0, k_f1_targets, dim3((q + kF1Threads - 1) / kF1Threads), dim3(kF1Threads), 0, a1);
     if (nblk2) {
         F2Args a2{d_desc, d_blk, hd[0], nsub, NP, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, P.scap, ctr,
-                  narrow ? P.nstage : P.stage, dbg, P.sparse, seg, stamps ? stamps + 8192 * 16 : nullptr};
+                  narrow ? P.nstage : P.stage, dbg, P.sparse, seg, (dbg & 256) ? stamps + 8192 * 16 : stamps};
         const dim3 g2(nblk2), b2(kF2Threads);
         const size_t l2 = f2_lds(P, narrow);
 #define F2_GO(MM)                                                    \
@@ -2148,7 +2195,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         (void)hipEventRecord(ev[2], s);
         (void)hipEventRecord(ev[3], s);
     }
-    if (dbg & ~(48u | 256u | 512u | 1024u | 2048u | 4096u | 8192u | (7u << 16) | (1u << 23))) {   // experiments: F1 + F2 only
+    if (dbg & ~(48u | 256u | 512u | 1024u | 2048u | 4096u | 8192u | (7u << 16) | (1u << 23) | kDbgResLog)) {   // experiments: F1 + F2 only
         for (int i = 4; ev && i < 8; ++i) (void)hipEventRecord(ev[i], s);
         if (dirty) *dirty = true;   // F3 (which resets the counters and the bitmap) did not run
         return hipGetLastError();
