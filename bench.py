@@ -211,7 +211,7 @@ HBM_PEAK_GBS = 8000.0
 # 64-bit lane; both fractions are reported (the packed prefilter is an algorithmic win).
 OPS_PER_PAIR = 1.0
 SURVEY_OPS_PER_PAIR = 3.0
-PMC_FILE = "profiles/r05/pmc_traffic.json"
+PMC_FILE = "profiles/r06/pmc_traffic.json"
 
 
 def oracle():
@@ -554,8 +554,11 @@ def main():
     last = (step_no[0] - 1) % D
     tie_rows = None
     if collective:   # every in-flight slot's last step: rows the tie exchange settled (the same inputs every step)
-        tie_rows = [settle(recs[d], xbufs[d], outs[d][0], outs[d][1], streams[d].cuda_stream, txs[d])
-                    for d in range(min(D, step_no[0]))]
+        tie_rows = []
+        for d in range(min(D, step_no[0])):
+            torch.cuda.set_stream(streams[d])   # the settlement's collectives order after its stream
+            tie_rows.append(settle(recs[d], xbufs[d], outs[d][0], outs[d][1], streams[d].cuda_stream, txs[d]))
+        torch.cuda.set_stream(tstream)
         torch.cuda.synchronize()
     got_idx = outs[last][0][:q_out].cpu().numpy().view(np.uint32).copy()
     got_tg = tgidx[:q_local].cpu().numpy().view(np.uint32).copy() if tgidx is not None \
@@ -700,7 +703,9 @@ def main():
         extra["find_closest"] = find_closest_leg(ctx, a, dev)
         ctx.close()   # the cfg-2 set is no longer needed: free HBM for the size legs
         ctx = None
-        for name, fn in (("cfg3_shard", cfg3_shard_leg), ("cfg4", cfg4_leg), ("cfg5", cfg5_leg)):
+        for name, fn in (("cfg3_prefix_rank", lambda *x: cfg3_rank_leg(*x, route="prefix")),
+                         ("cfg3_broadcast_rank", lambda *x: cfg3_rank_leg(*x, route="broadcast")),
+                         ("cfg3_shard", cfg3_shard_leg), ("cfg4", cfg4_leg), ("cfg5", cfg5_leg)):
             progress(f"{name} leg")
             try:
                 extra[name] = fn(a, L, dev, stream, tstream)
@@ -917,10 +922,166 @@ def find_closest_leg(ctx, a, dev):
             "note": "host API per call: snapshot + targets uploaded, results downloaded (PCIe included)"}
 
 
+CFG3_N, CFG3_Q, CFG3_WORLD = 1_000_000_000, 1 << 20, 8
+
+
+def cfg3_rank_setup(seed, route, L, dev, stream, rank=0, world=CFG3_WORLD):
+    """One rank's inputs of BASELINE cfg 3 (10^9 ids, 2^20 targets over `world` GPUs), exactly as the
+    N-rank job builds them (cfg3_multi_leg's seeds): the prefix route's rank holds the ids of the
+    10^9 stream whose top log2(world) bits equal its rank (gen_ids_prefix: ~1.25e8) and answers the
+    ~2^20 / world targets of that prefix, with GLOBAL stream indices; the broadcast route's rank holds
+    the id range shard_range(10^9, world, rank) and answers all 2^20 targets.
+    Returns (ctx, target planes, stride, q on this rank, target rows' global index or None, idx base)."""
+    c = opendht_amd.Context(dev.index)
+    tp_all, ts = gen_targets(L, seed + 11, CFG3_Q, dev, stream)
+    if route == "prefix":
+        pbits = world.bit_length() - 1
+        c.gen_ids_prefix(seed + 10, CFG3_N, pbits, rank)
+        c.set_global_indices(True)
+        tp = torch.empty_like(tp_all)
+        tgidx = torch.empty(ts, dtype=torch.int32, device=dev)
+        ql = c.select_prefix_dev(tp_all.data_ptr(), ts, CFG3_Q, pbits, rank, tp.data_ptr(), ts, tgidx.data_ptr(), stream)
+        return c, tp, ts, ql, tgidx, 0
+    lo, hi = sharding.shard_range(CFG3_N, world, rank)
+    c.gen_ids(seed + 10, hi - lo, start=lo)
+    return c, tp_all, ts, CFG3_Q, None, lo
+
+
+def k6_step_bytes(n, q, k, surv, record=False, mapped=False):
+    """Algorithmic bytes of one K6 call, per kernel: F1 12 B/target; F2
+    4 B/id (w0) + 8 B/survivor; F3 8 B/survivor + 36 B/target (bucket entry, target words, count)
+    + per result: 4 B written (index form) or 12 B written + 4 B of word 1 read (record form), + 4 B
+    of the index map read when results are mapped to global indices through a sub-partition map."""
+    per_res = (16 if record else 4) + (4 if mapped else 0)
+    return {"k_f1_targets": 12 * q, "k_f2_filter": 4 * n + 8 * surv,
+            "k_f3_answer": 8 * surv + q * (8 + 16 + 4) + q * k * per_res, "k_f4_fallback": 0}
+
+
+def cfg3_rank_leg(a, L, dev, stream, tstream, route):
+    """One rank of BASELINE cfg 3 at the exact N = 8 per-rank shape, on this one GPU:
+      prefix     ~1.25e8 ids (the 10^9 stream's prefix-0 shard) x ~2^17 targets (those of prefix 0),
+                 global indices -- what each rank of the prefix route does, no collective;
+      broadcast  1.25e8 ids (shard_range(10^9, 8, 0)) x all 2^20 targets, K6 in record form then K3
+                 over the one list -- each rank's work on the north-star route minus the all-gather
+                 (K3 merges 8 lists there).
+    Two calls in flight (one call's F3 / F4 / K3 beside the next call's F2).  roofline: F2 and the
+    whole step against 8 TB/s, algorithmic bytes per k6_step_bytes; PMC traffic from the committed
+    rocprofv3 passes of tools/batch_probe.py --cfg3 <route>.  Verified on >= 32 targets against the
+    generator-fed oracle (orc_topk_gen: std::partial_sort semantics over the 10^9-id stream or the
+    shard's range)."""
+    k = a.k
+    c, tp, ts, q, tgidx, lo = cfg3_rank_setup(a.seed, route, L, dev, stream)
+    try:
+        n = c.num_ids
+        record = route == "broadcast"
+        RW = sharding.REC_WORDS
+        st2 = [tstream, torch.cuda.Stream(dev)]
+        outs = [(torch.empty((q, k), dtype=torch.int32, device=dev), torch.empty(q, dtype=torch.int32, device=dev),
+                 torch.empty((q, k, RW), dtype=torch.int32, device=dev) if record else None) for _ in range(2)]
+
+        def call(i, s, ev=None):
+            oi, oc, rec = outs[i]
+            if ev is not None:
+                ev.arm(c)
+            if record:
+                c.batch_topk_dev(tp.data_ptr(), ts, q, k, None, None, rec.data_ptr(), lo, s)
+                assert L.dhtgpu_merge_dev(rec.data_ptr(), 1, q, k, tp.data_ptr(), ts, k, oi.data_ptr(), oc.data_ptr(),
+                                          None, 0, s) == 0
+            else:
+                c.batch_topk_dev(tp.data_ptr(), ts, q, k, oi.data_ptr(), oc.data_ptr(), None, 0, s)
+        t0 = time.perf_counter()
+        call(0, stream)
+        torch.cuda.synchronize()
+        first_s = time.perf_counter() - t0
+        for i in range(4):   # both streams' workspace slots set up before the timed windows
+            call(i % 2, st2[i % 2].cuda_stream)
+        steps = 20
+
+        def window(nst):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(steps):
+                call(i % 2, st2[i % nst].cuda_stream)
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) * 1e3 / steps
+        ms1 = window(1)
+        ms = window(2)
+        got = outs[(steps - 1) % 2][0].clone()
+        reps = 8   # kernel times: serial calls after the timed windows
+        ev = EvSets(reps, tstream)
+        for _ in range(reps):
+            call(0, tstream.cuda_stream, ev)
+        kms = ev.mean_ms()
+        k3_ms = None
+        if record:
+            k3_ms = ev_time(lambda: L.dhtgpu_merge_dev(outs[0][2].data_ptr(), 1, q, k, tp.data_ptr(), ts, k,
+                                                       outs[0][0].data_ptr(), outs[0][1].data_ptr(), None, 0, stream),
+                            reps, tstream)
+        _, fb, surv, slow = c.batch_topk_timed(tp.data_ptr(), ts, q, k, outs[0][0].data_ptr(), outs[0][1].data_ptr(),
+                                               stream)
+        alg = k6_step_bytes(n, q, k, surv, record=record, mapped=not record)
+        names = list(alg)
+        kern_ms = dict(zip(names, kms))
+        if record:   # K3 over the one list: records + target words 0..1 in, indices + counts out
+            alg["k_merge3"] = q * k * 12 + q * 8 + q * k * 4 + q * 4
+            kern_ms["k_merge3"] = k3_ms
+        step_bytes = sum(alg.values())
+        f2b, f2ms = alg["k_f2_filter"], kern_ms["k_f2_filter"]
+        key = f"cfg3{route}:{n}x{q}x{k}"
+        tb = pmc_traffic(key, "k_f2_filter")
+        tstep = None
+        try:
+            d = json.load(open(os.path.join(ROOT, PMC_FILE))).get("workloads", {}).get(key, {})
+            step_k = ("k_f1_targets", "k_f2_filter", "k_f3_answer", "k_f4", "k_merge3")   # the step's kernels only
+            tstep = sum(d[kn]["traffic_bytes"] for kn in step_k if kn in d) or None
+        except (OSError, ValueError):
+            pass
+        res = {"route": route,
+               "workload": (f"rank 0 of the prefix route at N = {CFG3_WORLD}: {n} ids (the 10^9 stream's prefix-0 shard) x "
+                            f"{q} targets (prefix 0 of {CFG3_Q}), k={k}, global indices" if route == "prefix" else
+                            f"rank 0 of the broadcast route at N = {CFG3_WORLD}: {n} ids (shard_range(10^9, 8, 0)) x {q} "
+                            f"targets, k={k}: K6 in record form + K3 over the one list (no all-gather)"),
+               "ms_per_step": ms, "qps": q / (ms * 1e-3), "inflight": 2, "ms_per_step_one_stream": ms1,
+               "setup_first_call_s": first_s, "kernels_ms": kern_ms,
+               "kernel_timing": f"{reps} serial calls after the timed windows (events on the kernels' own dispatches)",
+               "alg_bytes_per_launch": alg, "survivors": surv, "fallback": fb, "wave_path": slow,
+               "roofline": {"bound": "hbm", "kernel": "k_f2_filter", "achieved": f2b / (f2ms * 1e-3) / 1e9,
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": f2b / (f2ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                            "kernel_ms": f2ms, "alg_bytes_per_launch": f2b,
+                            "traffic": tb / (f2ms * 1e-3) / 1e9 if tb else None, "traffic_bytes_per_launch": tb,
+                            "traffic_source": f"{PMC_FILE} workloads[{key!r}]" if tb else None,
+                            "step_alg_bytes": step_bytes,
+                            "step_frac": step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                            "step_traffic_bytes": tstep,
+                            "served_from": f"HBM: the w0 planes ({4 * n / 1e6:.0f} MB) exceed the 256 MiB L3",
+                            "how": "frac: F2's algorithmic bytes / its mean event time; step_frac: every kernel's "
+                                   "algorithmic bytes / the 2-in-flight step time; peak 8 TB/s"}}
+        if not a.no_cpu:
+            O = oracle()
+            rows = np.linspace(0, q - 1, 32).astype(np.int64)
+            g = got.cpu().numpy().view(np.uint32)[rows]
+            tgt_all = O.gen_ids(a.seed + 11, CFG3_Q)
+            if route == "prefix":
+                gi = tgidx[:q].cpu().numpy().view(np.uint32)[rows].astype(np.int64)
+                want, _ = O.topk_gen(a.seed + 10, CFG3_N, tgt_all[gi], k, threads=usable_cpus())
+            else:
+                want, _ = O.topk_gen(a.seed + 10, n, tgt_all[rows], k, start=lo, threads=usable_cpus())
+            res["verified_targets"] = int(rows.size)
+            res["verified_exact"] = bool(np.array_equal(g, want))
+            res["verified_against"] = ("orc_topk_gen over the whole 10^9-id stream (global indices)" if route == "prefix"
+                                       else f"orc_topk_gen over the shard's ids [{lo}, {lo + n}) of the stream")
+        return res
+    finally:
+        c.close()
+        torch.cuda.synchronize()
+
+
 def cfg3_shard_leg(a, L, dev, stream, tstream):
-    """One GPU's shard of cfg 3: 2^27 ids (~10^9 / 8), 131,072 targets.  The library splits the
-    set once into 8 prefix sub-partitions of 2^24 (setup, not timed) and serves all of them with
-    ONE K6 launch sequence; their w0 planes (537 MB) exceed the Infinity Cache, so F2 streams HBM."""
+    """A 2^27-id set (~10^9 / 8, the prefix route's per-rank size rounded to a power of two) with
+    131,072 targets spread over every prefix: the prefix route's per-rank shape (VERDICT r4 item 2's
+    benchmark; cfg3_prefix_rank is the exact rank).  The library splits the set once into 8 prefix
+    sub-partitions of 2^24 (setup, not timed) and serves all of them with ONE K6 launch sequence;
+    their w0 planes (537 MB) exceed the Infinity Cache, so F2 streams HBM."""
     n, q, k = 1 << 27, 131072, a.k
     c = opendht_amd.Context(dev.index)
     try:
@@ -1150,12 +1311,13 @@ def broadcast_leg(a, L, dev, world, rank, exchange, tp, ts, ctx, lo, ref_idx, re
                 sharding.merge_allgather(ops, recs[i], g, k, outs[i][0], outs[i][1], txs[i], lo, st.cuda_stream)
     ms = timed_steps(step, a.steps, a.warmup, dev)
     last = (n_call[0] - 1) % D
-    if exchange == "alltoall":
-        sharding.settle_overflow_alltoall(ops, recs[last], xb[last].view(world, qo, k, RW), k, tlo, outs[last][0],
-                                          outs[last][1], txs[last], lo, streams[last].cuda_stream)
-    else:
-        sharding.settle_overflow_allgather(ops, recs[last], xb[last].view(world, q, k, RW), k, outs[last][0],
-                                           outs[last][1], txs[last], lo, streams[last].cuda_stream)
+    with torch.cuda.stream(streams[last]):
+        if exchange == "alltoall":
+            sharding.settle_overflow_alltoall(ops, recs[last], xb[last].view(world, qo, k, RW), k, tlo, outs[last][0],
+                                              outs[last][1], txs[last], lo, streams[last].cuda_stream)
+        else:
+            sharding.settle_overflow_allgather(ops, recs[last], xb[last].view(world, q, k, RW), k, outs[last][0],
+                                               outs[last][1], txs[last], lo, streams[last].cuda_stream)
     torch.cuda.synchronize()
     got = outs[last][0][:qo].cpu().numpy().view(np.uint32)
     # the rows both runs answered on this rank must agree (same shard, same targets)
@@ -1214,106 +1376,160 @@ def prefix_leg(a, L, dev, world, rank, strong):
 
 
 def cfg3_multi_leg(a, L, dev, stream, tstream, world, rank):
-    """BASELINE cfg 3 over the ranks: 10^9 ids, 2^20 targets, k = 8, each route timed:
-    broadcast (SURVEY 8(e) north star: id-range shards, every target on every rank, K6 record
-    mode, one RCCL all-gather of q*k*12 B, K3 merge + the tie exchange) and prefix (ids and targets routed by
-    their top log2(N) bits, no collective on the data path)."""
-    n, q, k = 1_000_000_000, 1 << 20, a.k
-    out = {"workload": f"{q} targets x {n} ids over {world} GPUs, k={k}"}
-    steps = 5
-    tp_all, ts = gen_targets(L, a.seed + 11, q, dev, stream)
-    # broadcast route
-    lo, hi = sharding.shard_range(n, world, rank)
-    c = opendht_amd.Context(dev.index)
-    try:
-        c.gen_ids(a.seed + 10, hi - lo, start=lo)
-        RW = sharding.REC_WORDS
-        rec = torch.empty((q, k, RW), dtype=torch.int32, device=dev)
-        gathered = torch.empty((world * q, k, RW), dtype=torch.int32, device=dev)
-        oi = torch.empty((q, k), dtype=torch.int32, device=dev)
-        oc = torch.empty(q, dtype=torch.int32, device=dev)
-        tx = sharding.TieExchange(world, k, dev)
-        ops = sharding.LibOps(L, c, tp_all.data_ptr(), ts)
+    """BASELINE cfg 3 over the ranks: 10^9 ids, 2^20 targets, k = 8, each route timed with two steps
+    in flight (one step's exchange + merge, or F3 / F4, beside the next step's K6):
+      broadcast  SURVEY 8(e) north star: id-range shards, every target on every rank, K6 record form,
+                 one RCCL all-gather of q*k*12 B, K3 over the world's lists + the tie exchange; beside
+                 it the same route with an all-to-all by target slice;
+      prefix     ids and targets routed by their top log2(N) bits, no collective on the data path,
+                 global indices.
+    Each route carries an aggregate roofline (every rank's F2 / step algorithmic bytes over the slowest
+    rank's time, against N x 8 TB/s; per-rank inputs = cfg3_rank_setup, the shapes the one-GPU
+    cfg3_<route>_rank legs measure) and rank 0's rows are verified against the generator-fed oracle
+    over the 10^9-id stream (32 targets)."""
+    q, k = CFG3_Q, a.k
+    out = {"workload": f"{q} targets x {CFG3_N} ids over {world} GPUs, k={k}", "inflight": 2}
+    steps = 10
+    D = 2
+    RW = sharding.REC_WORDS
 
-        def bstep():
-            c.batch_topk_dev(tp_all.data_ptr(), ts, q, k, None, None, rec.data_ptr(), lo, stream)
-            g = sharding.gather_records(rec, out=gathered)
-            sharding.merge_allgather(ops, rec, g, k, oi, oc, tx, lo, stream)
-        bstep()
+    def timed(step):
+        for i in range(2 * D):
+            step(i)
         torch.cuda.synchronize()
         dist.barrier()
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            bstep()
+        for i in range(steps):
+            step(i)
         torch.cuda.synchronize()
         dist.barrier()
+        torch.cuda.synchronize()
         tm = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        ms = float(tm.item()) * 1e3 / steps
-        nt = sharding.settle_overflow_allgather(ops, rec, gathered.view(world, q, k, RW), k, oi, oc, tx, lo, stream)
-        out["broadcast"] = {"ms_per_step": ms, "qps": q / (ms * 1e-3), "ids_per_gpu": hi - lo,
-                            "record_bytes_per_gpu": q * k * 12, "allgather_bytes_in_per_gpu": world * q * k * 12,
-                            "tie_rows": nt, "scaling": "strong (one global batch)"}
-        # the same route with an all-to-all by target slice: each rank receives and merges only
-        # its own q / world targets' candidates (world*q_r*k*12 B in per GPU instead of world times it)
+        return float(tm.item()) * 1e3 / steps
+
+    def aggregate(c, tp, ts, ql, ms, record, mapped, route):
+        """every rank's F2 and step algorithmic bytes over the slowest rank's times (serial calls)"""
+        ev = EvSets(6, tstream)
+        oi = torch.empty((max(ql, 1), k), dtype=torch.int32, device=dev)
+        oc = torch.empty(max(ql, 1), dtype=torch.int32, device=dev)
+        torch.cuda.set_stream(tstream)
+        for _ in range(6):
+            ev.arm(c)
+            c.batch_topk_dev(tp.data_ptr(), ts, ql, k, oi.data_ptr(), oc.data_ptr(), None, 0, stream)
+        kms = ev.mean_ms()
+        _, _, surv, _ = c.batch_topk_timed(tp.data_ptr(), ts, ql, k, oi.data_ptr(), oc.data_ptr(), stream)
+        alg = k6_step_bytes(c.num_ids, ql, k, surv, record=record, mapped=mapped)
+        tb = pmc_traffic(f"cfg3{route}:{c.num_ids}x{ql}x{k}", "k_f2_filter")
+        v = torch.tensor([float(alg["k_f2_filter"]), float(sum(alg.values())), float(tb or 0.0), 0.0 if tb else 1.0],
+                         dtype=torch.float64, device=dev)
+        slow = torch.tensor([kms[1]], dtype=torch.float64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        dist.all_reduce(slow, op=dist.ReduceOp.MAX)
+        f2b, sb, sm = float(v[0].item()), float(v[1].item()), float(slow.item())
+        tball = float(v[2].item()) if float(v[3].item()) == 0.0 else None
+        peak = HBM_PEAK_GBS * world
+        return {"ranks": world, "kernel": "k_f2_filter", "alg_bytes_all_ranks": f2b, "slowest_rank_kernel_ms": sm,
+                "achieved": f2b / (sm * 1e-3) / 1e9, "peak": peak, "unit": "GB/s",
+                "frac": f2b / (sm * 1e-3) / 1e9 / peak,
+                "traffic": tball / (sm * 1e-3) / 1e9 if tball else None, "traffic_bytes_all_ranks": tball,
+                "step_alg_bytes_all_ranks": sb, "step_frac": sb / (ms * 1e-3) / 1e9 / peak,
+                "how": "sum over ranks of the algorithmic bytes (k6_step_bytes) / the slowest rank's F2 event time "
+                       "(frac) or the timed step (step_frac) / (ranks x 8 TB/s); traffic: the ranks' PMC bytes "
+                       "when every rank's shape has a committed pass"}
+
+    def verify(rows_idx, tgi):
+        """rank 0: rows vs orc_topk_gen over the whole 10^9-id stream (global indices)"""
+        O = oracle()
+        tg = O.gen_ids(a.seed + 11, q)[tgi]
+        want, _ = O.topk_gen(a.seed + 10, CFG3_N, tg, k, threads=usable_cpus())
+        return {"verified_targets": int(len(tgi)), "verified_exact": bool(np.array_equal(rows_idx, want))}
+
+    # broadcast route: all-gather (north star), then the all-to-all beside it
+    c, tp, ts, ql, _, lo = cfg3_rank_setup(a.seed, "broadcast", L, dev, stream, rank, world)
+    try:
+        sts = [tstream, torch.cuda.Stream(dev)]
+        recs = [torch.empty((q, k, RW), dtype=torch.int32, device=dev) for _ in range(D)]
+        gath = [torch.empty((world * q, k, RW), dtype=torch.int32, device=dev) for _ in range(D)]
+        ois = [torch.empty((q, k), dtype=torch.int32, device=dev) for _ in range(D)]
+        ocs = [torch.empty(q, dtype=torch.int32, device=dev) for _ in range(D)]
+        txs = [sharding.TieExchange(world, k, dev) for _ in range(D)]
+        ops = sharding.LibOps(L, c, tp.data_ptr(), ts)
+
+        def bstep(i):
+            d = i % D
+            torch.cuda.set_stream(sts[d])
+            c.batch_topk_dev(tp.data_ptr(), ts, q, k, None, None, recs[d].data_ptr(), lo, sts[d].cuda_stream)
+            g = sharding.gather_records(recs[d], out=gath[d])
+            sharding.merge_allgather(ops, recs[d], g, k, ois[d], ocs[d], txs[d], lo, sts[d].cuda_stream)
+        ms = timed(bstep)
+        nt = []
+        for d in range(D):
+            torch.cuda.set_stream(sts[d])
+            nt.append(sharding.settle_overflow_allgather(ops, recs[d], gath[d].view(world, q, k, RW), k, ois[d],
+                                                         ocs[d], txs[d], lo, sts[d].cuda_stream))
+        torch.cuda.set_stream(tstream)
+        torch.cuda.synchronize()
+        row = {"ms_per_step": ms, "qps": q / (ms * 1e-3), "ids_per_gpu": c.num_ids, "record_bytes_per_gpu": q * k * 12,
+               "allgather_bytes_in_per_gpu": world * q * k * 12, "tie_rows": nt, "scaling": "strong (one global batch)"}
+        row["roofline"] = {"aggregate": aggregate(c, tp, ts, q, ms, True, False, "broadcast")}
+        ref = ois[(steps + 2 * D - 1) % D]
+        if rank == 0 and not a.no_cpu:
+            rows = np.linspace(0, q - 1, 32).astype(np.int64)
+            row.update(verify(ref.cpu().numpy().view(np.uint32)[rows], rows))
+        out["broadcast"] = row
+        # the all-to-all by target slice: each rank receives and merges only its own q / world targets
         tlo, thi = sharding.shard_range(q, world, rank)
         qm = thi - tlo
-        exch = torch.empty((world * qm, k, RW), dtype=torch.int32, device=dev)
-        om = torch.empty((max(qm, 1), k), dtype=torch.int32, device=dev)
-        ocm = torch.empty(max(qm, 1), dtype=torch.int32, device=dev)
-        txa = sharding.TieExchange(world, k, dev)
+        exs = [torch.empty((world * qm, k, RW), dtype=torch.int32, device=dev) for _ in range(D)]
+        oms = [torch.empty((max(qm, 1), k), dtype=torch.int32, device=dev) for _ in range(D)]
+        ocms = [torch.empty(max(qm, 1), dtype=torch.int32, device=dev) for _ in range(D)]
+        txa = [sharding.TieExchange(world, k, dev) for _ in range(D)]
 
-        def astep():
-            c.batch_topk_dev(tp_all.data_ptr(), ts, q, k, None, None, rec.data_ptr(), lo, stream)
-            ex = sharding.exchange_records(rec, out=exch)
-            sharding.merge_alltoall(ops, rec, ex, k, tlo, om, ocm, txa, lo, stream)
-        astep()
+        def astep(i):
+            d = i % D
+            torch.cuda.set_stream(sts[d])
+            c.batch_topk_dev(tp.data_ptr(), ts, q, k, None, None, recs[d].data_ptr(), lo, sts[d].cuda_stream)
+            ex = sharding.exchange_records(recs[d], out=exs[d])
+            sharding.merge_alltoall(ops, recs[d], ex, k, tlo, oms[d], ocms[d], txa[d], lo, sts[d].cuda_stream)
+        ms = timed(astep)
+        for d in range(D):
+            torch.cuda.set_stream(sts[d])
+            sharding.settle_overflow_alltoall(ops, recs[d], exs[d].view(world, qm, k, RW), k, tlo, oms[d], ocms[d],
+                                              txa[d], lo, sts[d].cuda_stream)
+        torch.cuda.set_stream(tstream)
         torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            astep()
-        torch.cuda.synchronize()
-        dist.barrier()
-        tm = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        ms = float(tm.item()) * 1e3 / steps
-        torch.cuda.synchronize()
-        sharding.settle_overflow_alltoall(ops, rec, exch.view(world, qm, k, RW), k, tlo, om, ocm, txa, lo, stream)
-        torch.cuda.synchronize()
-        agree = bool(torch.equal(om[:qm], oi[tlo:thi]) and torch.equal(ocm[:qm], oc[tlo:thi])) if qm else True
-        out["broadcast_alltoall"] = {"ms_per_step": ms, "qps": q / (ms * 1e-3), "ids_per_gpu": hi - lo,
+        last = (steps + 2 * D - 1) % D
+        agree = bool(torch.equal(oms[last][:qm], ref[tlo:thi])) if qm else True
+        out["broadcast_alltoall"] = {"ms_per_step": ms, "qps": q / (ms * 1e-3), "ids_per_gpu": c.num_ids,
                                      "exchange_bytes_in_per_gpu": world * qm * k * 12,
                                      "equals_allgather_route": agree,
                                      "results": "distributed by target slice (shard_range(q, world, rank))",
                                      "scaling": "strong (one global batch)"}
     finally:
+        torch.cuda.set_stream(tstream)
         c.close()
         torch.cuda.synchronize()
-    # prefix route
-    pbits = world.bit_length() - 1
-    c = opendht_amd.Context(dev.index)
+    # prefix route (global indices)
+    c, tp, ts, ql, tgidx, _ = cfg3_rank_setup(a.seed, "prefix", L, dev, stream, rank, world)
     try:
-        c.gen_ids_prefix(a.seed + 10, n, pbits, rank)
-        c.set_global_indices(False)
-        tp = torch.empty_like(tp_all)
-        ql = c.select_prefix_dev(tp_all.data_ptr(), ts, q, pbits, rank, tp.data_ptr(), ts, None, stream)
-        oi = torch.empty((max(ql, 1), k), dtype=torch.int32, device=dev)
-        oc = torch.empty(max(ql, 1), dtype=torch.int32, device=dev)
-        pstep = lambda: c.batch_topk_dev(tp.data_ptr(), ts, ql, k, oi.data_ptr(), oc.data_ptr(), None, 0, stream)
-        pstep()
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            pstep()
-        torch.cuda.synchronize()
-        dist.barrier()
-        tm = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        ms = float(tm.item()) * 1e3 / steps
-        out["prefix"] = {"ms_per_step": ms, "qps": q / (ms * 1e-3), "ids_per_gpu_rank0": c.num_ids,
-                         "targets_rank0": ql, "scaling": "strong (one global batch, routed by prefix)"}
+        sts = [tstream, torch.cuda.Stream(dev)]
+        ois = [torch.empty((max(ql, 1), k), dtype=torch.int32, device=dev) for _ in range(D)]
+        ocs = [torch.empty(max(ql, 1), dtype=torch.int32, device=dev) for _ in range(D)]
+
+        def pstep(i):
+            d = i % D
+            c.batch_topk_dev(tp.data_ptr(), ts, ql, k, ois[d].data_ptr(), ocs[d].data_ptr(), None, 0, sts[d].cuda_stream)
+        ms = timed(pstep)
+        row = {"ms_per_step": ms, "qps": q / (ms * 1e-3), "ids_per_gpu_rank0": c.num_ids, "targets_rank0": ql,
+               "result_indices": "global", "scaling": "strong (one global batch, routed by prefix)"}
+        row["roofline"] = {"aggregate": aggregate(c, tp, ts, ql, ms, False, True, "prefix")}
+        if rank == 0 and not a.no_cpu and ql:
+            rows = np.linspace(0, ql - 1, 32).astype(np.int64)
+            got = ois[(steps + 2 * D - 1) % D].cpu().numpy().view(np.uint32)[rows]
+            row.update(verify(got, tgidx[:ql].cpu().numpy().view(np.uint32)[rows].astype(np.int64)))
+        out["prefix"] = row
     finally:
         c.close()
         torch.cuda.synchronize()

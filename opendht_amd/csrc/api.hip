@@ -142,9 +142,11 @@ struct dhtgpu_ctx {
     uint64_t cache_version = 0;
     DevBuf cache_in, sort_scratch, cache_acc;
     DevBuf srch;            // search_insert / table_stats staging
-    // diagnostics: DHTGPU_DBG, the library's one diagnostics switch (bit 256 =
-    // per-block phase stamps of F2 / F3 printed to stderr, the other bits = the measurement
-    // ablations of DESIGN §5a, results then incomplete); read once at creation, 0 in production
+    // diagnostics: DHTGPU_DBG, the library's one diagnostics switch, read once at creation and
+    // masked to kDbgAllowed -- bit 256: per-block phase stamps of F2 / F3 printed to stderr;
+    // bit 2^23: K6 instead of KS for batches of <= 64 targets (both exact).  Neither changes a
+    // result; every other bit is ignored (the result-altering measurement ablations of earlier
+    // rounds are not in this library: DESIGN.md §5d)
     uint32_t dbg = 0;
     uint32_t search_alpha = 4;   // crawl model: requests per search round (MAX_REQUESTED_SEARCH_NODES)
     hipEvent_t next_ev[8] = {};   // dhtgpu_batch_events: the next K6 call records its kernels here
@@ -208,7 +210,7 @@ int dhtgpu_ctx_create(int device, dhtgpu_ctx** out) {
     c->device = device;
     hipError_t e = c->bind();
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    if (const char* d = getenv("DHTGPU_DBG")) c->dbg = (uint32_t)atoi(d);
+    if (const char* d = getenv("DHTGPU_DBG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0) & kDbgAllowed;
     if (e == hipSuccess) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
@@ -369,7 +371,7 @@ int dhtgpu_set_sub_handles(dhtgpu_ctx* c, int on) {
 
 static bool needs_subs(const dhtgpu_ctx* c, uint32_t q, uint32_t k);
 
-// measurement only (not in include/): the phase-stamp / residency-log buffer of DHTGPU_DBG runs
+// measurement only (not in include/): the phase-stamp buffer of DHTGPU_DBG=256 runs
 int dhtgpu_debug_stamps(dhtgpu_ctx* c, void** dev_ptr, uint64_t* bytes) {
     if (!c || !dev_ptr || !bytes) return DHTGPU_EINVAL;
     *dev_ptr = c->stamps.p;
@@ -679,7 +681,7 @@ static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hi
     bc.fb_hint_dev = c->fb_hint_dev;
     if (b.zeroed < head) DHT_TRY(hipMemsetAsync(b.ws.p, 0, head, s));
     b.zeroed = 0;   // re-established below once every launch went through
-    if (bc.dbg & (256u | (1u << 24))) {   // phase stamps / the residency log (zeroed when allocated)
+    if (bc.dbg & 256u) {   // phase stamps (zeroed when allocated)
         const bool fresh = !c->stamps.p;
         DHT_TRY(c->stamps.ensure((size_t)3 * 8192 * 16 * 8));
         if (fresh) DHT_TRY(hipMemsetAsync(c->stamps.p, 0, (size_t)3 * 8192 * 16 * 8, s));
@@ -687,10 +689,9 @@ static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hi
     }
     bc.ws = b.ws.p;
     bc.desc_sig = &b.desc_sig;
-    bool dirty = false;
-    DHT_TRY(launch_batch_topk(bc, s, &dirty));
+    DHT_TRY(launch_batch_topk(bc, s));
     b.last = s;
-    b.zeroed = dirty ? 0 : head;   // the call leaves its clean head zero
+    b.zeroed = head;   // the call leaves its clean head zero
     c->blast = si;
     c->last_n = n_plan;
     c->last_qp = bc.q_plan;
@@ -903,7 +904,7 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
         c->has_next_ev = false;
         ev = evs;
     }
-    // DHTGPU_DBG bit 2^23: K6 for small batches too (comparison runs)
+    // DHTGPU_DBG bit 2^23: K6 for small batches too (comparison runs; the same exact results)
     if (small_supported(c->n, q, k) && !(c->dbg & (1u << 23)))
         return small_run(c, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s, ev);
     c->last_small = false;

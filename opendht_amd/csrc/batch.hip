@@ -239,7 +239,7 @@ struct F2Args {
     uint32_t pcap;
     uint32_t* ctr;                // shared counters (F2 writes none; the survivor total is sum(pcount))
     uint32_t stage;               // LDS stage capacity (entries, <= kStage)
-    uint32_t dbg;                 // experiment switches (0 in production)
+    uint32_t dbg;                 // diagnostics: bit 256 = phase stamps (results unchanged)
     uint32_t sparse;              // 1: no per-sub-step barrier (plan: the stage holds a segment's survivors)
     uint32_t seg;                 // sparse mode: ids per segment (the stage is flushed after each)
     unsigned long long* stamps;   // dbg & 256: per-block phase timestamps [nblk2][16]
@@ -247,31 +247,6 @@ struct F2Args {
 #define F2_STAMP(i) \
     do { if ((a.dbg & 256) && threadIdx.x == 0) a.stamps[(uint64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
-// DHTGPU_DBG bit 2^24 (measurement build): a workgroup residency log of F2 and F3 -- thread 0 appends
-// {kernel | phase, HW_ID | XCC_ID << 32, s_memrealtime, blockIdx} at the workgroup's start and
-// end to stamps[4 + 4 i] (stamps[0]: the record count), across calls (tools/experiments/
-// residency_probe.py: do the two kernels of different batches in flight share CUs?)
-constexpr uint32_t kDbgResLog = 1u << 24;
-constexpr uint32_t kResLogCap = (3u * 8192 * 16 - 4) / 4;
-__device__ __forceinline__ void res_log(unsigned long long* log, uint32_t tag) {
-    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
-    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
-    const unsigned long long i = atomicAdd(log, 1ull);
-    if (i < kResLogCap) {
-        unsigned long long* r = log + 4 + 4 * i;
-        r[0] = tag;
-        r[1] = hw | ((unsigned long long)xcc << 32);
-        r[2] = t;
-        r[3] = blockIdx.x;
-    }
-}
-#ifdef DHT_RESLOG   // the log's code only in the measurement build (build_variant.sh ... -DDHT_RESLOG)
-#define RES_LOG(tag) \
-    do { if ((a.dbg & kDbgResLog) && threadIdx.x == 0) res_log(a.stamps, (tag)); } while (0)
-#else
-#define RES_LOG(tag) do { } while (0)
-#endif
 
 // Flush the stage: the entries move to registers, are counting-sorted by partition back
 // into the stage, and every partition's run is then written with consecutive lanes on
@@ -301,7 +276,6 @@ template <bool Narrow>
 __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* hist, uint32_t* wsum, uint32_t poff,
                          uint32_t ibase) {
     const uint32_t np = 1u << a.b1;
-    if (a.dbg & 128) { sync_lds(); return; }
     for (uint32_t i = threadIdx.x; i <= np; i += kF2Threads) hist[i] = 0;
     sync_lds();
     uint2 e[kStagePer];
@@ -322,7 +296,7 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
     for (uint32_t i = 0; i < 8; ++i) {
         const uint32_t p = i * kF2Threads + threadIdx.x;
         const uint32_t c = p < np ? hist[p] : 0u;
-        res[i] = c && !(a.dbg & 8) ? atomicAdd(a.pcount + set_off + p, c) : 0u;
+        res[i] = c ? atomicAdd(a.pcount + set_off + p, c) : 0u;
     }
     F2_STAMP(3);
     scan_lds<kF2Threads>(hist, np, wsum);   // hist = partition starts inside the stage
@@ -348,13 +322,11 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
     }
     sync_lds();
     F2_STAMP(4);
-    if (!(a.dbg & 2)) {
-        for (uint32_t j = threadIdx.x; j < cnt; j += kF2Threads) {
-            const uint2 x = stage_get<Narrow>(stage, a.stage, ibase, j);
-            const uint32_t p = top_bits(x.x, a.b1);
-            const uint32_t pos = hist[p] + j;
-            if (pos < a.pcap) a.pbuf[(uint64_t)((poff + p) * kSets + set) * a.pcap + pos] = x;
-        }
+    for (uint32_t j = threadIdx.x; j < cnt; j += kF2Threads) {
+        const uint2 x = stage_get<Narrow>(stage, a.stage, ibase, j);
+        const uint32_t p = top_bits(x.x, a.b1);
+        const uint32_t pos = hist[p] + j;
+        if (pos < a.pcap) a.pbuf[(uint64_t)((poff + p) * kSets + set) * a.pcap + pos] = x;
     }
     sync_lds();
 }
@@ -362,18 +334,12 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
 // Loads are unconditional 16-B loads (no data-dependent branches, so every load of the
 // ring stays in flight): addresses past the id range are clamped into the plane
 // allocation and their words are masked by the caller's range test.
-#ifndef DHT_S1_RING
-#define DHT_S1_RING 8   // (override: ring-depth A/B builds)
-#endif
-constexpr uint32_t kRing = DHT_S1_RING;     // S1's ring (two 512-thread workgroups per CU: 64 KB each)
+constexpr uint32_t kRing = 8;    // S1's ring (two 512-thread workgroups per CU: 64 KB each)
 // F2's ring: 2 sub-steps = 32 KB in flight per CU.  A pure 64 MB stream by one 1024-thread
 // workgroup per CU (tools/experiments/stream_probe.hip, profiles/r03/experiments) takes
 // 13.3 us with 8 (128 KB in flight), 11.7 with 4, 11.1 with 3, 10.3 with 2: a deeper ring only
 // queues longer.  F2 at cfg 2: 21.9 us with 4, 21.3 with 3, 20.7 with 2 (round 2: 8, 24.1 us)
-#ifndef DHT_F2_RING
-#define DHT_F2_RING 2   // (override: ring-depth A/B builds)
-#endif
-constexpr uint32_t kF2Ring = DHT_F2_RING;
+constexpr uint32_t kF2Ring = 2;
 // The ring loads are buffer loads through a descriptor based at the workgroup's first id
 // (f2_rsrc): the plane pointers come from sub-partition descriptors in memory, whose address
 // space the compiler cannot infer -- plain loads through them are FLAT loads, which also count
@@ -400,10 +366,9 @@ __device__ __forceinline__ uint4 f2_load1(__amdgpu_buffer_rsrc_t rs, uint32_t lo
 // a.seg ids (ranges longer than one stage-full: large sub-partitioned sets) -- its own
 // instantiation, because the flush inlined in the loop keeps the ring live across it (128
 // VGPRs, the whole register file at 16 waves per CU, where kF2Sparse needs 68 and leaves
-// room for the other stream's F1 / F4 waves); kF2Stream is the streaming-only
-// ablation (DHTGPU_DBG & 64).
+// room for the other stream's F1 / F4 waves).
 // kF2Narrow is kF2Sparse over the 6-B narrow stage (a workgroup's range < 2^16 ids).
-constexpr uint32_t kF2Dense = 0, kF2Sparse = 1, kF2Stream = 2, kF2Seg = 3, kF2Narrow = 4;
+constexpr uint32_t kF2Dense = 0, kF2Sparse = 1, kF2Seg = 3, kF2Narrow = 4;
 
 // Src: kF2One -- one set: its descriptor from the kernel arguments, the ring through plain
 // global loads; kF2Subs -- several sub-partitions (descriptors read from memory, the ring
@@ -432,7 +397,6 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     const uint64_t lo64 = (uint64_t)(blockIdx.x - d.blk0) * d.per_blk;
     if (lo64 >= d.n) return;
     F2_STAMP(0);
-    RES_LOG(0x20);
     const uint32_t* const w0 = d.w0;
     const uint32_t poff = sub * np;   // this sub-partition's first partition
     const uint32_t lo = (uint32_t)lo64;
@@ -454,7 +418,6 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
 #pragma unroll
             for (uint32_t r = 0; r < 4; ++r) {
                 uint32_t i = i0 + (r * kF2Threads + threadIdx.x) * 4;
-                if (a.dbg & 512) i = (i + (blockIdx.x & 31) * 512) & (a.nwords - 1);   // experiment: rotated start
                 ic[r] = i < a.nwords ? i : a.nwords - 4;
                 t[r] = *reinterpret_cast<const uint4*>(bsrc + ic[r]);
             }
@@ -495,9 +458,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
 #pragma unroll
         for (uint32_t r = 0; r < kF2Ring; ++r) {
             const uint32_t sb = c0 + r * kF2Sub;
-            if (Mode == kF2Stream) {
-                cnt += ring[r].x ^ ring[r].y ^ ring[r].z ^ ring[r].w;
-            } else if (sb < hi) {   // block-uniform
+            if (sb < hi) {   // block-uniform
                 if (Mode == kF2Dense && cnt > a.stage - kF2Sub) {
                     f2_flush<false>(a, cnt, stage, hist, wsum, poff, 0u);
                     cnt = 0;
@@ -572,7 +533,6 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
             ring[r] = Subs ? f2_load1<NT>(rs, lo, sb + kF2Ring * kF2Sub, lim) : f2_load1g(w0, sb + kF2Ring * kF2Sub, lim);
         }
     }
-    if (Mode == kF2Stream) { if (cnt == 0x12345678u) a.ctr[4] = cnt; return; }
     if (Sparse) {
         sync_lds();
         cnt = misc[0] < a.stage ? misc[0] : a.stage;
@@ -590,7 +550,6 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
         }
     }
     F2_STAMP(5);
-    RES_LOG(0x21);
 }
 
 // ---- candidate order ------------------------------------------------------------------
@@ -859,13 +818,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         a.gidx = d.gidx;
         a.base = d.base;
     }
-#ifdef DHT_F3_NOMAP
-    a.gidx = nullptr;   // measurement build: results left sub-partition-local (no map reads)
-    a.base = 0;
-#endif
     F3_STAMP(0);
-    if (Diag) RES_LOG(0x30);
-    if (Diag && (a.dbg & 1024)) __builtin_amdgcn_s_setprio(3);   // experiment: loads/sort first
     // survivors are sorted by their prefix bits [b1, Lq); a target answers from the deepest
     // level L in [Lm, Lq] whose subtree sub(t, L) holds >= want ids (a contiguous range)
     const uint32_t nsub = 1u << (a.Lq - a.b1);
@@ -928,7 +881,6 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     F3_STAMP(1);
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     constexpr uint32_t NWV = kF3Threads / 64;
-    if (Diag && (a.dbg & 32)) return;
     if (m > a.cap || over) {
         // strongly clustered ids: this partition's targets take the exact brute-force path
         if (threadIdx.x == 0) ntie[2] = atomicAdd(a.ctr, mt);   // one reservation for the block
@@ -974,7 +926,6 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     for (uint32_t u = 0; u < kF3Per; ++u)
         if (rk[u] != DHT_NONE) S[sofs[__builtin_amdgcn_ubfe(e[u].x, sq_sh, a.Lq - a.b1)] + rk[u]] = e[u];
     F3_STAMP(3);
-    if (Diag && (a.dbg & 16)) return;
     const uint32_t want = Exact ? (uint32_t)K : (a.n < a.k ? (uint32_t)a.n : a.k);
     const bool full_row = Exact && ((uintptr_t)a.out_idx & 15) == 0;
     for (uint32_t t0i = 0; t0i < mt; t0i += kF3Threads) {
@@ -983,7 +934,6 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         if (threadIdx.x == 0) slow[kF3Threads] = 0;
         sync_lds();
         if (t0i == 0) F3_STAMP(4);
-        if (Diag && (a.dbg & 1024)) __builtin_amdgcn_s_setprio(0);
         // A: G lanes per target (G = 4 / 2 / 1 as the chunk's targets fill the block).  Lane
         // j of a group scans candidates lo + j, lo + j + G, ... into its own top-K and the
         // group merges its lists with DPP butterflies (f3_merge).  G = 1 deals the targets
@@ -1034,7 +984,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                     uint32_t nxt = S[o < hi ? o : lo].x;   // next candidate's word, read ahead
                     for (; o < hi; o += G) {
                         const uint32_t c = ((nxt ^ t0) << 12) | o;
-                        nxt = (Diag && (a.dbg & 2048)) ? nxt * 2654435761u + o : S[o + G < hi ? o + G : o].x;   // 2048: no LDS (timing only)
+                        nxt = S[o + G < hi ? o + G : o].x;
                         lmin = min(lmin, max(c, key[K - 1]));
 #pragma unroll
                         for (int r = K - 1; r > 0; --r) key[r] = med3_u32(key[r - 1], key[r], c);
@@ -1077,9 +1027,6 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                 bool tie = rmin == dk[want - 1];
 #pragma unroll
                 for (int r = 0; r + 1 < K; ++r) tie = tie || ((uint32_t)r + 1 <= want && dk[r] == dk[r + 1]);
-#ifdef DHT_F3_NOTIES
-                tie = false;   // measurement build: w0 ties answered as if none (results may be wrong)
-#endif
                 if (tie && !Subs) {
                     if (gj == 0) {   // answered by the wave below, after the groups' results
                         tinl = true;
@@ -1132,14 +1079,11 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
 #pragma unroll
                         for (int r = 0; r < K; ++r) {
                             if (!a.rec.w0_direct) w0[r] = a.rec.planes[res[r]];
-                            // 2^16: word 1 not gathered (records wrong; timing only)
-                            w1[r] = (Diag && (a.dbg & (1u << 16))) ? w0[r] : a.rec.planes[a.rec.stride + res[r]];
+                            w1[r] = a.rec.planes[a.rec.stride + res[r]];
                             gi[r] = a.rec.gidx ? a.rec.gidx[res[r]] : res[r] + a.rec.base;
                         }
                         uint32_t* ro = a.rec.out + (uint64_t)qi * a.k * 3;
-                        if (Diag && (a.dbg & (1u << 17))) {
-                            // 2^17: records not stored (timing only)
-                        } else if (full_row && ((uintptr_t)a.rec.out & 15) == 0) {
+                        if (full_row && ((uintptr_t)a.rec.out & 15) == 0) {
                             // k == K == want: the row is 3K words from a 16-B boundary (K % 4 == 0),
                             // 3K / 4 vector stores instead of 3K dword stores
                             uint32_t wds[3 * K];
@@ -1265,7 +1209,6 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     // this partition's deferred ties for F4 (a plain store: no shared counter to serialise on)
     if (threadIdx.x == 0 && ntie[0]) a.tie_cnt[p] = ntie[0] < kTieSlots ? ntie[0] : kTieSlots;
     F3_STAMP(7);
-    if (Diag) RES_LOG(0x31);
 }
 
 // ---- F4: the fallback targets (K1 scan, run-time roles) and the deferred ties -------------
@@ -1636,33 +1579,14 @@ BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
             if (lq == P.Lm) break;
         }
     }
-#ifdef DHT_F3_FIVE   // experiment: five F3 workgroups per CU (the cfg-2 period is LDS x time bound)
-    if (P.fits) {
-        const double sub = (double)(1ull << (P.Lm - P.b1)), mu1 = (double)n / (double)(1ull << P.Lm);
-        const double mean = sub * f * mu1, sd = std::sqrt(sub * f * (1.0 - f) * mu1 * mu1 + sub * f * mu1);
-        const double minc = mean + (double)DHT_F3_FIVE * 0.1 * sd + 64.0;
-        constexpr size_t kF3Lds5 = kLdsMax / 5;
-        for (uint32_t lq = P.Lq; lq >= P.Lm && lq > P.b1; --lq) {
-            const size_t fw = (size_t)f3_words(1u << (lq - P.b1)) * 4;
-            if (fw + (size_t)(kF3Threads + 64) * 8 > kF3Lds5) continue;
-            uint32_t c5 = (uint32_t)((kF3Lds5 - fw) / 8 - kF3Threads) & ~63u;
-            c5 = std::min(c5, P.f3cap);
-            if ((double)c5 >= minc) { P.Lq = lq; P.f3cap = c5; break; }
-            if (lq == P.Lm) break;
-        }
-    }
-#endif
     P.nwords = P.Lm >= 5 ? (1u << (P.Lm - 5)) : 1u;
     P.nblk1 = (q + kF1Threads - 1) / kF1Threads;
     // target buckets: mean + 6 sigma + 64 (uniform targets); overflow spills to F4
     const double mu = (double)q / (double)(1u << P.b1);
     P.tcap = ((uint32_t)(mu + 6.0 * std::sqrt(mu) + 64.0) + 63u) & ~63u;
     // F2: one persistent workgroup per CU, ranges in whole chunks
-#ifndef DHT_F2_WG_PER_CU   // experiment: more, shorter F2 workgroups (dispatched as CUs free up)
-#define DHT_F2_WG_PER_CU 1
-#endif
     const uint64_t chunks = (n + kF2Step - 1) / kF2Step;
-    const uint64_t g = (num_cus > 0 ? (uint64_t)num_cus : 256) * DHT_F2_WG_PER_CU;
+    const uint64_t g = num_cus > 0 ? (uint64_t)num_cus : 256;
     const uint64_t cpb = (chunks + g - 1) / g;
     P.per_blk = (cpb ? cpb : 1) * kF2Step;
     P.nblk2 = (uint32_t)((n + P.per_blk - 1) / P.per_blk);
@@ -1828,12 +1752,12 @@ std::once_flag g_attr_once[kMaxDevices];   // set_lds_attributes, per device (pe
 
 void set_lds_attributes() {
     const void* fs[] = {(const void*)k_f2_filter<kF2Dense, kF2One>, (const void*)k_f2_filter<kF2Sparse, kF2One>,
-                        (const void*)k_f2_filter<kF2Stream, kF2One>, (const void*)k_f2_filter<kF2Seg, kF2One>,
+                        (const void*)k_f2_filter<kF2Seg, kF2One>,
                         (const void*)k_f2_filter<kF2Dense, kF2Subs>, (const void*)k_f2_filter<kF2Sparse, kF2Subs>,
-                        (const void*)k_f2_filter<kF2Stream, kF2Subs>, (const void*)k_f2_filter<kF2Seg, kF2Subs>,
+                        (const void*)k_f2_filter<kF2Seg, kF2Subs>,
                         (const void*)k_f2_filter<kF2Narrow, kF2One>, (const void*)k_f2_filter<kF2Narrow, kF2Subs>,
                         (const void*)k_f2_filter<kF2Dense, kF2SubsNT>, (const void*)k_f2_filter<kF2Sparse, kF2SubsNT>,
-                        (const void*)k_f2_filter<kF2Stream, kF2SubsNT>, (const void*)k_f2_filter<kF2Seg, kF2SubsNT>,
+                        (const void*)k_f2_filter<kF2Seg, kF2SubsNT>,
                         (const void*)k_f2_filter<kF2Narrow, kF2SubsNT>,
                         (const void*)k_f3_answer<8, false, true, false>,  (const void*)k_f3_answer<16, false, true, false>,
                         (const void*)k_f3_answer<32, false, true, false>, (const void*)k_f3_answer<8, true, true, false>,
@@ -2070,8 +1994,7 @@ hipError_t launch_idx_to_handles(const HandleSub* tab, const uint32_t* planes, u
     return hipGetLastError();
 }
 
-hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
-    if (dirty) *dirty = false;
+hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
     if (c.skip && !c.w0s && !c.nsub) return hipErrorInvalidValue;
     if (c.nsub > kMaxSubs) return hipErrorInvalidValue;
     if (!c.q) return hipSuccess;
@@ -2093,7 +2016,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     const bool nt = 4 * n_all > kNtBytes;   // F2's ring: non-temporal past the Infinity Cache
     const BatchPlan P = plan_batch(n_max, c.q_plan, k, c.num_cus);
     const uint32_t np = 1u << P.b1, NP = nsub * np;
-    uint32_t dbg = c.dbg;
+    uint32_t dbg = c.dbg & 256u;   // the only diagnostics bit: phase stamps (results unchanged)
     hipEvent_t* ev = c.ev;
     const WsLayout Ly = ws_layout(P, nsub, q, k);
     uint8_t* const w = static_cast<uint8_t*>(c.ws);
@@ -2125,7 +2048,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     if (nblk2 > kMaxF2Blocks) return hipErrorInvalidValue;
     // the narrow stage: every workgroup's range under 2^16 ids and its survivors (mean + 8 sigma
     // + 256 on uniform ids) within the narrow stage; no segments
-    bool narrow = P.nstage && P.sparse && !seg_used && !(dbg & 64);
+    bool narrow = P.nstage && P.sparse && !seg_used;
     {
         const double f = 1.0 - std::exp(-(double)c.q_plan / (double)(1ull << P.Lm));
         for (uint32_t i = 0; i < nsub && narrow; ++i) {
@@ -2168,8 +2091,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         if (ev) hipExtLaunchKernelGGL(kern, g, b, (uint32_t)lds, s, ev[2 * i], ev[2 * i + 1], 0, args...);
         else kern<<<g, b, lds, s>>>(args...);
     };
-    if (dbg & 256) dbg &= ~kDbgResLog;
-    unsigned long long* stamps = (dbg & (256u | kDbgResLog)) ? c.stamps : nullptr;   // F3 [8192][16] then F2 [8192][16]
+    unsigned long long* stamps = (dbg & 256u) ? c.stamps : nullptr;   // F3 [8192][16] then F2 [8192][16]
     if (dbg & 256) (void)hipMemsetAsync(stamps, 0, (size_t)3 * 8192 * 16 * 8, s);
     const F1Args a1{c.tp, c.tp + c.ts, q, P.Lm, P.b1, c.skip, c.sub_shift, c.nsub ? c.sub_bits : 0u, np, P.nwords,
                     bitmap, tcount, tbuf, P.tcap, ctr, tspill};
@@ -2185,8 +2107,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         else if (nsub > 1) go(1, k_f2_filter<MM, kF2Subs>, g2, b2, l2, a2);   \
         else go(1, k_f2_filter<MM, kF2One>, g2, b2, l2, a2);                  \
     } while (0)
-        if (dbg & 64) F2_GO(kF2Stream);
-        else if (narrow) F2_GO(kF2Narrow);
+        if (narrow) F2_GO(kF2Narrow);
         else if (P.sparse && seg_used) F2_GO(kF2Seg);
         else if (P.sparse) F2_GO(kF2Sparse);
         else F2_GO(kF2Dense);
@@ -2195,12 +2116,6 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
         (void)hipEventRecord(ev[2], s);
         (void)hipEventRecord(ev[3], s);
     }
-    if (dbg & ~(48u | 256u | 512u | 1024u | 2048u | 4096u | 8192u | (7u << 16) | (1u << 23) | kDbgResLog)) {   // experiments: F1 + F2 only
-        for (int i = 4; ev && i < 8; ++i) (void)hipEventRecord(ev[i], s);
-        if (dirty) *dirty = true;   // F3 (which resets the counters and the bitmap) did not run
-        return hipGetLastError();
-    }
-    if (dirty && (dbg & 48u)) *dirty = true;   // F3 ablation exits leave counters behind
     // the base arguments are the whole set's: F4's scan (fallback targets) runs over all its ids
     F3Args a{pbuf, pcount, P.scap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, c.planes, c.stride,
              c.n, c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, fb_sub, pstat, tie_hdr, tie_cand, tie_cnt,
@@ -2210,8 +2125,6 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
 
     // F3 stages the plan's 6-sigma bound only beside F2's narrow stage (which it makes room for)
     size_t l3 = f3_lds(P, a.cap);
-    if (dbg & 4096) l3 = l3 > 81920 ? l3 : 81920;   // experiment: 2 F3 blocks per CU
-    if (dbg & 8192) l3 = l3 > 54000 ? l3 : 54000;   // experiment: 3 F3 blocks per CU
     const dim3 g3(NP), b3(kF3Threads);
     const bool ex = c.n >= k && (k == 8 || k == 16 || k == 32);
 #define F3_GO(KK, DD, SS)                                                     \
@@ -2243,10 +2156,8 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty) {
     // 33.6 -> 31.7-31.9 us (profiles/r05/experiments/f4_idle_ab.txt, f4_idle_grid_ab.txt; 16 and
     // 8 equal).  (a sub-partitioned call fills the chip alone and defers ~1 tie per partition over
     // 2,048+ partitions: the full grid keeps them at about one per wave)
-#ifndef DHT_F4_IDLE_GRID
-#define DHT_F4_IDLE_GRID 32
-#endif
-    const uint32_t nfb = (c.fb_hint && *c.fb_hint == 0u && nsub == 1) ? (uint32_t)DHT_F4_IDLE_GRID : kFbBlocks;
+    constexpr uint32_t kF4IdleGrid = 32;
+    const uint32_t nfb = (c.fb_hint && *c.fb_hint == 0u && nsub == 1) ? kF4IdleGrid : kFbBlocks;
     // one set: F3 answers its ties inline, so F4 reads no deferred-tie counts (np_ties 0)
     const FbArgs fa{fb_rec, fb_done, nfb, nsub > 1 ? NP : 0u, c.fb_hint_dev};
     const dim3 g4(nfb), b4(kF4Threads);
@@ -2424,15 +2335,7 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
                     const uint32_t h = __builtin_amdgcn_ubfe(v4[f], h_off, hb);
                     hit[f] = ((b16[h >> 5] >> (h & 31)) & 1u) && tid4 + f < rem;
                 }
-#ifdef DHT_S1_MEASURE_NOFILTER
-                if (v4[0] == 0x12345678u && v4[1] == 0x9abcdef0u) nhit = hit[0] | hit[1] | hit[2] | hit[3];   // measurement build: stream + filter only
-                if (false)
-#endif
-#ifdef DHT_S1_MEASURE_HITS_NEVER   // measurement build: the hit block kept, never entered (results incomplete)
-                if (__ballot(hit[0] || hit[1] || hit[2] || hit[3]) && a.lim == 0xFFFFFFF7u) {
-#else
                 if (__ballot(hit[0] || hit[1] || hit[2] || hit[3])) {   // rare
-#endif
                     // the 16-bit hits go to the LDS queue as they are (one LDS atomic per wave, no
                     // search in the stream: the dependent binary search per hit held the whole wave
                     // at q = 64, S1 18.6 us against 10.6 for the bare stream); the level-Ls match
@@ -2450,9 +2353,6 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
                             if (qi < kS1Queue) {
                                 hitq[qi] = make_uint4(v4[f], sb + tid4 + f, DHT_NONE, 0u);
                             } else {   // past the queue (strongly clustered ids): matched and appended here
-#ifdef DHT_S1_MEASURE_NO_OVERFLOW   // measurement build (results incomplete past the queue)
-                                continue;
-#endif
                                 const uint32_t sl = match(v4[f]);
                                 if (sl != DHT_NONE) {
                                     const uint32_t j = sb + tid4 + f;
@@ -2468,9 +2368,6 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
         }
     }
     __syncthreads();
-#ifdef DHT_S1_MEASURE_NOTAIL
-    return;   // measurement build: no queue flush (results incomplete)
-#endif
     // the queue to the buckets (the level-Ls match of a 16-bit hit first): word 1 and the slot
     // reservation in one round trip
     const uint32_t nq = nhit < kS1Queue ? nhit : kS1Queue;
@@ -2478,16 +2375,8 @@ __global__ __launch_bounds__(NT) void k_s1_filter(SmallArgs a) {
         const uint4 e = hitq[i];
         const uint32_t sl = e.z != DHT_NONE ? e.z : match(e.x);
         if (sl == DHT_NONE) continue;
-#ifdef DHT_S1_MEASURE_TAIL_NOW1   // measurement builds (results wrong): the tail without its word-1 load / its atomic
-        const uint32_t w1 = 0u;
-#else
         const uint32_t w1 = a.w1[e.y];
-#endif
-#ifdef DHT_S1_MEASURE_TAIL_NOATOM
-        const uint32_t pos = i % kSmallCap;
-#else
         const uint32_t pos = atomicAdd(a.cnt + sl, 1u);
-#endif
         if (pos < kSmallCap) a.cand[sl * kSmallCap + pos] = make_uint4(e.x, e.y, w1, 0u);
     }
 }

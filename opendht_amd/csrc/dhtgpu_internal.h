@@ -137,6 +137,9 @@ struct SubSpec {
 };
 
 constexpr uint32_t kHandleMark = 0x80000000u;   // sets hold < 2^31 ids (batch_supported)
+// DHTGPU_DBG bits the library honours (dhtgpu_ctx::dbg): 256 = phase stamps, 2^23 = K6 for
+// small batches.  Diagnostics only -- no bit changes a result (tests/test_abi.py pins the mask).
+constexpr uint32_t kDbgAllowed = 256u | (1u << 23);
 // One sub-partition in handle space: handles [off, off + n) name its ids in its compacted order.
 struct HandleSub {
     uint64_t n;
@@ -174,14 +177,13 @@ struct BatchCall {
     // kHandleMark) and a pass after F4 turns them into handles through htab
     uint32_t handles; const HandleSub* htab;
     int num_cus;
-    uint32_t dbg;                          // DHTGPU_DBG diagnostics switches (0 in production)
+    uint32_t dbg;                          // DHTGPU_DBG & kDbgAllowed (0 in production)
     const volatile uint32_t* fb_hint;      // nullable: the slot's last fallback-list length (mapped host memory)
     uint32_t* fb_hint_dev;                 // its device address (F4 writes it)
     unsigned long long* stamps;            // dbg & 256: phase stamps [2 * 8192 * 16]
     hipEvent_t* ev;                        // nullable: 8 events around F1..F4
 };
-// *dirty (nullable) = an experiment exit skipped the kernels that re-zero the workspace head
-hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s, bool* dirty);
+hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s);
 // KS (batch.hip): batches of at most 64 targets -- one pass over word 0 and one workgroup per
 // distinct target prefix (K6's results).  sws: small_bytes(), zero before its first use (left
 // zero); parity: alternates between consecutive calls on one workspace (two counter sets);

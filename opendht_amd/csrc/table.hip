@@ -133,18 +133,9 @@ __global__ __launch_bounds__(256) void k_find_closest(
 // atomic per histogram bin it touched, and the 1,024 workgroups of 256 threads ended together with
 // 1,024 atomics on bin 0's address, serialised at the memory side (0.0926 -> 0.088 ms without them,
 // 0.0935 -> 0.0897-0.092 with 256 workgroups of 1,024: profiles/r05/experiments/k2_blocks.txt)
-#ifndef DHT_K2_BLOCK
-#define DHT_K2_BLOCK 1024
-#endif
-constexpr int kClsBlock = DHT_K2_BLOCK;
-#ifndef DHT_K2_PERCU
-#define DHT_K2_PERCU 1
-#endif
-#ifndef DHT_K2_U
-#define DHT_K2_U 3
-#endif
-constexpr int kClsPerCu = DHT_K2_PERCU;          // workgroups per CU (16 waves per CU: 0.105 -> 0.096 ms against 32 in r04)
-constexpr uint32_t kClsU = DHT_K2_U;             // uint4 of word 0 per lane per chunk
+constexpr int kClsBlock = 1024;
+constexpr int kClsPerCu = 1;                     // workgroups per CU (16 waves per CU: 0.105 -> 0.096 ms against 32 in r04)
+constexpr uint32_t kClsU = 3;                    // uint4 of word 0 per lane per chunk
 static_assert(4 * kClsU <= 15, "4-bit histogram fields flushed once per chunk");
 constexpr uint32_t kClsT = 10, kClsCells = 1u << kClsT;
 constexpr uint32_t kClsExact = 0x8000u;          // table flag: the cell's ids take the exact path
@@ -152,6 +143,12 @@ constexpr uint32_t kClsSkip = 15u;               // histogram field an exact-pat
 constexpr uint32_t kRegT = 15u;                  // register path: commonBits below this from word 0
 constexpr uint32_t kClsFlush = 255u / (4 * kClsU);   // chunks per byte-counter flush
 constexpr uint32_t kClsQCap = 1024;              // queued exact-path ids per wave (> one chunk's 4 * 64 * kClsU)
+// k_classify's static LDS (sf, sh, lut, s_bad, s_map, s_q, s_qn below): 73 KB with the exact-path
+// queues -- more than the 64 KB per workgroup of earlier CDNA parts; gfx950 gives a workgroup the
+// CU's 160 KB (the Makefile builds gfx950 only)
+constexpr size_t kClsLds = (size_t)DHT_W * 256 * 4 + 161 * 4 + (size_t)(1u << 10) * 2 + 4 + 16 +
+                           (size_t)(kClsBlock / 64) * kClsQCap * 4 + (kClsBlock / 64) * 4;
+static_assert(kClsLds <= kLdsBytes, "k_classify's LDS exceeds gfx950's 160 KB per workgroup");
 
 // the reference's findBucket over the firsts in LDS (sf: plane-major, nb entries per plane):
 // the last bucket whose first <= id, bucket 0 when none (a linear walk from the front stops
@@ -362,11 +359,7 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
             for (uint32_t u = 0; u < kClsU; ++u) {
                 const uint64_t i4 = c * CH + u * 64 + lane;
                 if (FULL || 4 * i4 + 3 < n) {
-#ifdef DHT_K2_NTSTORE
-                    __builtin_nontemporal_store(packed[u], reinterpret_cast<uint32_t*>(out_bucket + 4 * i4));
-#else
                     *reinterpret_cast<uint32_t*>(out_bucket + 4 * i4) = packed[u];
-#endif
                 } else {
                     for (uint32_t e = 0; e < 4; ++e)
                         if (4 * i4 + e < n) out_bucket[4 * i4 + e] = (uint8_t)(packed[u] >> (8 * e));
@@ -406,10 +399,8 @@ __global__ __launch_bounds__(kClsBlock) void k_classify(
     answer_queue();
     flush_acc();
     __syncthreads();
-#ifndef DHT_K2_NOHIST   // measurement build: no global histogram atomics (results incomplete)
     for (uint32_t i = threadIdx.x; i < 161; i += kClsBlock)
         if (sh[i]) atomicAdd(hist + i, (unsigned long long)sh[i]);
-#endif
 }
 
 // ---------------------------------------------------------------------------------

@@ -14,6 +14,16 @@ the full keys.  The exchange is always issued (fixed size, stream-ordered, no ho
 more than TIE_CAP rows tie, `settle_overflow_*` (after a synchronisation) repeats it for every
 row.  With one rank there is nothing to tie across and no second exchange.
 
+Per-step contract (a pipelined caller): a step's results are final once its stream has run
+merge_* AND `unsettled(tx)` is false (a device flag, no host sync); when it is true -- more than
+TIE_CAP rows tied, crafted ids only -- the caller synchronises and calls settle_overflow_* before
+reading the rows.  merge_* never returns such a step's rows as final silently: the flag is the tie
+count itself, written by K3 on the step's stream.
+
+Streams: every device step of one lookup (K3, the tie words, the full-key settlement) runs on ONE
+stream -- the caller's, or torch's current stream when the caller passes none -- and that stream
+must be torch's current stream, because RCCL orders the collectives after it.
+
 Two exchanges: the all-gather (`gather_records`, the north star's: every rank merges every
 target, so every rank holds the same tie rows) and the all-to-all by target slice
 (`exchange_records`: rank r receives only the records of the targets it owns, shard_range(q,
@@ -34,27 +44,52 @@ def shard_range(n, world, rank):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-_GLOO = {}   # group -> its backend is gloo (looked up once: a per-step lookup costs microseconds)
+_GROUPS = {}   # resolved process group -> (its backend is gloo, world size): looked up once per group
+
+
+def _group_info(group):
+    """(gloo?, world size) of `group` (None = the default group, resolved to its current object, so
+    a destroyed and re-created default group -- another backend -- is looked up afresh)"""
+    g = group if group is not None else dist.group.WORLD
+    info = _GROUPS.get(g)
+    if info is None:
+        if len(_GROUPS) > 64:
+            _GROUPS.clear()
+        info = _GROUPS[g] = (dist.get_backend(group) == "gloo", dist.get_world_size(group))
+    return info
 
 
 def _host_staged(group, *ts):
     """gloo moves host tensors only: device tensors are staged through host copies (the
     one-GPU multi-rank rehearsal); RCCL takes device tensors as they are"""
-    g = _GLOO.get(group)
-    if g is None:
-        g = _GLOO[group] = dist.get_backend(group) == "gloo"
-    return g and any(t.is_cuda for t in ts)
+    return _group_info(group)[0] and any(t.is_cuda for t in ts)
+
+
+def _stream(stream, t):
+    """The one stream of a lookup's device steps: the caller's, else torch's current stream on
+    t's device (RCCL orders the collectives after the current stream, so a caller's stream must be
+    that one).  None for host tensors (the CPU tests' stand-in ops)."""
+    if not t.is_cuda:
+        return stream
+    cur = torch.cuda.current_stream(t.device).cuda_stream
+    if stream is None:
+        return cur
+    if stream != cur:
+        raise ValueError("sharding: the lookup's stream must be torch's current stream (RCCL orders the "
+                         "collectives after it); set it with torch.cuda.set_stream first")
+    return stream
 
 
 def gather_records(rec, group=None, out=None):
     """All-gather this rank's (q, k, W) int32 records -> (world, q, k, W).  `out` may be a
     preallocated (world*q, k, W) buffer (the concatenated form every backend accepts); list l of
     the result is rank l's shard.  Also moves the tie words ((TIE_CAP, k, 3) per rank)."""
+    world = _group_info(group)[1]
     if out is None:
-        world = dist.get_world_size(group)
         out = torch.empty((world * rec.shape[0],) + tuple(rec.shape[1:]), dtype=rec.dtype, device=rec.device)
-    else:
-        world = out.shape[0] // rec.shape[0]
+    elif tuple(out.shape) != (world * rec.shape[0],) + tuple(rec.shape[1:]):
+        raise ValueError(f"gather_records: out {tuple(out.shape)} is not (world * q, ...) for world {world} and "
+                         f"records {tuple(rec.shape)}")
     if _host_staged(group, rec, out):
         h = torch.empty(out.shape, dtype=out.dtype)
         dist.all_gather_into_tensor(h, rec.contiguous().cpu(), group=group)
@@ -67,7 +102,7 @@ def gather_records(rec, group=None, out=None):
 def exchange_records(rec, group=None, out=None):
     """All-to-all of this rank's (q, k, W) records by target slice -> (world, q_r, k, W): list s
     holds rank s's candidates for this rank's targets shard_range(q, world, rank)."""
-    world = dist.get_world_size(group)
+    world = _group_info(group)[1]
     rank = dist.get_rank(group)
     q = rec.shape[0]
     sizes = [b - a for a, b in (shard_range(q, world, r) for r in range(world))]
@@ -105,6 +140,12 @@ class TieExchange:
         self.words_in = torch.empty((world, TIE_CAP, k, 3), dtype=torch.int32, device=device)
 
 
+def unsettled(tx):
+    """Device flag (0-dim bool tensor, no host sync): the last merge_* through `tx` listed more tie
+    rows than one tie exchange settles, so its rows are final only after settle_overflow_*."""
+    return tx.ties[0] > TIE_CAP
+
+
 def _check(code, what):
     if code != 0:
         raise RuntimeError(f"libdhtgpu: {what} failed ({code})")
@@ -139,6 +180,7 @@ def merge_allgather(ops, rec, gathered, k, out_idx, out_cnt, tx, idx_base, strea
     rec: this rank's own (q, k, 3) records (the tie words come from its own id set); gathered:
     (world, q, k, 3).  Stream-ordered, no host sync."""
     world = gathered.shape[0]
+    stream = _stream(stream, rec)
     ops.merge(gathered, 0, k, out_idx, out_cnt, tx.ties if world > 1 else None, stream)
     if world == 1:
         return
@@ -154,6 +196,7 @@ def merge_alltoall(ops, rec, exch, k, tlo, out_idx, out_cnt, tx, idx_base, strea
     them to the owners."""
     world, qr = exch.shape[0], exch.shape[1]
     q = rec.shape[0]
+    stream = _stream(stream, rec)
     if qr:
         ops.merge(exch, tlo, k, out_idx, out_cnt, tx.ties if world > 1 else None, stream)
     else:
@@ -175,6 +218,7 @@ def settle_overflow_allgather(ops, rec, gathered, k, out_idx, out_cnt, tx, idx_b
     on every rank of the all-gather route), every row is merged again on the full keys.  Returns
     the tie count."""
     world, q = gathered.shape[0], gathered.shape[1]
+    stream = _stream(stream, rec)
     count = int(tx.ties[0].item()) if world > 1 else 0
     if count > TIE_CAP:
         words = torch.empty((q, k, 3), dtype=torch.int32, device=rec.device)
@@ -192,9 +236,10 @@ def settle_overflow_alltoall(ops, rec, exch, k, tlo, out_idx, out_cnt, tx, idx_b
     world, qr = exch.shape[0], exch.shape[1]
     if world == 1:
         return 0
+    stream = _stream(stream, rec)
     mine = int(tx.ties[0].item()) if qr else 0
     top = torch.tensor([mine], dtype=torch.int64)
-    if dist.get_backend(group) != "gloo":
+    if not _group_info(group)[0]:
         top = top.to(rec.device)
     dist.all_reduce(top, op=dist.ReduceOp.MAX, group=group)
     if int(top.item()) > TIE_CAP:

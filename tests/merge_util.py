@@ -40,11 +40,16 @@ def host_words_fn(ids, rec_host):
 
 
 def ctx_words_fn(L, ctxs, rec, bases, k, stream=None):
-    """words_fn over live shard contexts: dhtgpu_tie_words_dev on each list's own records."""
+    """words_fn over live shard contexts: dhtgpu_tie_words_dev on each list's own records, on the
+    stream of the merge (torch's current stream when none is given: K3 and the tie words must be
+    ordered on one stream -- the contexts' own streams do not wait for it)."""
+    import torch
+
     def fn(j, ties, out, cap):
         q = rec.shape[1]
+        s = stream if stream is not None else torch.cuda.current_stream(rec.device).cuda_stream
         ctxs[j].tie_words_dev(rec[j].data_ptr(), q, k, bases[j], ties.data_ptr() if ties is not None else None,
-                              cap, 0, out.data_ptr(), stream)
+                              cap, 0, out.data_ptr(), s)
     return fn
 
 
@@ -57,11 +62,12 @@ def merge(L, rec, tp, ts, k, words, tie_cap=256, force_all=False):
     import torch
     lists, q, kin = rec.shape[0], rec.shape[1], rec.shape[2]
     dev = rec.device
+    s = torch.cuda.current_stream(dev).cuda_stream   # K3, the tie words and the settlement: one stream
     out = torch.empty((q, k), dtype=torch.int32, device=dev)
     cnt = torch.empty(q, dtype=torch.int32, device=dev)
     ties = torch.full((1 + tie_cap,), -1, dtype=torch.int32, device=dev)   # merge_dev zeroes the count
     assert L.dhtgpu_merge_dev(rec.data_ptr(), lists, q, kin, tp.data_ptr(), ts, k, out.data_ptr(), cnt.data_ptr(),
-                              ties.data_ptr() if lists > 1 else None, tie_cap, None) == 0
+                              ties.data_ptr() if lists > 1 else None, tie_cap, s) == 0
     count = 0
     if lists > 1:
         kind, fn = words
@@ -84,12 +90,12 @@ def merge(L, rec, tp, ts, k, words, tie_cap=256, force_all=False):
         if tie_cap:
             w = fill(False)
             assert L.dhtgpu_merge_ties_dev(rec.data_ptr(), w.data_ptr(), lists, q, kin, tp.data_ptr(), ts, k,
-                                           ties.data_ptr(), tie_cap, out.data_ptr(), cnt.data_ptr(), None) == 0
+                                           ties.data_ptr(), tie_cap, out.data_ptr(), cnt.data_ptr(), s) == 0
         torch.cuda.synchronize()
         count = int(ties[0].item())
         if count > tie_cap or force_all:
             w = fill(True)
             assert L.dhtgpu_merge_ties_dev(rec.data_ptr(), w.data_ptr(), lists, q, kin, tp.data_ptr(), ts, k, None,
-                                           0, out.data_ptr(), cnt.data_ptr(), None) == 0
+                                           0, out.data_ptr(), cnt.data_ptr(), s) == 0
     torch.cuda.synchronize()
     return out.cpu().numpy().view(np.uint32).copy(), cnt.cpu().numpy().view(np.uint32).copy(), count

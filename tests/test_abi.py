@@ -78,3 +78,29 @@ def test_table_depth_vs_oracle():
         for b in range(firsts.shape[0]):
             assert opendht_amd.table_depth(firsts, b) == O.depth(firsts, b)
     assert opendht_amd.table_depth(np.zeros((0, 20), np.uint8), 0) == 0
+
+
+def test_production_build_has_no_measurement_switches():
+    """The shipped library cannot return different nodes (SURVEY §8(b) error contract): the
+    sources carry no result-altering measurement macro (#if/#ifdef on a DHT_* name), the Makefile
+    takes no extra defines and builds gfx950 only, and DHTGPU_DBG is masked at context creation to
+    the diagnostics bits that leave results unchanged (phase stamps; K6 instead of KS for small
+    batches -- both exact; tests/test_gpu_parity.py::test_dbg_bits_leave_results_unchanged)."""
+    csrc = os.path.join(ROOT, "opendht_amd", "csrc")
+    bad = []
+    for fn in sorted(os.listdir(csrc)):
+        if not fn.endswith((".hip", ".h")):
+            continue
+        for no, line in enumerate(open(os.path.join(csrc, fn)), 1):
+            if re.match(r"\s*#\s*(if|ifdef|ifndef|elif)\b.*\bDHT_[A-Z0-9_]+", line):
+                bad.append(f"{fn}:{no}: {line.strip()}")
+    assert not bad, bad
+    mk = open(os.path.join(csrc, "Makefile")).read()
+    assert "EXTRA" not in mk and "$(error" in mk and "ifneq ($(ARCH),gfx950)" in mk
+    internal = open(os.path.join(csrc, "dhtgpu_internal.h")).read()
+    m = re.search(r"constexpr uint32_t kDbgAllowed = ([^;]+);", internal)
+    assert m and m.group(1).replace(" ", "") == "256u|(1u<<23)", m
+    api = open(os.path.join(csrc, "api.hip")).read()
+    assert re.search(r'getenv\("DHTGPU_DBG"\)\)\s*c->dbg = .*& kDbgAllowed;', api)
+    batch = open(os.path.join(csrc, "batch.hip")).read()
+    assert "c.dbg & 256u" in batch   # K6 honours the stamp bit only

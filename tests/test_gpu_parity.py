@@ -1106,3 +1106,19 @@ def test_f4_half_grid_then_fallback_list():
             assert np.array_equal(cnt, wcnt), k
             bad = np.nonzero((got != want).any(axis=1))[0]
             assert bad.size == 0, f"k={k}: {bad.size} targets differ, first {bad[:5]}"
+
+
+def test_dbg_bits_leave_results_unchanged(monkeypatch):
+    """DHTGPU_DBG with every bit set (the variable is read at context creation and masked to the
+    diagnostics bits; tests/test_abi.py pins the mask): K6, KS (here: K6 on small batches, bit 2^23)
+    and the sub-partitioned route return exactly the oracle's nodes."""
+    import opendht_amd
+    monkeypatch.setenv("DHTGPU_DBG", str(0xFFFFFFFF & ~256))   # 256 (stamps) prints to stderr: left out
+    ids = O.gen_ids(4242, 1 << 20)
+    with opendht_amd.Context(0) as c:
+        c.set_ids(ids)
+        for q in (5, 64, 3000):
+            tg = O.gen_ids(4243 + q, q)
+            want, wcnt = O.topk(ids, tg, 8)
+            got, cnt = c.batch_topk(tg, 8)
+            assert np.array_equal(cnt, wcnt) and np.array_equal(got, want), q

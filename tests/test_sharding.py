@@ -144,7 +144,7 @@ def _crafted(n, q, seed):
     return ids, tg
 
 
-def _worker_proto(rank, world, port, n, q, k, exchange, cap, ret):
+def _worker_proto(rank, world, port, n, q, k, exchange, cap, ret, settle=True):
     """The whole protocol (records -> exchange -> K3 -> tie exchange -> overflow settlement) with
     host stand-ins for the device steps."""
     import oracle as O
@@ -162,17 +162,19 @@ def _worker_proto(rank, world, port, n, q, k, exchange, cap, ret):
         g = sharding.gather_records(rec)
         oi, oc = torch.empty((q, k), dtype=torch.int32), torch.empty(q, dtype=torch.int32)
         sharding.merge_allgather(ops, rec, g, k, oi, oc, tx, lo)
-        nt = sharding.settle_overflow_allgather(ops, rec, g, k, oi, oc, tx, lo)
+        flagged = bool(sharding.unsettled(tx))
+        nt = sharding.settle_overflow_allgather(ops, rec, g, k, oi, oc, tx, lo) if settle else int(tx.ties[0])
     else:
         tlo, thi = sharding.shard_range(q, world, rank)
         ex = sharding.exchange_records(rec)
         oi, oc = torch.empty((max(thi - tlo, 1), k), dtype=torch.int32), torch.empty(max(thi - tlo, 1), dtype=torch.int32)
         sharding.merge_alltoall(ops, rec, ex, k, tlo, oi, oc, tx, lo)
-        nt = sharding.settle_overflow_alltoall(ops, rec, ex, k, tlo, oi, oc, tx, lo)
+        flagged = bool(sharding.unsettled(tx))
+        nt = sharding.settle_overflow_alltoall(ops, rec, ex, k, tlo, oi, oc, tx, lo) if settle else int(tx.ties[0])
     want, wcnt = O.topk(ids, tg[tlo:thi], k, threads=2)
     got = oi.numpy().view(np.uint32)[:thi - tlo]
     ret[rank] = (bool(np.array_equal(got, want) and np.array_equal(oc.numpy()[:thi - tlo].astype(np.uint32), wcnt)),
-                 nt)
+                 nt, flagged)
     dist.destroy_process_group()
 
 
@@ -188,6 +190,25 @@ def test_tie_protocol_gloo(world, exchange, cap):
     mp.spawn(_worker_proto, args=(world, _free_port(), 1500, 60, 8, exchange, cap, ret), nprocs=world, join=True)
     assert all(ret[r][0] for r in range(world)), dict(ret)
     assert max(ret[r][1] for r in range(world)) > 0
+    # the overflow flag is raised exactly where more rows tied than one exchange settles
+    assert all(ret[r][2] == (ret[r][1] > cap) for r in range(world)), dict(ret)
+
+
+def test_tie_overflow_flagged_when_not_settled():
+    """More than TIE_CAP rows tie (cap 2) and the caller skips settle_overflow_*: the rows past the
+    cap are provisional, and unsettled(tx) says so on every rank that holds them -- a
+    pipelined caller reads the flag instead of silently taking inexact rows.  Rows of a rank whose
+    flag is down are exact."""
+    world = 2
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker_proto, args=(world, _free_port(), 1500, 60, 8, "allgather", 2, ret, False), nprocs=world,
+             join=True)
+    for r in range(world):
+        exact, count, flagged = ret[r]
+        assert flagged == (count > 2), dict(ret)
+        assert flagged or exact, dict(ret)
+    assert any(ret[r][2] for r in range(world)), dict(ret)
 
 
 def merge_records(gathered, targets, k):

@@ -25,6 +25,7 @@ import opendht_amd  # noqa: E402
 class A:
     seed = 2024
     k = 8
+    no_cpu = False
 
 
 def main():

@@ -40,6 +40,9 @@ except (OSError, ValueError):
     doc = {}
 doc["note"] = ("per-launch HBM-side bytes: 2 x FETCH_SIZE (gfx950 wide-read correction) + WRITE_SIZE, averaged over "
                "the launches of each kernel; separate rocprofv3 --pmc passes on tools/batch_probe.py")
-doc.setdefault("workloads", {})[sys.argv[4]] = res
+key = sys.argv[4]
+if key.startswith("@"):   # the probe wrote the key (its shape is known only after its setup)
+    key = open(key[1:]).read().strip()
+doc.setdefault("workloads", {})[key] = res
 json.dump(doc, open(sys.argv[3], "w"), indent=1)
-print(sys.argv[4], json.dumps(res, indent=1))
+print(key, json.dumps(res, indent=1))
