@@ -115,6 +115,7 @@ struct dhtgpu_ctx {
     bool last_small = false;   // the last K6-API call took the small-batch path
     uint64_t last_n = 0;       // ... else its plan: largest sub-partition, planned targets, sub-partitions
     uint32_t last_qp = 0, last_nsub = 1;
+    bool last_cells = false;
     // Prefix sub-partitions of a large id set (built on the first K6 call K6 cannot plan in
     // one piece, e.g. the 2^27-id cfg-3 shard): the ids whose next sub_bits bits (after the
     // shard's own prefix) equal i, compacted in order, with their shifted word-0 plane; one K6
@@ -124,6 +125,7 @@ struct dhtgpu_ctx {
         uint64_t n = 0, stride = 0;
     };
     std::vector<SubPart> subs;
+    DevBuf cells;            // [subs][1 << cell_level()] u8 id counts per level-cell_level() prefix (F1's sibling rule)
     uint32_t sub_bits = 0;
     bool subs_valid = false;
     // dhtgpu_set_sub_handles: sub-partitioned calls return handles (a sub-partition's offset +
@@ -161,6 +163,7 @@ struct dhtgpu_ctx {
             for (DevBuf* b : {&sp.planes, &sp.map, &sp.gmap, &sp.w0s}) b->release();
         subs.clear();
         sub_tab.release();
+        cells.release();
         sub_bits = 0;
     }
 
@@ -670,8 +673,9 @@ static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hi
     uint64_t n_plan = bc.nsub ? 0 : bc.n;   // the plan is the largest sub-partition's
     for (uint32_t i = 0; i < bc.nsub; ++i) n_plan = std::max<uint64_t>(n_plan, bc.subs[i].n);
     const uint32_t nsub = bc.nsub ? bc.nsub : 1u;
-    const size_t need = batch_bytes(n_plan, bc.q, bc.q_plan, bc.k, c->num_cus, nsub);
-    const size_t head = batch_clean_bytes(n_plan, bc.q_plan, bc.k, c->num_cus, nsub);
+    const bool cells = bc.cells != nullptr;
+    const size_t need = batch_bytes(n_plan, bc.q, bc.q_plan, bc.k, c->num_cus, nsub, cells);
+    const size_t head = batch_clean_bytes(n_plan, bc.q_plan, bc.k, c->num_cus, nsub, cells);
     if (need > b.ws.cap) {   // reallocated: nothing of it is known
         b.zeroed = 0;
         b.desc_sig = 0;
@@ -696,6 +700,7 @@ static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hi
     c->last_n = n_plan;
     c->last_qp = bc.q_plan;
     c->last_nsub = nsub;
+    c->last_cells = cells;
     return DHTGPU_OK;
 }
 
@@ -738,6 +743,19 @@ static int build_subs(dhtgpu_ctx* c) {
             DHT_TRY(launch_map_idx(sp.gmap.as<uint32_t>(), m, c->gidx.as<uint32_t>(), 0, s));
         }
     }
+    // level-cell_level() id counts of every sub-partition (sibling marking, BatchCall::cells)
+    const size_t ncell = (size_t)1 << cell_level();
+    DHT_TRY(c->cells.ensure(c->subs.size() * ncell));
+    {
+        DevBuf cnt;   // (DevBuf frees nothing by itself: released on every path)
+        hipError_t e = cnt.ensure(ncell * 4);
+        for (size_t i = 0; e == hipSuccess && i < c->subs.size(); ++i)
+            e = launch_cell_counts(c->subs[i].w0s.as<uint32_t>(), c->subs[i].n, cnt.as<uint32_t>(),
+                                   c->cells.as<uint8_t>() + i * ncell, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        cnt.release();
+        DHT_TRY(e);
+    }
     std::vector<HandleSub> tab(c->subs.size());
     uint64_t off = 0;
     for (size_t i = 0; i < tab.size(); ++i) {
@@ -769,7 +787,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     uint64_t n_max = 0;
     for (const auto& sp : c->subs) n_max = std::max<uint64_t>(n_max, sp.n);
     const bool handles = c->sub_handles && !out_rec;
-    if (!batch_supported(n_max, q_plan, k, c->num_cus, S)) {
+    if (!batch_supported(n_max, q_plan, k, c->num_cus, S, true)) {
         if (!handles) return dhtgpu_topk_dev(c, tp, ts, q, k, out_idx, out_cnt, out_rec, idx_base, s);
         // handles on the K1 route: context-local indices, then their handles
         const bool mg = c->map_global;
@@ -812,6 +830,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     bc.q_plan = q_plan;
     bc.k = k;
     bc.skip = P;
+    bc.cells = c->cells.as<uint8_t>();
     bc.gidx = global ? c->gidx.as<uint32_t>() : nullptr;
     bc.base = 0;
     bc.out_idx = li;
@@ -986,7 +1005,7 @@ int dhtgpu_batch_topk_timed(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint
         for (int i = 0; i < 4; ++i) stats4[i] = 0;
     } else if (stats4) {
         DHT_TRY(batch_read_stats(c->bslot[c->blast].ws.p, c->last_n, q, c->last_qp, k, c->num_cus, stats4, s,
-                                 c->last_nsub));
+                                 c->last_nsub, c->last_cells));
     }
     return DHTGPU_OK;
 }

@@ -188,6 +188,7 @@ struct F1Args {
     uint32_t* bitmap;
     uint32_t* tcount; uint2* tbuf; uint32_t tcap;
     uint32_t* ctr; uint32_t* tspill;
+    const uint8_t* cells; uint32_t k;   // nullable: per sub-partition level-Lm cell counts (sibling marking)
 };
 
 __global__ __launch_bounds__(kF1Threads) void k_f1_targets(F1Args a) {
@@ -198,7 +199,10 @@ __global__ __launch_bounds__(kF1Threads) void k_f1_targets(F1Args a) {
     const uint32_t sub = a.sub_bits ? (w << a.sub_shift) >> (32 - a.sub_bits) : 0u;
     const uint32_t v = a.shift ? (w << a.shift) | (a.tw1[i] >> (32 - a.shift)) : w;
     const uint32_t pre = top_bits(v, a.Lm);
-    atomicOr(a.bitmap + sub * a.nwords + (pre >> 5), 1u << (pre & 31));
+    // sibling marking (plans with cells): a level-Lm cell holding < k ids marks its sibling too, so
+    // the target's level-(Lm - 1) subtree is complete among the survivors
+    const bool sib = a.cells && a.cells[((uint64_t)sub << a.Lm) + pre] < a.k;
+    atomicOr(a.bitmap + sub * a.nwords + (pre >> 5), (1u << (pre & 31)) | (sib ? 1u << ((pre ^ 1u) & 31) : 0u));
     const uint32_t p = sub * a.np + top_bits(v, a.b1);
     const uint32_t slot = atomicAdd(a.tcount + p * kCtrStride, 1u);
     if (slot < a.tcap) {
@@ -650,7 +654,24 @@ struct F3Args {
     unsigned long long* stamps;          // dbg & 256: per-block phase timestamps [np][16]
     uint32_t cap;                        // LDS stage entries (the plan's, <= kF3Cap)
     RecOut rec;                          // record form: F3's fast path writes compact records itself
+    uint32_t Lmin;                       // coarsest complete level: Lm, or Lm - 1 with sibling marking (F1)
 };
+
+// [lo, hi) of the deepest level L in [Lmin, Lq] whose subtree sub(t, L) holds >= want survivors
+// (survivors sorted by their prefix bits [b1, Lq); sq = t's bits [b1, Lq)).  Every level in
+// [Lmin, Lq] that the loop can stop at is complete among the survivors: a target's level-Lm subtree
+// is marked whole, and with sibling marking its level-(Lm - 1) subtree too whenever the level-Lm one
+// holds fewer than k ids -- the loop only reaches Lm - 1 for such a target.
+__device__ __forceinline__ void level_range(const uint32_t* sofs, uint32_t sq, uint32_t Lq, uint32_t Lmin, uint32_t want,
+                                            uint32_t& lo, uint32_t& hi) {
+    uint32_t L = Lq + 1;
+    do {
+        --L;
+        const uint32_t sh_l = Lq - L;
+        lo = sofs[(sq >> sh_l) << sh_l];
+        hi = sofs[((sq >> sh_l) + 1) << sh_l];
+    } while (hi - lo < want && L > Lmin);
+}
 
 // (w0 distance, w1 distance, index) order; words 2..4 are read only when both distances tie
 __device__ __forceinline__ bool key2_less(uint32_t da, uint32_t a1, uint32_t ia, uint32_t db, uint32_t b1, uint32_t ib,
@@ -938,7 +959,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         // j of a group scans candidates lo + j, lo + j + G, ... into its own top-K and the
         // group merges its lists with DPP butterflies (f3_merge).  G = 1 deals the targets
         // round-robin over the waves so that every SIMD runs a share of the candidate loops.
-        const uint32_t G = a.Lm >= 12 ? (mtr <= kF3Threads / 4 ? 4u : mtr <= kF3Threads / 2 ? 2u : 1u) : 1u;
+        const uint32_t G = a.Lmin >= 12 ? (mtr <= kF3Threads / 4 ? 4u : mtr <= kF3Threads / 2 ? 2u : 1u) : 1u;
         const uint32_t slot = G == 4 ? threadIdx.x >> 2 : G == 2 ? threadIdx.x >> 1 : lane * NWV + wv;
         const uint32_t gj = threadIdx.x & (G - 1);
         // one set (no sub-partitions): a group leader's tied target, answered inline by its wave
@@ -947,15 +968,9 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
         if (slot < mtr) {   // group-uniform from here on
             const uint2 te = T[slot];
             const uint32_t t0 = te.x, qi = te.y;
-            // deepest level L in [Lm, Lq] with >= want ids in sub(t, L)
-            const uint32_t sq = top_bits(t0, a.Lq) & smask;
-            uint32_t lo = 0, hi = 0, L = a.Lq + 1;
-            do {
-                --L;
-                const uint32_t sh_l = a.Lq - L;
-                lo = sofs[(sq >> sh_l) << sh_l];
-                hi = sofs[((sq >> sh_l) + 1) << sh_l];
-            } while (hi - lo < want && L > a.Lm);
+            // deepest level L in [Lmin, Lq] with >= want ids in sub(t, L)
+            uint32_t lo = 0, hi = 0;
+            level_range(sofs, top_bits(t0, a.Lq) & smask, a.Lq, a.Lmin, want, lo, hi);
             const uint32_t mm = hi - lo;
             if (t0i == 0) F3_STAMP(8);
             if (mm < want) {
@@ -972,9 +987,9 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
             } else {
                 uint32_t dk[K], ok[K];
                 uint32_t rmin = DHT_NONE;   // smallest distance that left (or never entered) the list
-                if (a.Lm >= 12) {
+                if (a.Lmin >= 12) {
                     // packed keys (w0 distance << 12 | LDS position): distances are below
-                    // 2^(32 - Lm) <= 2^20 and positions below kF3Cap = 2^12, so the key order
+                    // 2^(32 - Lmin) <= 2^20 and positions below kF3Cap = 2^12, so the key order
                     // is the (distance, position) order; one v_med3 per slot inserts
                     uint32_t key[K];
 #pragma unroll
@@ -1066,22 +1081,24 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                     // the stores instead of one per place
                     uint32_t res[K];
                     if (a.rec.out) {   // record form (block-uniform): the target's records here
-                        uint32_t w0[K];
+                        uint32_t w0[K], w1[K], gi[K];
 #pragma unroll
                         for (int r = 0; r < K; ++r) {
                             const uint2 e = S[(uint32_t)r < want && ok[r] < a.cap ? ok[r] : 0u];
                             res[r] = e.y;
                             w0[r] = e.x;
                         }
-#pragma unroll
-                        for (int r = 0; r < K; ++r) res[r] = map_out(res[r], a.gidx, a.base);   // context-local
-                        uint32_t w1[K], gi[K];
+                        // words 0 / 1 from the planes the stage indexes (a sub-partition's own: its
+                        // local index) together with the index map: one round trip, not two
+                        // dependent ones (the map first, then the context's planes)
 #pragma unroll
                         for (int r = 0; r < K; ++r) {
-                            if (!a.rec.w0_direct) w0[r] = a.rec.planes[res[r]];
-                            w1[r] = a.rec.planes[a.rec.stride + res[r]];
-                            gi[r] = a.rec.gidx ? a.rec.gidx[res[r]] : res[r] + a.rec.base;
+                            if (!a.rec.w0_direct) w0[r] = a.planes[res[r]];
+                            w1[r] = a.planes[a.stride + res[r]];
+                            res[r] = map_out(res[r], a.gidx, a.base);   // context-local
                         }
+#pragma unroll
+                        for (int r = 0; r < K; ++r) gi[r] = a.rec.gidx ? a.rec.gidx[res[r]] : res[r] + a.rec.base;
                         uint32_t* ro = a.rec.out + (uint64_t)qi * a.k * 3;
                         if (full_row && ((uintptr_t)a.rec.out & 15) == 0) {
                             // k == K == want: the row is 3K words from a 16-B boundary (K % 4 == 0),
@@ -1189,15 +1206,16 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                 (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 8 & 0xFFu) | (__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xFu) << 8;
             a.stamps[(uint64_t)blockIdx.x * 16 + 14] = ntie[0];
         }
-        // B: one wave per target for ties and large subtrees (the level-Lm subtree range)
+        // B: one wave per target for ties and large subtrees (phase A's range: complete, >= want ids)
         const uint32_t ns = slow[kF3Threads];
         for (uint32_t i = wv; i < ns; i += NWV) {
             const uint2 te = T[slow[i]];
             const uint32_t t0 = __builtin_amdgcn_readfirstlane(te.x);
             const uint32_t qi = __builtin_amdgcn_readfirstlane(te.y);
-            const uint32_t sh_m = a.Lq - a.Lm;
-            const uint32_t sm = (top_bits(t0, a.Lq) & smask) >> sh_m;
-            f3_wave_answer(a, S, sofs[sm << sh_m], sofs[(sm + 1) << sh_m], qi, t0, want, lane);
+            uint32_t lo = 0, hi = 0;
+            level_range(sofs, top_bits(t0, a.Lq) & smask, a.Lq, a.Lmin, want, lo, hi);
+            f3_wave_answer(a, S, __builtin_amdgcn_readfirstlane(lo), __builtin_amdgcn_readfirstlane(hi), qi, t0, want,
+                           lane);
         }
         if (ns || t0i + kF3Threads < mt) sync_lds();   // T / slow are reused by the next chunk
         if (t0i == 0) F3_STAMP(6);
@@ -1475,10 +1493,12 @@ __global__ __launch_bounds__(kF4Threads) void k_f4(F3Args a, FbArgs f) {
 
 struct BatchPlan {
     uint32_t Lm, b1, Lq, nwords, nblk1, nblk2, stage, sparse, tcap;
+    uint32_t sib;    // 1: sibling marking from the set's level-Lm cell counts (Lmin = Lm - 1)
     uint32_t nstage; // F2's narrow stage entries (6 B each; 0: none) -- F2 then leaves room for an F3 workgroup
     uint32_t f3cap;  // F3's LDS stage entries (kF3Cap, or the 6-sigma bound when that buys a 4th workgroup per CU)
     uint32_t scap;   // survivors per (bucket set, partition)
     uint32_t f3cap_wide;   // F3's LDS stage entries when F2 runs its 8-B stage (no narrow stage)
+    uint32_t cap6;         // the plan's 6-sigma partition bound (F3 stage entries, <= kF3Cap)
     bool fits;   // partitions' survivors fit the F3 stage on uniform ids
     uint64_t per_blk;
 };
@@ -1501,22 +1521,22 @@ double poisson_below(double m, uint32_t k) {
     return sum;
 }
 
-BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus);
+BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bool cells);
 
-// plan_batch is a pure function of (n, q, k, CUs), asked three times per call (workspace size,
-// clean head, the launch): the last few plans are kept per host thread
-BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
-    struct Entry { uint64_t n; uint32_t q, k; int cus; BatchPlan P; bool used; };
+// plan_batch is a pure function of (n, q, k, CUs, cells), asked three times per call (workspace
+// size, clean head, the launch): the last few plans are kept per host thread
+BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus, bool cells = false) {
+    struct Entry { uint64_t n; uint32_t q, k; int cus; bool cells; BatchPlan P; bool used; };
     thread_local Entry cache[4] = {};
     thread_local uint32_t next = 0;
     for (const Entry& e : cache)
-        if (e.used && e.n == n && e.q == q && e.k == k && e.cus == num_cus) return e.P;
+        if (e.used && e.n == n && e.q == q && e.k == k && e.cus == num_cus && e.cells == cells) return e.P;
     Entry& e = cache[next++ & 3u];
-    e = Entry{n, q, k, num_cus, plan_batch_compute(n, q, k, num_cus), true};
+    e = Entry{n, q, k, num_cus, cells, plan_batch_compute(n, q, k, num_cus, cells), true};
     return e.P;
 }
 
-BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
+BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bool cells) {
     BatchPlan P;
     // mark level: 4k or more ids per level-Lm subtree -- or one level finer (2k..4k) when, on
     // uniform ids, fewer than 0.01 of the q targets are expected to land in a subtree with
@@ -1525,13 +1545,28 @@ BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     // double the survivors.
     const uint64_t per = 4ull * k;
     P.Lm = n >= per ? floor_log2(n / per) : 0;
-    if (n >= per && P.Lm < kMaxLm && poisson_below((double)n / (double)(1ull << (P.Lm + 1)), k) * q <= 0.01) ++P.Lm;
+    P.sib = 0;
+    if (n >= per && P.Lm < kMaxLm) {
+        if (poisson_below((double)n / (double)(1ull << (P.Lm + 1)), k) * q <= 0.01) {
+            ++P.Lm;
+        } else if (cells && P.Lm + 1 == kMaxLm && poisson_below((double)n / (double)(1ull << P.Lm), k) * q <= 0.01) {
+            // sibling marking (the set's level-kMaxLm cell counts, kept with its sub-partitions):
+            // a target whose level-Lm cell holds < k ids marks the sibling cell too, so it answers
+            // from its complete level-(Lm - 1) subtree; only a short PAIR falls back.  One level
+            // finer than the rule above allows: the survivors drop from 1 - exp(-q / 2^(Lm-1)) to
+            // about 1 - exp(-q / 2^Lm) (cfg 3's broadcast rank: 39 % -> 22 %)
+            ++P.Lm;
+            P.sib = 1;
+        }
+    }
     if (P.Lm > kMaxLm) P.Lm = kMaxLm;
-    // survivors on uniform ids: n (1 - exp(-q / 2^Lm)); partitions of about kF3Cap / 2
-    const double f = 1.0 - std::exp(-(double)q / (double)(1ull << P.Lm));
+    // survivors on uniform ids: n (1 - exp(-q (1 + p) / 2^Lm)), p = the fraction of targets that
+    // mark a sibling too; partitions of about kF3Cap / 2
+    const double psib = P.sib ? poisson_below((double)n / (double)(1ull << P.Lm), k) : 0.0;
+    const double f = 1.0 - std::exp(-(double)q * (1.0 + psib) / (double)(1ull << P.Lm));
     const double surv = (double)n * f + 1.0;
     uint32_t b1 = 0;
-    while (b1 < P.Lm && surv / (double)(1ull << b1) > kF3Cap / 2) ++b1;
+    while (b1 + P.sib < P.Lm && surv / (double)(1ull << b1) > kF3Cap / 2) ++b1;   // F3 sorts level Lm - sib
     if (P.Lm > kMaxSubBits && b1 < P.Lm - kMaxSubBits) b1 = P.Lm - kMaxSubBits;
     if (b1 > 13) b1 = 13;   // kMaxParts
     // a partition's survivors come in whole level-Lm subtrees (n / 2^Lm ids each, marked
@@ -1546,7 +1581,7 @@ BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
         const double mean = sub * f * mu, var = sub * f * (1.0 - f) * mu * mu + sub * f * mu;
         need = mean + 6.0 * std::sqrt(var) + 64.0;
         if (need <= (double)kF3Cap) { P.fits = true; break; }
-        if (b1 >= 13 || b1 >= P.Lm) break;
+        if (b1 >= 13 || b1 + P.sib >= P.Lm) break;
     }
     P.b1 = b1;
     {   // a set holds each id with probability 1 / kSets (ids are spread over the blocks by
@@ -1572,6 +1607,7 @@ BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus) {
     };
     constexpr size_t kF3Lds4 = kLdsMax / 4;
     const uint32_t cap6 = std::min<uint32_t>(kF3Cap, ((uint32_t)need + 63u) & ~63u);
+    P.cap6 = cap6;
     if (P.fits && lds3(P.Lq, P.f3cap) > kF3Lds4) {
         for (uint32_t lq = P.Lq; lq >= P.Lm && lq > P.b1; --lq) {
             if (lds3(lq, kF3Cap) <= kF3Lds4) { P.Lq = lq; break; }
@@ -1874,9 +1910,9 @@ uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, 
 
 }  // namespace
 
-bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t nsub) {
+bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t nsub, bool cells) {
     if (k == 0 || k > DHTGPU_MAX_K_DEV || n >= (1ull << 31) || nsub == 0 || nsub > kMaxSubs) return false;
-    const BatchPlan P = plan_batch(n, q, k, num_cus);
+    const BatchPlan P = plan_batch(n, q, k, num_cus, cells);
     if ((uint64_t)q * nsub > kMaxQ) return false;
     if (((uint64_t)nsub << P.b1) > kMaxParts) return false;
     // dense mode flushes whenever less than one sub-step of room is left
@@ -1884,17 +1920,17 @@ bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t n
     return f3_lds(P, P.f3cap_wide) <= kLdsMax && f2_lds(P) <= kLdsMax;
 }
 
-size_t batch_clean_bytes(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub) {
-    return ws_layout(plan_batch(n, q_plan, k, num_cus), nsub, 0, k).clean;
+size_t batch_clean_bytes(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub, bool cells) {
+    return ws_layout(plan_batch(n, q_plan, k, num_cus, cells), nsub, 0, k).clean;
 }
 
-size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub) {
-    return ws_layout(plan_batch(n, q_plan, k, num_cus), nsub, q, k).total;
+size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub, bool cells) {
+    return ws_layout(plan_batch(n, q_plan, k, num_cus, cells), nsub, q, k).total;
 }
 
 hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus,
-                            uint32_t* stats4, hipStream_t s, uint32_t nsub) {
-    const BatchPlan P = plan_batch(n, q_plan, k, num_cus);
+                            uint32_t* stats4, hipStream_t s, uint32_t nsub, bool cells) {
+    const BatchPlan P = plan_batch(n, q_plan, k, num_cus, cells);
     const WsLayout Ly = ws_layout(P, nsub, q, k);
     const size_t NP = (size_t)nsub << P.b1;
     const uint8_t* w = static_cast<const uint8_t*>(ws);
@@ -1912,6 +1948,28 @@ __global__ void k_shift_w0(const uint32_t* __restrict__ planes, uint64_t stride,
                            uint32_t* __restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < stride) out[i] = (planes[i] << shift) | (planes[stride + i] >> (32 - shift));
+}
+
+// Level-kMaxLm cell counts of a sub-partition (its shifted word-0 plane): u32 counters, then
+// saturated to u8 (F1's sibling rule only compares them with k <= DHTGPU_MAX_K_DEV < 255).
+// Persistent with the sub-partitions (2^kMaxLm B each), rebuilt when the set changes.
+__global__ void k_cell_count(const uint32_t* __restrict__ w0s, uint64_t n, uint32_t* __restrict__ cnt) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        atomicAdd(cnt + (w0s[i] >> (32 - kMaxLm)), 1u);
+}
+__global__ void k_cell_pack(const uint32_t* __restrict__ cnt, uint8_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < (1u << kMaxLm)) out[i] = (uint8_t)(cnt[i] < 255u ? cnt[i] : 255u);
+}
+
+uint32_t cell_level() { return kMaxLm; }
+
+hipError_t launch_cell_counts(const uint32_t* w0s, uint64_t n, uint32_t* scratch, uint8_t* out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(scratch, 0, ((size_t)1 << kMaxLm) * 4, s);
+    if (e != hipSuccess) return e;
+    if (n) k_cell_count<<<dim3(2048), dim3(256), 0, s>>>(w0s, n, scratch);
+    k_cell_pack<<<dim3((1u << kMaxLm) / 256), dim3(256), 0, s>>>(scratch, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_shift_w0(const uint32_t* planes, uint64_t stride, uint32_t shift, uint32_t* out, hipStream_t s) {
@@ -2014,7 +2072,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
         n_all += subs[i].n;
     }
     const bool nt = 4 * n_all > kNtBytes;   // F2's ring: non-temporal past the Infinity Cache
-    const BatchPlan P = plan_batch(n_max, c.q_plan, k, c.num_cus);
+    const BatchPlan P = plan_batch(n_max, c.q_plan, k, c.num_cus, c.cells != nullptr);
     const uint32_t np = 1u << P.b1, NP = nsub * np;
     uint32_t dbg = c.dbg & 256u;   // the only diagnostics bit: phase stamps (results unchanged)
     hipEvent_t* ev = c.ev;
@@ -2094,7 +2152,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
     unsigned long long* stamps = (dbg & 256u) ? c.stamps : nullptr;   // F3 [8192][16] then F2 [8192][16]
     if (dbg & 256) (void)hipMemsetAsync(stamps, 0, (size_t)3 * 8192 * 16 * 8, s);
     const F1Args a1{c.tp, c.tp + c.ts, q, P.Lm, P.b1, c.skip, c.sub_shift, c.nsub ? c.sub_bits : 0u, np, P.nwords,
-                    bitmap, tcount, tbuf, P.tcap, ctr, tspill};
+                    bitmap, tcount, tbuf, P.tcap, ctr, tspill, P.sib ? c.cells : nullptr, k};
     go(0, k_f1_targets, dim3((q + kF1Threads - 1) / kF1Threads), dim3(kF1Threads), 0, a1);
     if (nblk2) {
         F2Args a2{d_desc, d_blk, hd[0], nsub, NP, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, P.scap, ctr,
@@ -2119,11 +2177,19 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
     // the base arguments are the whole set's: F4's scan (fallback targets) runs over all its ids
     F3Args a{pbuf, pcount, P.scap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, c.planes, c.stride,
              c.n, c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, fb_sub, pstat, tie_hdr, tie_cand, tie_cnt,
-             d_desc, np, dbg, stamps, narrow ? P.f3cap : P.f3cap_wide, RecOut{}};
+             d_desc, np, dbg, stamps, narrow ? P.f3cap : P.f3cap_wide, RecOut{}, P.Lm - P.sib};
     if (c.out_rec)
         a.rec = RecOut{c.out_rec, c.planes, c.stride, c.rec_gidx, c.rec_base, (nsub == 1 && !c.w0s && !c.skip) ? 1u : 0u};
 
-    // F3 stages the plan's 6-sigma bound only beside F2's narrow stage (which it makes room for)
+    // F3 stages the plan's 6-sigma bound beside F2's narrow stage (which it makes room for), and on
+    // sub-partitioned calls whose partitions run in several rounds of workgroups when that lets 5 or
+    // 6 of them share a CU instead of 4 (F3<8> holds 78 VGPRs: 6 waves per SIMD); F3 is a chain of
+    // round trips per workgroup, so a round of more workgroups shortens the launch (a partition past
+    // the bound sends its targets to the exact fallback, as one past kF3Cap does)
+    if (!narrow && nsub > 1 && k <= 8 && P.fits && P.cap6 < a.cap && NP >= 8u * (uint32_t)std::max(c.num_cus, 1)) {
+        auto per_cu = [](size_t l) { return std::min<size_t>(6, kLdsMax / ((l + 1023) & ~(size_t)1023)); };
+        if (per_cu(f3_lds(P, P.cap6)) > per_cu(f3_lds(P, a.cap))) a.cap = P.cap6;
+    }
     size_t l3 = f3_lds(P, a.cap);
     const dim3 g3(NP), b3(kF3Threads);
     const bool ex = c.n >= k && (k == 8 || k == 16 || k == 32);

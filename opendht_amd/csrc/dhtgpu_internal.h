@@ -119,14 +119,20 @@ hipError_t launch_index_query(const void* ws, uint64_t n, uint32_t B, const uint
 // batch.hip: K6 per-batch target-prefix filter + exact top-k (no persistent index).
 // n: ids of the largest sub-partition (or of the set); q_plan: the targets one sub-partition
 // is planned for (q / nsub); nsub: sub-partitions served by the call (1: the set itself).
-bool batch_supported(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1);
-size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1);
+bool batch_supported(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1, bool cells = false);
+size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1, bool cells = false);
 // leading workspace bytes that must be zero before a call (the call leaves them zero)
-size_t batch_clean_bytes(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1);
+size_t batch_clean_bytes(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1, bool cells = false);
 // stats4 = {fallback targets, survivors, wave-path targets, 0} of the last call on workspace ws
 // (synchronises s)
 hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus,
-                            uint32_t* stats4, hipStream_t s, uint32_t nsub = 1);
+                            uint32_t* stats4, hipStream_t s, uint32_t nsub = 1, bool cells = false);
+// cells: the sub-partitions' level-cell_level() id counts (launch_cell_counts) are available, which
+// lets the plan mark one level finer with sibling marking (BatchCall::cells)
+uint32_t cell_level();
+// u8 counts (saturated) of the n ids of a shifted word-0 plane per top-cell_level()-bit prefix;
+// scratch: 4 << cell_level() bytes
+hipError_t launch_cell_counts(const uint32_t* w0s, uint64_t n, uint32_t* scratch, uint8_t* out, hipStream_t s);
 // prefix shards: out[i] = planes word 0 << shift | word 1 >> (32 - shift), i < stride
 hipError_t launch_shift_w0(const uint32_t* planes, uint64_t stride, uint32_t shift, uint32_t* out, hipStream_t s);
 // One prefix sub-partition of a K6 call's id set (host view; see batch.hip SubDesc).
@@ -165,6 +171,7 @@ struct BatchCall {
     uint32_t sub_shift, sub_bits;          // a target's sub-partition: its bits [sub_shift, +sub_bits)
     uint64_t* desc_sig;                    // the workspace's uploaded sub-partition descriptors (signature)
     uint32_t skip; const uint32_t* w0s;    // w0s = 32 id bits from bit `skip` (every id shares its top skip bits)
+    const uint8_t* cells;                  // nullable: [nsub][1 << cell_level()] cell counts of the sub-partitions
     const uint32_t* gidx; uint32_t base;   // result index map (nullable) or offset
     uint32_t* out_idx; uint32_t* out_cnt;  // rows of the ORIGINAL target indices
     // record form (nullable): every writer of a result row (F3, the wave paths, F4's scan and

@@ -204,6 +204,43 @@ def test_subpartition_deficient_subtree_targets(ctx):
     assert np.array_equal(got[picks], want) and np.array_equal(cnt[picks], wcnt)
 
 
+def test_subpartition_sibling_marking(ctx):
+    """Sibling marking (round 6): 31.25 M ids = 2 prefix sub-partitions of ~1.56e7 with 65,536
+    targets plan one level finer than the 4k rule (level-19 cells of ~30 ids) because the
+    sub-partitions carry their level-19 cell counts: a target whose own cell holds < k ids marks the
+    sibling cell too and answers from the complete pair.  Crafted: 48 targets' cells emptied down
+    to 3 ids (moved into the sibling: the pair keeps them all), 16 targets' whole pairs emptied
+    down to 2 + 2 ids (the pair is short: F3's fallback scan of the sub-partition).  Whole batch
+    == K1 scan; the crafted targets and a sample == std::partial_sort(xorCmp)."""
+    n, q, k = 31_250_000, 65536, 8
+    ids = O.gen_ids(3434, n)
+    tg = O.gen_ids(3435, q)
+    key = lambda a: ((a[:, 0].astype(np.uint32) << 12) | (a[:, 1].astype(np.uint32) << 4) | (a[:, 2] >> 4))
+    ik, tk = key(ids), key(tg)
+    rng = np.random.default_rng(3436)
+    picks = rng.choice(q, 64, replace=False)
+    for j, t in enumerate(picks):
+        cell = tk[t]
+        if j < 48:   # the cell keeps 3 ids, the rest move to the sibling cell (bit 19)
+            inside = np.nonzero(ik == cell)[0][3:]
+            ids[inside, 2] ^= 0x10
+        else:        # cell and sibling keep 2 ids each, the rest move to the other pair (bit 18)
+            for c_ in (cell, cell ^ 1):
+                inside = np.nonzero(ik == c_)[0][2:]
+                ids[inside, 2] ^= 0x20
+        ik = key(ids)
+    assert len(np.unique(ids, axis=0)) == n
+    ctx.set_ids(ids)
+    got, cnt = ctx.batch_topk(tg, k)
+    sc, scnt = ctx.topk(tg, k)
+    assert np.array_equal(cnt, scnt)
+    bad = np.nonzero((got != sc).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} targets differ from the K1 scan, first {bad[:5]}"
+    rows = np.r_[picks, sample_rows(q, 16)]
+    want, wcnt = O.topk(ids, tg[rows], k, threads=16)
+    assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
+
+
 @pytest.mark.parametrize("k", [8, 32])
 def test_clustered_ids_fallback_scan(ctx, k):
     """Verdict item 4: 2^24 ids of which 25 % share one 24-bit prefix, and targets inside the
