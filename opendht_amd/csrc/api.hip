@@ -126,6 +126,7 @@ struct dhtgpu_ctx {
     };
     std::vector<SubPart> subs;
     DevBuf cells;            // [subs][1 << cell_level()] u8 id counts per level-cell_level() prefix (F1's sibling rule)
+    DevBuf hinv;             // [n] context-local index -> sub-partition handle
     uint32_t sub_bits = 0;
     bool subs_valid = false;
     // dhtgpu_set_sub_handles: sub-partitioned calls return handles (a sub-partition's offset +
@@ -164,6 +165,7 @@ struct dhtgpu_ctx {
         subs.clear();
         sub_tab.release();
         cells.release();
+        hinv.release();
         sub_bits = 0;
     }
 
@@ -705,8 +707,13 @@ static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hi
 }
 
 // Build the prefix sub-partitions: the smallest split into 2^s parts of <= 2^24 expected ids
-// (s <= 8), each compacted in id order (so index ties break the same way) from the context's
-// planes, with its shifted word-0 plane and its index maps.
+// (s <= 8), each compacted from the context's planes and then sorted by its ids (stable: equal
+// ids keep their index order, so index ties break the same way), with its shifted word-0 plane,
+// its index maps, its level-19 cell counts and the context's inverse handle map.  Prefix order
+// is the layout K6 wants: an F2 workgroup's contiguous range of a sub-partition covers a narrow
+// prefix range, so its survivors fall into a few partitions (long, coalesced bucket runs instead
+// of a few entries in every partition) and a partition's survivors, results and result-map
+// entries sit in a narrow index window (F3's gathers and record words hit lines they share).
 static int build_subs(dhtgpu_ctx* c) {
     if (c->subs_valid) return DHTGPU_OK;
     c->invalidate_subs();
@@ -736,6 +743,26 @@ static int build_subs(dhtgpu_ctx* c) {
             DHT_TRY(launch_fill(sp.planes.as<uint32_t>() + (uint64_t)w * sp.stride + m, sp.stride - m, 0u, s));
         DHT_TRY(launch_select_prefix(planes, c->stride, c->n, P, pv, scratch, d_total, sp.planes.as<uint32_t>(),
                                      sp.stride, sp.map.as<uint32_t>(), 0, s));
+        if (m > 1) {   // prefix order (stable sort of the compacted ids; perm -> context-local map)
+            DevBuf sorted, perm, sscr;
+            int unique = 1;
+            hipError_t e = sorted.ensure((size_t)sp.stride * 5 * 4);
+            if (e == hipSuccess) e = perm.ensure((size_t)m * 4);
+            if (e == hipSuccess) e = sscr.ensure(sort_scratch_bytes(m));
+            for (int w = 0; e == hipSuccess && w < 5; ++w)
+                e = launch_fill(sorted.as<uint32_t>() + (uint64_t)w * sp.stride + m, sp.stride - m, 0u, s);
+            if (e == hipSuccess)
+                e = launch_sort_ids(sp.planes.as<uint32_t>(), sp.stride, m, sorted.as<uint32_t>(), sp.stride,
+                                    perm.as<uint32_t>(), sscr.p, &unique, s);
+            if (e == hipSuccess) e = launch_map_idx(perm.as<uint32_t>(), m, sp.map.as<uint32_t>(), 0, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(sp.map.p, perm.p, (size_t)m * 4, hipMemcpyDeviceToDevice, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e == hipSuccess) std::swap(sp.planes, sorted);
+            sorted.release();
+            perm.release();
+            sscr.release();
+            DHT_TRY(e);
+        }
         DHT_TRY(launch_shift_w0(sp.planes.as<uint32_t>(), sp.stride, P, sp.w0s.as<uint32_t>(), s));
         if (c->has_gidx) {   // sub -> global stream index, composed once
             DHT_TRY(sp.gmap.ensure((size_t)sp.stride * 4));
@@ -755,6 +782,14 @@ static int build_subs(dhtgpu_ctx* c) {
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         cnt.release();
         DHT_TRY(e);
+    }
+    DHT_TRY(c->hinv.ensure((size_t)(c->n ? c->n : 1) * 4));
+    {
+        uint64_t o = 0;
+        for (const auto& sp : c->subs) {
+            DHT_TRY(launch_handle_inverse(sp.map.as<uint32_t>(), sp.n, (uint32_t)o, c->hinv.as<uint32_t>(), s));
+            o += sp.n;
+        }
     }
     std::vector<HandleSub> tab(c->subs.size());
     uint64_t off = 0;
@@ -795,8 +830,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
         r = dhtgpu_topk_dev(c, tp, ts, q, k, out_idx, out_cnt, nullptr, 0, s);
         c->map_global = mg;
         if (r) return r;
-        DHT_TRY(launch_idx_to_handles(c->sub_tab.as<HandleSub>(), c->planes.as<uint32_t>(), c->shard_pbits, sb, out_idx,
-                                      (uint64_t)q * k, s));
+        DHT_TRY(launch_idx_to_handles(c->hinv.as<uint32_t>(), out_idx, (uint64_t)q * k, s));
         return DHTGPU_OK;
     }
     const bool global = !handles && c->has_gidx && c->map_global && !out_rec;
@@ -847,6 +881,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     bc.rec_base = idx_base;
     bc.handles = handles ? 1u : 0u;
     bc.htab = c->sub_tab.as<HandleSub>();
+    bc.hinv = c->hinv.as<uint32_t>();
     if (handles) bc.base = kHandleMark;   // whole-set fallback rows, marked for the pass after F4
     r = batch_slot_run(c, si, bc, s, ev);
     if (r) return r;

@@ -1999,19 +1999,16 @@ __global__ void k_handles_to_idx(const HandleSub* __restrict__ tab, uint32_t nsu
     out[i] = r;
 }
 
-__global__ void k_idx_to_handles(const HandleSub* __restrict__ tab, const uint32_t* __restrict__ planes, uint32_t hshift,
-                                 uint32_t hbits, uint32_t* __restrict__ idx, uint64_t m) {
+__global__ void k_idx_to_handles(const uint32_t* __restrict__ hinv, uint32_t* __restrict__ idx, uint64_t m) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= m) return;
     const uint32_t x = idx[i];
-    if (x == DHT_NONE) return;
-    const HandleSub t = tab[__builtin_amdgcn_ubfe(planes[x], 32u - hshift - hbits, hbits)];
-    uint64_t lo = 0, hi = t.n;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (t.map[mid] < x) lo = mid + 1; else hi = mid;
-    }
-    idx[i] = t.off + (uint32_t)lo;
+    if (x != DHT_NONE) idx[i] = hinv[x];
+}
+
+__global__ void k_handle_inverse(const uint32_t* __restrict__ map, uint64_t m, uint32_t off, uint32_t* __restrict__ hinv) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256)
+        hinv[map[j]] = off + (uint32_t)j;
 }
 
 // Sub-partition handles: the rows F4 answered from the whole set (targets whose own sub-partition
@@ -2020,21 +2017,13 @@ __global__ void k_idx_to_handles(const HandleSub* __restrict__ tab, const uint32
 // handles.  The fallback list and its count (ctr[0]) are the call's own, F1 of the next call
 // resets them.
 __global__ void k_fb_handles(uint32_t* __restrict__ out_idx, uint32_t k, const uint32_t* __restrict__ fb_list,
-                             const uint32_t* __restrict__ ctr, const HandleSub* __restrict__ tab,
-                             const uint32_t* __restrict__ planes, uint32_t hshift, uint32_t hbits) {
+                             const uint32_t* __restrict__ ctr, const uint32_t* __restrict__ hinv) {
     const uint64_t m = (uint64_t)ctr[0] * k;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
         uint32_t* p = out_idx + (uint64_t)fb_list[i / k] * k + i % k;
         const uint32_t x = *p;
         if (x == DHT_NONE || !(x & kHandleMark)) continue;
-        const uint32_t cl = x & ~kHandleMark;
-        const HandleSub t = tab[__builtin_amdgcn_ubfe(planes[cl], 32u - hshift - hbits, hbits)];
-        uint64_t lo = 0, hi = t.n;
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (t.map[mid] < cl) lo = mid + 1; else hi = mid;
-        }
-        *p = t.off + (uint32_t)lo;
+        *p = hinv[x & ~kHandleMark];
     }
 }
 
@@ -2045,10 +2034,15 @@ hipError_t launch_handles_to_idx(const HandleSub* tab, uint32_t nsub, const uint
     return hipGetLastError();
 }
 
-hipError_t launch_idx_to_handles(const HandleSub* tab, const uint32_t* planes, uint32_t hshift, uint32_t hbits,
-                                 uint32_t* idx, uint64_t m, hipStream_t s) {
+hipError_t launch_idx_to_handles(const uint32_t* hinv, uint32_t* idx, uint64_t m, hipStream_t s) {
     if (!m) return hipSuccess;
-    k_idx_to_handles<<<dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s>>>(tab, planes, hshift, hbits, idx, m);
+    k_idx_to_handles<<<dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s>>>(hinv, idx, m);
+    return hipGetLastError();
+}
+
+hipError_t launch_handle_inverse(const uint32_t* map, uint64_t m, uint32_t off, uint32_t* hinv, hipStream_t s) {
+    if (!m) return hipSuccess;
+    k_handle_inverse<<<dim3(2048), dim3(256), 0, s>>>(map, m, off, hinv);
     return hipGetLastError();
 }
 
@@ -2231,8 +2225,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
     else if (k <= 16) go(3, k_f4<16>, g4, b4, 0, a, fa);
     else go(3, k_f4<32>, g4, b4, 0, a, fa);
     if (c.handles && nsub > 1 && !c.out_rec)   // the whole-set fallback rows -> handles
-        k_fb_handles<<<dim3(64), dim3(256), 0, s>>>(c.out_idx, k, fb_list, ctr, c.htab, c.planes, c.sub_shift,
-                                                   c.sub_bits);
+        k_fb_handles<<<dim3(64), dim3(256), 0, s>>>(c.out_idx, k, fb_list, ctr, c.hinv);
     return hipGetLastError();
 }
 

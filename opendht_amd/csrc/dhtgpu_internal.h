@@ -146,19 +146,20 @@ constexpr uint32_t kHandleMark = 0x80000000u;   // sets hold < 2^31 ids (batch_s
 // DHTGPU_DBG bits the library honours (dhtgpu_ctx::dbg): 256 = phase stamps, 2^23 = K6 for
 // small batches.  Diagnostics only -- no bit changes a result (tests/test_abi.py pins the mask).
 constexpr uint32_t kDbgAllowed = 256u | (1u << 23);
-// One sub-partition in handle space: handles [off, off + n) name its ids in its compacted order.
+// One sub-partition in handle space: handles [off, off + n) name its ids in its (prefix-sorted) order.
 struct HandleSub {
     uint64_t n;
-    const uint32_t* map;    // sub-local -> context-local, ascending
+    const uint32_t* map;    // sub-local -> context-local
     const uint32_t* gmap;   // sub-local -> global stream index (nullable: no global map)
     uint32_t off, pad;
 };
 // out[i] = the index handle h[i] names: gmap (global) or map + base; DHT_NONE stays
 hipError_t launch_handles_to_idx(const HandleSub* tab, uint32_t nsub, const uint32_t* h, uint64_t m, uint32_t* out,
                                  bool global, uint32_t base, hipStream_t s);
-// idx[i] (context-local) -> its handle in place (its sub-partition from word-0 bits [hshift, +hbits))
-hipError_t launch_idx_to_handles(const HandleSub* tab, const uint32_t* planes, uint32_t hshift, uint32_t hbits,
-                                 uint32_t* idx, uint64_t m, hipStream_t s);
+// idx[i] (context-local) -> its handle in place: hinv[idx[i]] (DHT_NONE stays)
+hipError_t launch_idx_to_handles(const uint32_t* hinv, uint32_t* idx, uint64_t m, hipStream_t s);
+// hinv[map[j]] = off + j, j < m: the context-local -> handle map of one sub-partition
+hipError_t launch_handle_inverse(const uint32_t* map, uint64_t m, uint32_t off, uint32_t* hinv, hipStream_t s);
 
 struct BatchCall {
     void* ws;                              // workspace (batch_bytes), head zero (batch_clean_bytes)
@@ -183,6 +184,7 @@ struct BatchCall {
     // answers from the whole set carry context-local index | kHandleMark (gidx null, base =
     // kHandleMark) and a pass after F4 turns them into handles through htab
     uint32_t handles; const HandleSub* htab;
+    const uint32_t* hinv;                  // handles: context-local index -> handle
     int num_cus;
     uint32_t dbg;                          // DHTGPU_DBG & kDbgAllowed (0 in production)
     const volatile uint32_t* fb_hint;      // nullable: the slot's last fallback-list length (mapped host memory)
