@@ -239,7 +239,7 @@ struct F2Args {
     uint32_t Lm, b1;
     const uint32_t* bitmap; uint32_t nwords;
     uint32_t* pcount;             // [kSets][np_all] survivors per set and partition (all-zero between calls)
-    uint2* pbuf;                  // [np_all][kSets][pcap] survivors, partition- and set-major
+    uint2* pbuf;                  // [np_all][nsets][pcap] survivors, partition- and set-major
     uint32_t pcap;
     uint32_t* ctr;                // shared counters (F2 writes none; the survivor total is sum(pcount))
     uint32_t stage;               // LDS stage capacity (entries, <= kStage)
@@ -247,6 +247,7 @@ struct F2Args {
     uint32_t sparse;              // 1: no per-sub-step barrier (plan: the stage holds a segment's survivors)
     uint32_t seg;                 // sparse mode: ids per segment (the stage is flushed after each)
     unsigned long long* stamps;   // dbg & 256: per-block phase timestamps [nblk2][16]
+    uint32_t nsets;               // kSets, or 1 over prefix-sorted sub-partitions (a partition's survivors come from one or two workgroups)
 };
 #define F2_STAMP(i) \
     do { if ((a.dbg & 256) && threadIdx.x == 0) a.stamps[(uint64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -295,7 +296,7 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
     sync_lds();
     // reserve the partitions' slots (before the scan overwrites the counts)
     uint32_t res[8];
-    const uint32_t set = blockIdx.x % kSets, set_off = set * a.np_all + poff;   // this block's bucket set
+    const uint32_t set = a.nsets == 1 ? 0u : blockIdx.x % kSets, set_off = set * a.np_all + poff;   // this block's bucket set
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) {
         const uint32_t p = i * kF2Threads + threadIdx.x;
@@ -330,7 +331,7 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
         const uint2 x = stage_get<Narrow>(stage, a.stage, ibase, j);
         const uint32_t p = top_bits(x.x, a.b1);
         const uint32_t pos = hist[p] + j;
-        if (pos < a.pcap) a.pbuf[(uint64_t)((poff + p) * kSets + set) * a.pcap + pos] = x;
+        if (pos < a.pcap) a.pbuf[(uint64_t)((poff + p) * a.nsets + set) * a.pcap + pos] = x;
     }
     sync_lds();
 }
@@ -549,7 +550,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
             while (m) {
                 const uint32_t b = (uint32_t)__ffs(m) - 1;
                 m &= m - 1;
-                atomicAdd(a.pcount + (blockIdx.x % kSets) * a.np_all + poff + 32 * i + b, a.pcap + 1u);
+                atomicAdd(a.pcount + (a.nsets == 1 ? 0u : blockIdx.x % kSets) * a.np_all + poff + 32 * i + b, a.pcap + 1u);
             }
         }
     }
@@ -655,6 +656,7 @@ struct F3Args {
     uint32_t cap;                        // LDS stage entries (the plan's, <= kF3Cap)
     RecOut rec;                          // record form: F3's fast path writes compact records itself
     uint32_t Lmin;                       // coarsest complete level: Lm, or Lm - 1 with sibling marking (F1)
+    uint32_t nsets;                      // F2's bucket sets per partition (pbuf stride): kSets or 1
 };
 
 // [lo, hi) of the deepest level L in [Lmin, Lq] whose subtree sub(t, L) holds >= want survivors
@@ -866,7 +868,7 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
     const uint2* tsrc = a.tbuf + (uint64_t)p * a.tcap;
     const uint2 tfirst = tsrc[threadIdx.x < a.tcap ? threadIdx.x : 0u];
     uint2 e[kF3Per];
-    const uint2* pb = a.pbuf + (uint64_t)p * kSets * a.pcap;
+    const uint2* pb = a.pbuf + (uint64_t)p * a.nsets * a.pcap;
 #pragma unroll
     for (uint32_t u = 0; u < kF3Per; ++u) e[u] = make_uint2(0u, 0u);
     const uint32_t mt = mt0 < a.tcap ? mt0 : a.tcap;
@@ -1499,6 +1501,7 @@ struct BatchPlan {
     uint32_t scap;   // survivors per (bucket set, partition)
     uint32_t f3cap_wide;   // F3's LDS stage entries when F2 runs its 8-B stage (no narrow stage)
     uint32_t cap6;         // the plan's 6-sigma partition bound (F3 stage entries, <= kF3Cap)
+    uint32_t nsets;        // F2 bucket sets per partition: kSets, or 1 over prefix-sorted sub-partitions
     bool fits;   // partitions' survivors fit the F3 stage on uniform ids
     uint64_t per_blk;
 };
@@ -1584,9 +1587,14 @@ BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bo
         if (b1 >= 13 || b1 + P.sib >= P.Lm) break;
     }
     P.b1 = b1;
+    // prefix-sorted sub-partitions (the plans with cell counts): an F2 workgroup's range is a
+    // narrow prefix range, so a partition's survivors come from one or two workgroups -- one
+    // bucket set, sized for the whole partition (with 8 sets planned for an eighth each, every
+    // partition overflowed its set)
+    P.nsets = cells ? 1u : kSets;
     {   // a set holds each id with probability 1 / kSets (ids are spread over the blocks by
         // index, independently of their prefix): mean + 8 sigma + 64 of one set's share
-        const double sub = (double)(1ull << (P.Lm - b1)), mu = (double)n / (double)(1ull << P.Lm) / kSets;
+        const double sub = (double)(1ull << (P.Lm - b1)), mu = (double)n / (double)(1ull << P.Lm) / P.nsets;
         const double mean = sub * f * mu, var = sub * f * (1.0 - f) * mu * mu + sub * f * mu;
         const double cap = mean + 8.0 * std::sqrt(var) + 64.0;
         P.scap = cap >= (double)kF3Cap ? kF3Cap : ((uint32_t)cap + 63u) & ~63u;
@@ -1848,7 +1856,7 @@ WsLayout ws_layout(const BatchPlan& P, uint32_t nsub, uint32_t q, uint32_t k) {
     L.pstat = take(NP * 4);
     L.tbuf = take(NP * P.tcap * 8);
     L.tie_cand = take(NP * kTieSlots * 64 * 8);
-    L.pbuf = take(NP * kSets * P.scap * 8);
+    L.pbuf = take(NP * P.nsets * P.scap * 8);
     L.fb_rec = take((size_t)kFbBlocks * kFbGroup * k * 24);
     L.desc = take((size_t)kMaxSubs * sizeof(SubDesc));
     L.blk_sub = take(kMaxF2Blocks);
@@ -2151,6 +2159,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
     if (nblk2) {
         F2Args a2{d_desc, d_blk, hd[0], nsub, NP, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, P.scap, ctr,
                   narrow ? P.nstage : P.stage, dbg, P.sparse, seg, (dbg & 256) ? stamps + 8192 * 16 : stamps};
+        a2.nsets = P.nsets;
         const dim3 g2(nblk2), b2(kF2Threads);
         const size_t l2 = f2_lds(P, narrow);
 #define F2_GO(MM)                                                    \
@@ -2171,7 +2180,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
     // the base arguments are the whole set's: F4's scan (fallback targets) runs over all its ids
     F3Args a{pbuf, pcount, P.scap, tbuf, tcount, P.tcap, tspill, P.Lm, P.b1, P.Lq, bitmap, P.nwords, c.planes, c.stride,
              c.n, c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, fb_sub, pstat, tie_hdr, tie_cand, tie_cnt,
-             d_desc, np, dbg, stamps, narrow ? P.f3cap : P.f3cap_wide, RecOut{}, P.Lm - P.sib};
+             d_desc, np, dbg, stamps, narrow ? P.f3cap : P.f3cap_wide, RecOut{}, P.Lm - P.sib, P.nsets};
     if (c.out_rec)
         a.rec = RecOut{c.out_rec, c.planes, c.stride, c.rec_gidx, c.rec_base, (nsub == 1 && !c.w0s && !c.skip) ? 1u : 0u};
 
