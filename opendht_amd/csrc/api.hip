@@ -123,8 +123,10 @@ struct dhtgpu_ctx {
     struct SubPart {
         DevBuf planes, map, gmap, w0s;   // planes: 5 * stride u32; map: sub -> ctx-local; gmap: sub -> global
         uint64_t n = 0, stride = 0;
+        uint32_t span[32] = {};          // launch_cell_spans of w0s (host copy): F2's window bound
     };
     std::vector<SubPart> subs;
+    std::vector<uint32_t> spans;   // [subs][32] the sub-partitions' span tables (BatchCall::spans)
     DevBuf cells;            // [subs][1 << cell_level()] u8 id counts per level-cell_level() prefix (F1's sibling rule)
     DevBuf hinv;             // [n] context-local index -> sub-partition handle
     uint32_t sub_bits = 0;
@@ -779,9 +781,17 @@ static int build_subs(dhtgpu_ctx* c) {
         for (size_t i = 0; e == hipSuccess && i < c->subs.size(); ++i)
             e = launch_cell_counts(c->subs[i].w0s.as<uint32_t>(), c->subs[i].n, cnt.as<uint32_t>(),
                                    c->cells.as<uint8_t>() + i * ncell, s);
+        for (size_t i = 0; e == hipSuccess && i < c->subs.size(); ++i) {   // window bounds (sorted subs)
+            e = launch_cell_spans(c->subs[i].w0s.as<uint32_t>(), c->subs[i].n, cnt.as<uint32_t>(), s);
+            if (e == hipSuccess) e = hipMemcpyAsync(c->subs[i].span, cnt.p, 32 * 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+        }
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         cnt.release();
         DHT_TRY(e);
+        c->spans.resize(c->subs.size() * 32);
+        for (size_t i = 0; i < c->subs.size(); ++i)
+            std::copy(c->subs[i].span, c->subs[i].span + 32, c->spans.begin() + i * 32);
     }
     DHT_TRY(c->hinv.ensure((size_t)(c->n ? c->n : 1) * 4));
     {
@@ -865,6 +875,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     bc.k = k;
     bc.skip = P;
     bc.cells = c->cells.as<uint8_t>();
+    bc.spans = c->spans.empty() ? nullptr : c->spans.data();
     bc.gidx = global ? c->gidx.as<uint32_t>() : nullptr;
     bc.base = 0;
     bc.out_idx = li;

@@ -227,6 +227,10 @@ constexpr int kF2Threads = 1024;
 constexpr uint32_t kF2Sub = 4 * kF2Threads;          // ids per sub-step (one uint4 per thread)
 constexpr uint32_t kF2Step = 4 * kF2Sub;             // ids per chunk
 constexpr uint32_t kStage = 11264;                   // LDS stage entries (88 KB)
+// window mode (prefix-sorted sub-partitions: a workgroup's bitmap is the window of words its
+// sorted range spans, a few KB instead of 64): the stage takes the freed LDS when one final flush
+// then holds the workgroup's survivors (the cfg-3 shard: 16.2 K per workgroup, two flushes before)
+constexpr uint32_t kStageWin = 25600;
 
 __host__ __device__ inline uint32_t f2_fixed_words(uint32_t nwords, uint32_t np) {
     return (36 + nwords + np + 1 + 17 + np / 32 + 1 + 3) & ~3u;
@@ -248,6 +252,8 @@ struct F2Args {
     uint32_t seg;                 // sparse mode: ids per segment (the stage is flushed after each)
     unsigned long long* stamps;   // dbg & 256: per-block phase timestamps [nblk2][16]
     uint32_t nsets;               // kSets, or 1 over prefix-sorted sub-partitions (a partition's survivors come from one or two workgroups)
+    uint32_t wwords;              // window mode: bitmap words in LDS (the window from the range's first word)
+    uint32_t pk_ob;               // window + Sparse: index-offset bits of the packed stage (StagePk)
 };
 #define F2_STAMP(i) \
     do { if ((a.dbg & 256) && threadIdx.x == 0) a.stamps[(uint64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -262,34 +268,49 @@ struct F2Args {
 // [a.stage] u32 then the id's offset from the workgroup's first id [a.stage] u16 -- 6 B per
 // entry instead of 8, so F2's LDS leaves room for an F3 workgroup of another batch on its CU.
 constexpr uint32_t kStagePer = (kStage + 1023) / 1024;
-template <bool Narrow>
-__device__ __forceinline__ uint2 stage_get(const uint2* stage, uint32_t cap, uint32_t ibase, uint32_t j) {
-    if (!Narrow) return stage[j];
+constexpr uint32_t kStagePerWin = (kStageWin + 1023) / 1024;
+// Packed stage (window mode, Sparse): the same two arrays, holding the 48-bit value
+// (w0 - wb0) << ob | (index - the workgroup's first id): a sorted workgroup range spans a few
+// thousand bitmap words, so its word 0 minus the window's first word fits 48 - ob bits (the host
+// checks) -- the stage of the cfg-3 shard's 16 K-survivor ranges then fits one final flush.
+struct StagePk { uint32_t wb0, ob; };
+template <int Fmt>   // 0: 8-B {w0, index}; 1: narrow (u32 w0, u16 offset); 2: packed
+__device__ __forceinline__ uint2 stage_get(const uint2* stage, uint32_t cap, uint32_t ibase, uint32_t j, StagePk pk) {
+    if (Fmt == 0) return stage[j];
     const uint32_t* sw = reinterpret_cast<const uint32_t*>(stage);
     const uint16_t* si = reinterpret_cast<const uint16_t*>(sw + cap);
-    return make_uint2(sw[j], ibase + si[j]);
+    if (Fmt == 1) return make_uint2(sw[j], ibase + si[j]);
+    const uint64_t v = (uint64_t)si[j] << 32 | sw[j];
+    return make_uint2(pk.wb0 + (uint32_t)(v >> pk.ob), ibase + (uint32_t)(v & ((1ull << pk.ob) - 1ull)));
 }
-template <bool Narrow>
-__device__ __forceinline__ void stage_put(uint2* stage, uint32_t cap, uint32_t ibase, uint32_t j, uint32_t w, uint32_t i) {
-    if (!Narrow) { stage[j] = make_uint2(w, i); return; }
+template <int Fmt>
+__device__ __forceinline__ void stage_put(uint2* stage, uint32_t cap, uint32_t ibase, uint32_t j, uint32_t w, uint32_t i,
+                                          StagePk pk) {
+    if (Fmt == 0) { stage[j] = make_uint2(w, i); return; }
     uint32_t* sw = reinterpret_cast<uint32_t*>(stage);
     uint16_t* si = reinterpret_cast<uint16_t*>(sw + cap);
-    sw[j] = w;
-    si[j] = (uint16_t)(i - ibase);
+    if (Fmt == 1) {
+        sw[j] = w;
+        si[j] = (uint16_t)(i - ibase);
+        return;
+    }
+    const uint64_t v = (uint64_t)(w - pk.wb0) << pk.ob | (i - ibase);
+    sw[j] = (uint32_t)v;
+    si[j] = (uint16_t)(v >> 32);
 }
-template <bool Narrow>
+template <int Fmt, uint32_t Per = kStagePer>
 __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* hist, uint32_t* wsum, uint32_t poff,
-                         uint32_t ibase) {
+                         uint32_t ibase, StagePk pk = StagePk{0u, 0u}) {
     const uint32_t np = 1u << a.b1;
     for (uint32_t i = threadIdx.x; i <= np; i += kF2Threads) hist[i] = 0;
     sync_lds();
-    uint2 e[kStagePer];
-    uint32_t rk[kStagePer];
+    uint2 e[Per];
+    uint32_t rk[Per];
 #pragma unroll
-    for (uint32_t r = 0; r < kStagePer; ++r) {
+    for (uint32_t r = 0; r < Per; ++r) {
         const uint32_t j = r * kF2Threads + threadIdx.x;
         if (j < cnt) {
-            e[r] = stage_get<Narrow>(stage, a.stage, ibase, j);
+            e[r] = stage_get<Fmt>(stage, a.stage, ibase, j, pk);
             rk[r] = atomicAdd(hist + top_bits(e[r].x, a.b1), 1u);
         }
     }
@@ -307,9 +328,9 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
     scan_lds<kF2Threads>(hist, np, wsum);   // hist = partition starts inside the stage
     if (threadIdx.x == 0) hist[np] = cnt;
 #pragma unroll
-    for (uint32_t r = 0; r < kStagePer; ++r) {
+    for (uint32_t r = 0; r < Per; ++r) {
         const uint32_t j = r * kF2Threads + threadIdx.x;
-        if (j < cnt) stage_put<Narrow>(stage, a.stage, ibase, hist[top_bits(e[r].x, a.b1)] + rk[r], e[r].x, e[r].y);
+        if (j < cnt) stage_put<Fmt>(stage, a.stage, ibase, hist[top_bits(e[r].x, a.b1)] + rk[r], e[r].x, e[r].y, pk);
     }
     // wsum is free again: reuse the stage-local starts to turn reservations into deltas
     // (bucket offset of stage position j = res[p] - start[p] + j)
@@ -328,7 +349,7 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
     sync_lds();
     F2_STAMP(4);
     for (uint32_t j = threadIdx.x; j < cnt; j += kF2Threads) {
-        const uint2 x = stage_get<Narrow>(stage, a.stage, ibase, j);
+        const uint2 x = stage_get<Fmt>(stage, a.stage, ibase, j, pk);
         const uint32_t p = top_bits(x.x, a.b1);
         const uint32_t pos = hist[p] + j;
         if (pos < a.pcap) a.pbuf[(uint64_t)((poff + p) * a.nsets + set) * a.pcap + pos] = x;
@@ -384,19 +405,28 @@ constexpr uint32_t kF2Dense = 0, kF2Sparse = 1, kF2Seg = 3, kF2Narrow = 4;
 // non-temporal ones re-read it from HBM every call (cfg 2: F2 20.5 -> 22.9 us).
 constexpr uint32_t kF2One = 0, kF2Subs = 1, kF2SubsNT = 2;
 constexpr uint64_t kNtBytes = 192ull << 20;   // 3/4 of the 256 MB Infinity Cache
-template <uint32_t Mode, uint32_t Src>
+// Win (Subs only): the sub-partitions are sorted by prefix, so a workgroup's contiguous id range
+// spans a narrow run of bitmap words, starting at its first id's: only that window (a.wwords words,
+// which the host bounded from the sub-partitions' span table) is copied to LDS, and the stage
+// takes the rest (Sparse: one final flush of up to kStageWin entries)
+template <uint32_t Mode, uint32_t Src, bool Win = false>
 __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     constexpr bool Subs = Src != kF2One, NT = Src == kF2SubsNT;
     constexpr bool Narrow = Mode == kF2Narrow;
     constexpr bool Sparse = Mode == kF2Sparse || Mode == kF2Seg || Narrow;
-    extern __shared__ uint32_t sh[];   // (32 spare) | misc[8] | bm[nwords] | hist[np + 1] | wsum[17] | lost[np/32 + 1] | stage
+    constexpr bool Pack = Win && Mode == kF2Sparse;   // window + one final flush: the packed stage
+    constexpr int Fmt = Pack ? 2 : Narrow ? 1 : 0;
+    constexpr uint32_t Per = Pack ? kStagePerWin : kStagePer;
+    static_assert(!Win || (Subs && !Narrow), "window mode: sorted sub-partitions, 8-B stage");
+    extern __shared__ uint32_t sh[];   // (32 spare) | misc[8] | bm[bmw] | hist[np + 1] | wsum[17] | lost[np/32 + 1] | stage
     const uint32_t np = 1u << a.b1;
+    const uint32_t bmw = Win ? a.wwords : a.nwords;
     uint32_t* misc = sh + 28;
     uint32_t* bm = sh + 36;
-    uint32_t* hist = bm + a.nwords;
+    uint32_t* hist = bm + bmw;
     uint32_t* wsum = hist + np + 1;
     uint32_t* lost = wsum + 17;   // sparse mode: partitions that lost survivors past a full stage
-    uint2* stage = reinterpret_cast<uint2*>(sh + f2_fixed_words(a.nwords, np));
+    uint2* stage = reinterpret_cast<uint2*>(sh + f2_fixed_words(bmw, np));
     const uint32_t sub = Subs ? (uint32_t)a.blk_sub[blockIdx.x] : 0u;
     const SubDesc d = Subs ? a.subs[sub] : a.one;
     const uint64_t lo64 = (uint64_t)(blockIdx.x - d.blk0) * d.per_blk;
@@ -416,7 +446,21 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
     // shorten this phase either: it is the fabric, not the source); indices past the end are
     // clamped, so a clamped lane rewrites a word with its own value
     const uint32_t* bsrc = a.bitmap + sub * a.nwords;
-    if ((a.nwords & 3) == 0) {
+    // window mode: the bitmap word of the range's first (smallest) id -- the first load of the
+    // workgroup, waited for alone; the window's words (<= 2 per thread) are loaded before the ring
+    // is issued and stored to LDS after it, so their round trip overlaps the ring's
+    uint32_t wbase = 0, wv0 = 0, wv1 = 0;
+    if (Win) {
+        const uint32_t flim = min(d.lim, ((hi + 3u) & ~3u) - 4u);
+        const uint32_t f0 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(f2_rsrc(w0, lo, flim), 0, 0, 0);
+        wbase = a.Lm > 5 ? __builtin_amdgcn_readfirstlane(f0 >> (pre_off + 5)) : 0u;
+        const uint32_t i0 = wbase + threadIdx.x, i1 = i0 + kF2Threads;
+        wv0 = threadIdx.x < a.wwords && i0 < a.nwords ? bsrc[i0] : 0u;
+        wv1 = threadIdx.x + kF2Threads < a.wwords && i1 < a.nwords ? bsrc[i1] : 0u;
+    }
+    const StagePk pk{Win && a.Lm > 5 ? wbase << (pre_off + 5) : 0u, a.pk_ob};
+    if (Win) {
+    } else if ((a.nwords & 3) == 0) {
         for (uint32_t i0 = 0; i0 < a.nwords; i0 += kF2Threads * 16) {
             uint4 t[4];
             uint32_t ic[4];
@@ -442,6 +486,10 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
 #pragma unroll
     for (uint32_t r = 0; r < kF2Ring; ++r)
         ring[r] = Subs ? f2_load1<NT>(rs, lo, lo + r * kF2Sub, lim) : f2_load1g(w0, lo + r * kF2Sub, lim);
+    if (Win) {
+        if (threadIdx.x < a.wwords) bm[threadIdx.x] = wv0;
+        if (threadIdx.x + kF2Threads < a.wwords) bm[threadIdx.x + kF2Threads] = wv1;
+    }
     if (threadIdx.x < 3) misc[threadIdx.x] = 0;
     for (uint32_t i = threadIdx.x; i <= np / 32; i += kF2Threads) lost[i] = 0;
     sync_lds();
@@ -456,7 +504,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
         if (Mode == kF2Seg && c0 != lo && (c0 - lo) % a.seg == 0) {
             // segment boundary (block-uniform): flush while the ring's next loads are in flight
             sync_lds();
-            f2_flush<false>(a, misc[0] < a.stage ? misc[0] : a.stage, stage, hist, wsum, poff, 0u);
+            f2_flush<0, Per>(a, misc[0] < a.stage ? misc[0] : a.stage, stage, hist, wsum, poff, 0u);
             if (threadIdx.x == 0) misc[0] = 0;
             sync_lds();
         }
@@ -465,7 +513,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
             const uint32_t sb = c0 + r * kF2Sub;
             if (sb < hi) {   // block-uniform
                 if (Mode == kF2Dense && cnt > a.stage - kF2Sub) {
-                    f2_flush<false>(a, cnt, stage, hist, wsum, poff, 0u);
+                    f2_flush<0, Per>(a, cnt, stage, hist, wsum, poff, 0u);
                     cnt = 0;
                 }
                 const uint32_t j0 = sb + 4 * threadIdx.x;
@@ -479,7 +527,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                 // read waited before the next issued)
                 uint32_t bw[4];
 #pragma unroll
-                for (uint32_t f = 0; f < 4; ++f) bw[f] = bm[__builtin_amdgcn_ubfe(v4[f], pre_off + 5, lm5)];
+                for (uint32_t f = 0; f < 4; ++f) bw[f] = bm[__builtin_amdgcn_ubfe(v4[f], pre_off + 5, lm5) - wbase];
 #pragma unroll
                 for (uint32_t f = 0; f < 4; ++f) {
                     // prefix bit: word pre >> 5 of the bitmap, bit pre & 31 (v_bfe masks it)
@@ -506,7 +554,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                         if (sv[f]) {
                             const uint32_t at = __builtin_amdgcn_mbcnt_hi(
                                 (uint32_t)(bal[f] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[f], pos));
-                            stage_put<Narrow>(stage, a.stage, lo, at, v4[f], j0 + f);
+                            stage_put<Fmt>(stage, a.stage, lo, at, v4[f], j0 + f, pk);
                         }
                         pos += (uint32_t)__popcll(bal[f]);
                     }
@@ -521,7 +569,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
                             const uint32_t at = __builtin_amdgcn_mbcnt_hi(
                                 (uint32_t)(bal[f] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[f], pos));
                             if (at < a.stage) {
-                                stage_put<Narrow>(stage, a.stage, lo, at, v4[f], j0 + f);
+                                stage_put<Fmt>(stage, a.stage, lo, at, v4[f], j0 + f, pk);
                             } else {
                                 const uint32_t p = top_bits(v4[f], a.b1);
                                 atomicOr(lost + (p >> 5), 1u << (p & 31));
@@ -543,7 +591,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
         cnt = misc[0] < a.stage ? misc[0] : a.stage;
     }
     F2_STAMP(2);
-    if (cnt) f2_flush<Narrow>(a, cnt, stage, hist, wsum, poff, lo);
+    if (cnt) f2_flush<Fmt, Per>(a, cnt, stage, hist, wsum, poff, lo, pk);
     if (Sparse) {   // partitions that lost entries: count past any stage (F3 -> fallback)
         for (uint32_t i = threadIdx.x; i <= np / 32; i += kF2Threads) {
             uint32_t m = lost[i];
@@ -1501,7 +1549,13 @@ struct BatchPlan {
     uint32_t scap;   // survivors per (bucket set, partition)
     uint32_t f3cap_wide;   // F3's LDS stage entries when F2 runs its 8-B stage (no narrow stage)
     uint32_t cap6;         // the plan's 6-sigma partition bound (F3 stage entries, <= kF3Cap)
+    uint32_t wwords;       // F2 window mode: bitmap words in LDS per workgroup (0: the whole bitmap)
+    bool wpack;            // window mode's stage is packed (6 B; one final flush) -- else 8 B, segments
     uint32_t nsets;        // F2 bucket sets per partition: kSets, or 1 over prefix-sorted sub-partitions
+    // variance of an F2 range's survivor count per expected survivor: ids of a range are a random
+    // sample (1 - f), or -- prefix-sorted sub-partitions -- whole level-Lm cells of mu ids each,
+    // marked with probability f ((1 - f) mu + 1: ~30x the binomial at the cfg-3 shard)
+    double clump;
     bool fits;   // partitions' survivors fit the F3 stage on uniform ids
     uint64_t per_blk;
 };
@@ -1524,23 +1578,25 @@ double poisson_below(double m, uint32_t k) {
     return sum;
 }
 
-BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bool cells);
+BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bool cells, uint32_t wwords);
 
-// plan_batch is a pure function of (n, q, k, CUs, cells), asked three times per call (workspace
-// size, clean head, the launch): the last few plans are kept per host thread
-BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus, bool cells = false) {
-    struct Entry { uint64_t n; uint32_t q, k; int cus; bool cells; BatchPlan P; bool used; };
-    thread_local Entry cache[4] = {};
+// plan_batch is a pure function of (n, q, k, CUs, cells, window), asked three times per call
+// (workspace size, clean head, the launch): the last few plans are kept per host thread
+BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus, bool cells = false, uint32_t wwords = 0) {
+    struct Entry { uint64_t n; uint32_t q, k; int cus; bool cells; uint32_t ww; BatchPlan P; bool used; };
+    thread_local Entry cache[6] = {};
     thread_local uint32_t next = 0;
     for (const Entry& e : cache)
-        if (e.used && e.n == n && e.q == q && e.k == k && e.cus == num_cus && e.cells == cells) return e.P;
-    Entry& e = cache[next++ & 3u];
-    e = Entry{n, q, k, num_cus, cells, plan_batch_compute(n, q, k, num_cus, cells), true};
+        if (e.used && e.n == n && e.q == q && e.k == k && e.cus == num_cus && e.cells == cells && e.ww == wwords)
+            return e.P;
+    Entry& e = cache[next++ % 6u];
+    e = Entry{n, q, k, num_cus, cells, wwords, plan_batch_compute(n, q, k, num_cus, cells, wwords), true};
     return e.P;
 }
 
-BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bool cells) {
+BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bool cells, uint32_t wwords) {
     BatchPlan P;
+    P.wwords = wwords;
     // mark level: 4k or more ids per level-Lm subtree -- or one level finer (2k..4k) when, on
     // uniform ids, fewer than 0.01 of the q targets are expected to land in a subtree with
     // under k ids (those go to the F4 brute force).  Without the finer step a prefix shard
@@ -1592,6 +1648,7 @@ BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bo
     // bucket set, sized for the whole partition (with 8 sets planned for an eighth each, every
     // partition overflowed its set)
     P.nsets = cells ? 1u : kSets;
+    P.clump = cells ? (1.0 - f) * (double)n / (double)(1ull << P.Lm) + 1.0 : 1.0 - f;
     {   // a set holds each id with probability 1 / kSets (ids are spread over the blocks by
         // index, independently of their prefix): mean + 8 sigma + 64 of one set's share
         const double sub = (double)(1ull << (P.Lm - b1)), mu = (double)n / (double)(1ull << P.Lm) / P.nsets;
@@ -1634,15 +1691,18 @@ BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bo
     const uint64_t cpb = (chunks + g - 1) / g;
     P.per_blk = (cpb ? cpb : 1) * kF2Step;
     P.nblk2 = (uint32_t)((n + P.per_blk - 1) / P.per_blk);
-    // F2 LDS stage: what is left of the LDS next to the bitmap and histogram
-    const size_t fixed = (size_t)f2_fixed_words(P.nwords, 1u << P.b1) * 4;
+    // F2 LDS stage: what is left of the LDS next to the bitmap (or its window) and histogram
+    const size_t fixed = (size_t)f2_fixed_words(wwords ? wwords : P.nwords, 1u << P.b1) * 4;
+    // (window mode: a packed 6-B stage while one final flush holds the range's survivors)
     const size_t room = fixed < kLdsMax ? (kLdsMax - fixed) / 8 : 0;
-    P.stage = (uint32_t)(room < kStage ? room : kStage);
+    const size_t room6 = fixed + 1024 < kLdsMax ? (kLdsMax - fixed - 1024) / 6 : 0;
+    P.stage = wwords ? (uint32_t)std::min<size_t>(room6, kStageWin) : (uint32_t)(room < kStage ? room : kStage);
+    P.wpack = wwords != 0;
     // sparse mode when a block's survivors (mean + 8 sigma on uniform ids) fit the stage,
     // with ranges shrunk (more blocks) while that helps
     P.sparse = 0;
     for (uint64_t pb = P.per_blk; pb >= kF2Step; pb /= 2) {
-        const double mean = (double)pb * f, sd = std::sqrt(mean * (1.0 - f));
+        const double mean = (double)pb * f, sd = std::sqrt(mean * P.clump);
         if (mean + 8.0 * sd + 256.0 <= (double)P.stage) {
             P.sparse = 1;
             P.per_blk = (pb / kF2Step) * kF2Step;
@@ -1650,6 +1710,12 @@ BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bo
             break;
         }
         if (pb == kF2Step) break;
+    }
+    // window mode past one stage-full: the segmented instantiation's flush holds kStagePer entries
+    // per thread in registers (its ring stays live across the flush: 128 VGPRs at most)
+    if (wwords && !P.sparse) {
+        P.stage = (uint32_t)(room < kStage ? room : kStage);
+        P.wpack = false;
     }
     // F2's narrow stage (6 B per entry: ranges < 2^16 ids, the cfg-2 shape): sized so that F2
     // plus one F3 workgroup fit a CU's LDS -- the F2 of one batch in flight and the F3 of another
@@ -1659,7 +1725,7 @@ BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bo
     // for the LDS allocation granule.
     P.nstage = 0;
     P.f3cap_wide = P.f3cap;
-    if (P.sparse && P.per_blk <= 65536) {
+    if (P.sparse && P.per_blk <= 65536 && !wwords) {
         const double mean = (double)P.per_blk * f, sd = std::sqrt(mean * (1.0 - f));
         const double need2 = mean + 8.0 * sd + 256.0;
         for (int pass = 0; pass < 2 && !P.nstage; ++pass) {
@@ -1681,7 +1747,9 @@ BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bo
 }
 
 size_t f2_lds(const BatchPlan& P, bool narrow = false) {
-    return (size_t)f2_fixed_words(P.nwords, 1u << P.b1) * 4 + (narrow ? (size_t)P.nstage * 6 : (size_t)P.stage * 8);
+    const size_t fixed = (size_t)f2_fixed_words(P.wwords ? P.wwords : P.nwords, 1u << P.b1) * 4;
+    if (P.wpack) return fixed + (size_t)P.stage * 6;   // window mode's packed stage
+    return fixed + (narrow ? (size_t)P.nstage * 6 : (size_t)P.stage * 8);
 }
 
 size_t f3_lds(const BatchPlan& P, uint32_t cap) {
@@ -1803,6 +1871,8 @@ void set_lds_attributes() {
                         (const void*)k_f2_filter<kF2Dense, kF2SubsNT>, (const void*)k_f2_filter<kF2Sparse, kF2SubsNT>,
                         (const void*)k_f2_filter<kF2Seg, kF2SubsNT>,
                         (const void*)k_f2_filter<kF2Narrow, kF2SubsNT>,
+                        (const void*)k_f2_filter<kF2Sparse, kF2Subs, true>, (const void*)k_f2_filter<kF2Seg, kF2Subs, true>,
+                        (const void*)k_f2_filter<kF2Sparse, kF2SubsNT, true>, (const void*)k_f2_filter<kF2Seg, kF2SubsNT, true>,
                         (const void*)k_f3_answer<8, false, true, false>,  (const void*)k_f3_answer<16, false, true, false>,
                         (const void*)k_f3_answer<32, false, true, false>, (const void*)k_f3_answer<8, true, true, false>,
                         (const void*)k_f3_answer<16, true, true, false>,  (const void*)k_f3_answer<32, true, true, false>,
@@ -1876,7 +1946,7 @@ uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, 
     if (P.sparse) {
         pb_cap = kF2Step;
         for (uint64_t pb = kF2Step; pb <= (1ull << 31); pb += kF2Step) {
-            const double mean = (double)pb * f, sd = std::sqrt(mean * (1.0 - f));
+            const double mean = (double)pb * f, sd = std::sqrt(mean * P.clump);
             if (mean + 8.0 * sd + 256.0 > (double)P.stage) break;
             pb_cap = pb;
         }
@@ -1971,6 +2041,38 @@ __global__ void k_cell_pack(const uint32_t* __restrict__ cnt, uint8_t* __restric
 }
 
 uint32_t cell_level() { return kMaxLm; }
+
+// spans[j] = max over i of cell(i + 2^j - 1) - cell(i) (level-kMaxLm cells of a prefix-sorted
+// shifted word-0 plane; the last id when 2^j > n - i): the most cells (hence bitmap words) any
+// 2^j consecutive ids of the sub-partition span -- F2's window bound (j < 32)
+__global__ void k_cell_spans(const uint32_t* __restrict__ w0s, uint64_t n, uint32_t* __restrict__ spans) {
+    __shared__ uint32_t smax[32];
+    if (threadIdx.x < 32) smax[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t mx[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) mx[j] = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t c0 = w0s[i] >> (32 - kMaxLm);
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const uint64_t e = i + (1ull << j) - 1;
+            const uint32_t c1 = w0s[e < n ? e : n - 1] >> (32 - kMaxLm);
+            mx[j] = max(mx[j], c1 - c0);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 32; ++j) atomicMax(&smax[j], mx[j]);
+    __syncthreads();
+    if (threadIdx.x < 32) atomicMax(spans + threadIdx.x, smax[threadIdx.x]);
+}
+
+hipError_t launch_cell_spans(const uint32_t* w0s, uint64_t n, uint32_t* spans, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(spans, 0, 32 * 4, s);
+    if (e != hipSuccess || !n) return e;
+    k_cell_spans<<<dim3(1024), dim3(256), 0, s>>>(w0s, n, spans);
+    return hipGetLastError();
+}
 
 hipError_t launch_cell_counts(const uint32_t* w0s, uint64_t n, uint32_t* scratch, uint8_t* out, hipStream_t s) {
     hipError_t e = hipMemsetAsync(scratch, 0, ((size_t)1 << kMaxLm) * 4, s);
@@ -2074,7 +2176,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
         n_all += subs[i].n;
     }
     const bool nt = 4 * n_all > kNtBytes;   // F2's ring: non-temporal past the Infinity Cache
-    const BatchPlan P = plan_batch(n_max, c.q_plan, k, c.num_cus, c.cells != nullptr);
+    BatchPlan P = plan_batch(n_max, c.q_plan, k, c.num_cus, c.cells != nullptr);
     const uint32_t np = 1u << P.b1, NP = nsub * np;
     uint32_t dbg = c.dbg & 256u;   // the only diagnostics bit: phase stamps (results unchanged)
     hipEvent_t* ev = c.ev;
@@ -2101,8 +2203,60 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
     // arguments; several are uploaded when they differ from what this workspace holds
     // (steady-state calls upload nothing)
     SubDesc hd[kMaxSubs];
-    uint32_t seg = 0;
-    const uint32_t nblk2 = deal_f2_blocks(P, subs, nsub, c.q_plan, c.num_cus, hd, &seg);
+    uint32_t seg = 0, pk_ob = 0;
+    uint32_t nblk2 = deal_f2_blocks(P, subs, nsub, c.q_plan, c.num_cus, hd, &seg);
+    // window mode (prefix-sorted sub-partitions with span tables): every workgroup's bitmap window
+    // is bounded by its sub-partition's largest cell span over as many consecutive ids as the
+    // workgroup holds; taken when that bound is small (the cfg-3 shard: ~520 words of 16,384)
+    if (c.spans && nsub > 1 && P.sparse && P.Lm >= 6 && P.Lm <= kMaxLm) {
+        auto need = [&](const SubDesc* dd) {
+            uint32_t w = 0;
+            for (uint32_t i = 0; i < nsub; ++i) {
+                if (!dd[i].nblk) continue;
+                uint32_t j = 0;
+                while (j < 31 && (1ull << j) < dd[i].per_blk) ++j;
+                const uint32_t span19 = c.spans[i * 32 + j];   // level-kMaxLm cells
+                w = std::max<uint32_t>(w, (span19 >> (kMaxLm - P.Lm + 5)) + 3u);
+            }
+            return w;
+        };
+        uint32_t ww = 64;
+        while (ww < need(hd)) ww <<= 1;
+        if (ww <= 2 * kF2Threads && 2 * ww <= P.nwords) {
+            BatchPlan Pw = plan_batch(n_max, c.q_plan, k, c.num_cus, c.cells != nullptr, ww);
+            SubDesc hw[kMaxSubs];
+            uint32_t segw = 0;
+            uint32_t nbw = deal_f2_blocks(Pw, subs, nsub, c.q_plan, c.num_cus, hw, &segw);
+            bool segd = false;
+            for (uint32_t i = 0; i < nsub; ++i) segd = segd || (hw[i].nblk && hw[i].per_blk > segw);
+            if (Pw.sparse && segd) {   // ranges past one packed stage-full: 8-B segments (kStagePer in registers)
+                const size_t fx = (size_t)f2_fixed_words(ww, 1u << Pw.b1) * 4;
+                Pw.stage = (uint32_t)std::min<size_t>(fx < kLdsMax ? (kLdsMax - fx) / 8 : 0, kStage);
+                Pw.wpack = false;
+                nbw = deal_f2_blocks(Pw, subs, nsub, c.q_plan, c.num_cus, hw, &segw);
+            }
+            // the packed stage's index offsets take ob bits, word 0 above the window's first word
+            // log2(ww) + 37 - Lm bits: 48 in all
+            uint64_t pbmax = 1;
+            for (uint32_t i = 0; i < nsub; ++i) pbmax = std::max<uint64_t>(pbmax, hw[i].nblk ? hw[i].per_blk : 1);
+            uint32_t ob = 0, lw = 0;
+            while ((1ull << ob) < pbmax) ++ob;
+            while ((1u << lw) < ww) ++lw;
+            bool ok = Pw.sparse && need(hw) <= ww && nbw <= kMaxF2Blocks;
+            bool segw_used = false;
+            for (uint32_t i = 0; i < nsub; ++i) segw_used = segw_used || (hw[i].nblk && hw[i].per_blk > segw);
+            if (Pw.wpack) ok = ok && !segw_used && lw + 37 - Pw.Lm + ob <= 48;
+            else ok = ok && segw_used;   // (8-B window stage: the segmented instantiation only)
+            if (ok) {
+                P = Pw;
+                nblk2 = nbw;
+                seg = segw;
+                pk_ob = ob;
+                std::copy(hw, hw + nsub, hd);
+            }
+        }
+    }
+    const bool win = P.wwords != 0;
     bool seg_used = false;   // some workgroup's range spans more than one segment
     for (uint32_t i = 0; i < nsub; ++i) seg_used = seg_used || (hd[i].nblk && hd[i].per_blk > seg);
     if (nblk2 > kMaxF2Blocks) return hipErrorInvalidValue;
@@ -2112,7 +2266,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
     {
         const double f = 1.0 - std::exp(-(double)c.q_plan / (double)(1ull << P.Lm));
         for (uint32_t i = 0; i < nsub && narrow; ++i) {
-            const double mean = (double)hd[i].per_blk * f, sd = std::sqrt(mean * (1.0 - f));
+            const double mean = (double)hd[i].per_blk * f, sd = std::sqrt(mean * P.clump);
             if (hd[i].nblk && (hd[i].per_blk > 65536 || mean + 8.0 * sd + 256.0 > (double)P.nstage)) narrow = false;
         }
     }
@@ -2160,6 +2314,8 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
         F2Args a2{d_desc, d_blk, hd[0], nsub, NP, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, P.scap, ctr,
                   narrow ? P.nstage : P.stage, dbg, P.sparse, seg, (dbg & 256) ? stamps + 8192 * 16 : stamps};
         a2.nsets = P.nsets;
+        a2.wwords = P.wwords;
+        a2.pk_ob = pk_ob;
         const dim3 g2(nblk2), b2(kF2Threads);
         const size_t l2 = f2_lds(P, narrow);
 #define F2_GO(MM)                                                    \
@@ -2168,7 +2324,12 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
         else if (nsub > 1) go(1, k_f2_filter<MM, kF2Subs>, g2, b2, l2, a2);   \
         else go(1, k_f2_filter<MM, kF2One>, g2, b2, l2, a2);                  \
     } while (0)
-        if (narrow) F2_GO(kF2Narrow);
+        // window mode: the packed stage with one final flush (P.wpack), or 8-B segments
+        if (win && nt && !P.wpack) go(1, k_f2_filter<kF2Seg, kF2SubsNT, true>, g2, b2, l2, a2);
+        else if (win && nt) go(1, k_f2_filter<kF2Sparse, kF2SubsNT, true>, g2, b2, l2, a2);
+        else if (win && !P.wpack) go(1, k_f2_filter<kF2Seg, kF2Subs, true>, g2, b2, l2, a2);
+        else if (win) go(1, k_f2_filter<kF2Sparse, kF2Subs, true>, g2, b2, l2, a2);
+        else if (narrow) F2_GO(kF2Narrow);
         else if (P.sparse && seg_used) F2_GO(kF2Seg);
         else if (P.sparse) F2_GO(kF2Sparse);
         else F2_GO(kF2Dense);

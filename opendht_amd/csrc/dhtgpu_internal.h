@@ -133,6 +133,9 @@ uint32_t cell_level();
 // u8 counts (saturated) of the n ids of a shifted word-0 plane per top-cell_level()-bit prefix;
 // scratch: 4 << cell_level() bytes
 hipError_t launch_cell_counts(const uint32_t* w0s, uint64_t n, uint32_t* scratch, uint8_t* out, hipStream_t s);
+// spans[j] (device, 32 words) = the most level-cell_level() cells that 2^j consecutive ids of a
+// prefix-sorted shifted word-0 plane span (K6's F2 window bound)
+hipError_t launch_cell_spans(const uint32_t* w0s, uint64_t n, uint32_t* spans, hipStream_t s);
 // prefix shards: out[i] = planes word 0 << shift | word 1 >> (32 - shift), i < stride
 hipError_t launch_shift_w0(const uint32_t* planes, uint64_t stride, uint32_t shift, uint32_t* out, hipStream_t s);
 // One prefix sub-partition of a K6 call's id set (host view; see batch.hip SubDesc).
@@ -173,6 +176,7 @@ struct BatchCall {
     uint64_t* desc_sig;                    // the workspace's uploaded sub-partition descriptors (signature)
     uint32_t skip; const uint32_t* w0s;    // w0s = 32 id bits from bit `skip` (every id shares its top skip bits)
     const uint8_t* cells;                  // nullable: [nsub][1 << cell_level()] cell counts of the sub-partitions
+    const uint32_t* spans;                 // nullable, HOST: [nsub][32] cell spans of the (prefix-sorted) sub-partitions
     const uint32_t* gidx; uint32_t base;   // result index map (nullable) or offset
     uint32_t* out_idx; uint32_t* out_cnt;  // rows of the ORIGINAL target indices
     // record form (nullable): every writer of a result row (F3, the wave paths, F4's scan and
