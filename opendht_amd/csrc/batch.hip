@@ -298,7 +298,11 @@ __device__ __forceinline__ void stage_put(uint2* stage, uint32_t cap, uint32_t i
     sw[j] = (uint32_t)v;
     si[j] = (uint16_t)(v >> 32);
 }
-template <int Fmt, uint32_t Per = kStagePer>
+// Agg (window mode): the stage holds a sorted range's survivors in stream order, so a wave's 64
+// entries fall into one or two partitions -- one LDS atomic per (wave, partition) instead of one
+// per entry on the same one or two addresses (which serialise: the window's single flush of 15 K
+// entries into ~8 partitions cost more than the two flushes it replaced)
+template <int Fmt, uint32_t Per = kStagePer, bool Agg = false>
 __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* hist, uint32_t* wsum, uint32_t poff,
                          uint32_t ibase, StagePk pk = StagePk{0u, 0u}) {
     const uint32_t np = 1u << a.b1;
@@ -306,12 +310,30 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
     sync_lds();
     uint2 e[Per];
     uint32_t rk[Per];
+    const uint32_t lane = lane_id();
 #pragma unroll
     for (uint32_t r = 0; r < Per; ++r) {
         const uint32_t j = r * kF2Threads + threadIdx.x;
-        if (j < cnt) {
-            e[r] = stage_get<Fmt>(stage, a.stage, ibase, j, pk);
-            rk[r] = atomicAdd(hist + top_bits(e[r].x, a.b1), 1u);
+        if (!Agg) {
+            if (j < cnt) {
+                e[r] = stage_get<Fmt>(stage, a.stage, ibase, j, pk);
+                rk[r] = atomicAdd(hist + top_bits(e[r].x, a.b1), 1u);
+            }
+            continue;
+        }
+        if (r * kF2Threads >= cnt) continue;   // block-uniform
+        if (j < cnt) e[r] = stage_get<Fmt>(stage, a.stage, ibase, j, pk);
+        const uint32_t key = j < cnt ? top_bits(e[r].x, a.b1) : DHT_NONE;
+        uint64_t todo = __ballot(j < cnt);
+        while (todo) {   // wave-uniform: one round per distinct partition among the wave's entries
+            const uint32_t l0 = (uint32_t)__ffsll((long long)todo) - 1;
+            const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)l0);
+            const uint64_t m = __ballot(key == kk) & todo;
+            uint32_t base = 0;
+            if (lane == l0) base = atomicAdd(hist + kk, (uint32_t)__popcll(m));
+            base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)l0);
+            if ((m >> lane) & 1ull) rk[r] = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            todo &= ~m;
         }
     }
     sync_lds();
@@ -504,7 +526,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
         if (Mode == kF2Seg && c0 != lo && (c0 - lo) % a.seg == 0) {
             // segment boundary (block-uniform): flush while the ring's next loads are in flight
             sync_lds();
-            f2_flush<0, Per>(a, misc[0] < a.stage ? misc[0] : a.stage, stage, hist, wsum, poff, 0u);
+            f2_flush<0, Per, Win>(a, misc[0] < a.stage ? misc[0] : a.stage, stage, hist, wsum, poff, 0u);
             if (threadIdx.x == 0) misc[0] = 0;
             sync_lds();
         }
@@ -513,7 +535,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
             const uint32_t sb = c0 + r * kF2Sub;
             if (sb < hi) {   // block-uniform
                 if (Mode == kF2Dense && cnt > a.stage - kF2Sub) {
-                    f2_flush<0, Per>(a, cnt, stage, hist, wsum, poff, 0u);
+                    f2_flush<0, Per, Win>(a, cnt, stage, hist, wsum, poff, 0u);
                     cnt = 0;
                 }
                 const uint32_t j0 = sb + 4 * threadIdx.x;
@@ -591,7 +613,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
         cnt = misc[0] < a.stage ? misc[0] : a.stage;
     }
     F2_STAMP(2);
-    if (cnt) f2_flush<Fmt, Per>(a, cnt, stage, hist, wsum, poff, lo, pk);
+    if (cnt) f2_flush<Fmt, Per, Win>(a, cnt, stage, hist, wsum, poff, lo, pk);
     if (Sparse) {   // partitions that lost entries: count past any stage (F3 -> fallback)
         for (uint32_t i = threadIdx.x; i <= np / 32; i += kF2Threads) {
             uint32_t m = lost[i];
