@@ -298,96 +298,88 @@ __device__ __forceinline__ void stage_put(uint2* stage, uint32_t cap, uint32_t i
     sw[j] = (uint32_t)v;
     si[j] = (uint16_t)(v >> 32);
 }
-// Agg (window mode): the stage holds a sorted range's survivors in stream order, so it is sorted by
-// partition except inside the sub-step where one partition ends and the next begins.  Wave w takes
-// the contiguous chunk [w C, (w + 1) C) of the stage (C = Per slices of 64 entries each), counts its
-// entries per distinct partition with ballots (one or two partitions per chunk), reserves each
-// partition's share of the stage with ONE returning LDS atomic per (wave, partition), and ranks its
-// entries from it.  (The per-entry LDS atomics of the general form hit one or two addresses here and
-// serialise: the window's single flush of 15 K entries cost 6.3 us of ranking, profiles/r06/stamps.)
+// Agg (window mode): a sorted range's survivors sit in the stage in stream order, so wave w's
+// contiguous chunk [w C, (w + 1) C) of it holds one or two partitions.  No stage sort: the wave
+// ranks its entries per partition in registers (up to 4 partitions a round), reserves each
+// partition's share of its bucket with one returning atomic per (wave, partition) -- all of a
+// round's in one instruction -- and stores the entries there itself.  (Sorting a sorted stage by
+// per-entry LDS atomics on one or two addresses serialised: the window's single flush of 15 K
+// entries spent 6 us ranking them.)
 template <int Fmt, uint32_t Per = kStagePer, bool Agg = false>
 __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* hist, uint32_t* wsum, uint32_t poff,
                          uint32_t ibase, StagePk pk = StagePk{0u, 0u}) {
     const uint32_t np = 1u << a.b1;
-    for (uint32_t i = threadIdx.x; i <= np; i += kF2Threads) hist[i] = 0;
-    sync_lds();
     uint2 e[Per];
     uint32_t rk[Per];
     const uint32_t lane = lane_id();
-    if (!Agg) {
-#pragma unroll
-        for (uint32_t r = 0; r < Per; ++r) {
-            const uint32_t j = r * kF2Threads + threadIdx.x;
-            if (j < cnt) {
-                e[r] = stage_get<Fmt>(stage, a.stage, ibase, j, pk);
-                rk[r] = atomicAdd(hist + top_bits(e[r].x, a.b1), 1u);
-            }
-        }
-    } else {
-        // phase 1 (registers only): wave w's chunk [w C, (w + 1) C), its entries' ranks among the
-        // chunk's entries of the same partition, up to 4 distinct partitions tracked per wave
+    if (Agg) {
         const uint32_t w = threadIdx.x >> 6;
         const uint32_t C = (cnt + kF2Threads - 1) / kF2Threads * 64;   // entries per wave (<= Per * 64)
-        uint32_t tk[4] = {DHT_NONE, DHT_NONE, DHT_NONE, DHT_NONE}, tc[4] = {0u, 0u, 0u, 0u}, nt = 0;
-        bool spill = false;
+        uint32_t valid = 0;   // bit r: slice r holds an entry for this lane
 #pragma unroll
         for (uint32_t r = 0; r < Per; ++r) {
-            if (r * 64 >= C) continue;   // block-uniform
             const uint32_t j = w * C + r * 64 + lane;
-            const bool v = j < cnt;
-            if (v) e[r] = stage_get<Fmt>(stage, a.stage, ibase, j, pk);
-            const uint32_t key = v ? top_bits(e[r].x, a.b1) : DHT_NONE;
-            uint64_t act = __ballot(v);
-            while (act) {   // wave-uniform: the slice's distinct partitions (one or two)
-                const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane((int)key, __ffsll((long long)act) - 1);
-                const uint64_t m = __ballot(key == kk) & act;
-                act &= ~m;
-                uint32_t q = 4;
-#pragma unroll
-                for (uint32_t x = 0; x < 4; ++x) q = (x < nt && tk[x] == kk) ? x : q;
-                if (q == 4 && nt < 4) { q = nt++; tk[q] = kk; }
-                if (q == 4) { spill = true; continue; }
-                if ((m >> lane) & 1ull) rk[r] = (tc[q] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))) | (q << 28);
-                tc[q] += (uint32_t)__popcll(m);
+            if (r * 64 < C && j < cnt) {
+                e[r] = stage_get<Fmt>(stage, a.stage, ibase, j, pk);
+                valid |= 1u << r;
             }
         }
-        // phase 2: every wave's (partition, count) pairs through LDS -- the stage area is free once
-        // every entry sits in registers -- then each entry's rank among ALL entries of its partition
-        // (the counts of the same partition in lower waves first); a chunk with more than 4
-        // partitions (not on sorted uniform ids) sends the block to per-entry atomics
-        uint32_t* tab = reinterpret_cast<uint32_t*>(stage);   // [16 waves][4] keys, then [16][4] counts, flag
-        sync_lds();
-        if (lane < 4) {
-            tab[w * 4 + lane] = lane < nt ? tk[lane] : DHT_NONE;
-            tab[64 + w * 4 + lane] = lane < nt ? tc[lane] : 0u;
-        }
-        if (threadIdx.x == 0) tab[128] = 0;
-        sync_lds();
-        if (spill && lane == 0) tab[128] = 1;
-        sync_lds();
-        if (tab[128]) {   // block-uniform
+        F2_STAMP(6);
+        sync_lds();   // every entry is in registers: the caller may refill the stage after this flush
+        const uint32_t set = a.nsets == 1 ? 0u : blockIdx.x % kSets, set_off = set * a.np_all + poff;
+        for (;;) {   // wave-uniform rounds of up to 4 partitions (one round on sorted uniform ids)
+            uint32_t tk[4] = {DHT_NONE, DHT_NONE, DHT_NONE, DHT_NONE}, tc[4] = {0u, 0u, 0u, 0u}, nt = 0, pend = 0;
 #pragma unroll
             for (uint32_t r = 0; r < Per; ++r) {
-                const uint32_t j = w * C + r * 64 + lane;
-                if (r * 64 < C && j < cnt) rk[r] = atomicAdd(hist + top_bits(e[r].x, a.b1), 1u);
-            }
-        } else {
-            uint32_t pre[4] = {0u, 0u, 0u, 0u};
-            for (uint32_t x = 0; x < 64; ++x) {   // (wave-uniform reads: broadcast)
-                const uint32_t kx = tab[x], cx = tab[64 + x];
-                if (kx == DHT_NONE || (x >> 2) >= w) continue;
+                const bool v = (valid >> r) & 1u;
+                const uint32_t key = v ? top_bits(e[r].x, a.b1) : DHT_NONE;
+                uint64_t act = __ballot(v);
+                while (act) {
+                    const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane((int)key, __ffsll((long long)act) - 1);
+                    const uint64_t m = __ballot(key == kk) & act;
+                    act &= ~m;
+                    uint32_t q = 4;
 #pragma unroll
-                for (uint32_t q = 0; q < 4; ++q) pre[q] += (q < nt && tk[q] == kx) ? cx : 0u;
-            }
-            if (threadIdx.x < 64 && tab[threadIdx.x] != DHT_NONE) atomicAdd(hist + tab[threadIdx.x], tab[64 + threadIdx.x]);
-#pragma unroll
-            for (uint32_t r = 0; r < Per; ++r) {
-                const uint32_t j = w * C + r * 64 + lane;
-                if (r * 64 < C && j < cnt) {
-                    const uint32_t q = rk[r] >> 28;
-                    rk[r] = (rk[r] & 0x0FFFFFFFu) + (q == 0 ? pre[0] : q == 1 ? pre[1] : q == 2 ? pre[2] : pre[3]);
+                    for (uint32_t x = 0; x < 4; ++x) q = (x < nt && tk[x] == kk) ? x : q;
+                    if (q == 4 && nt < 4) { q = nt++; tk[q] = kk; }
+                    if (q == 4) continue;   // a fifth partition: the next round
+                    if ((m >> lane) & 1ull) {
+                        rk[r] = (tc[q] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))) | (q << 28);
+                        pend |= 1u << r;
+                    }
+                    tc[q] += (uint32_t)__popcll(m);
                 }
             }
+            if (nt == 0) break;
+            uint32_t res = 0;
+            if (lane < nt) {
+                const uint32_t kq = lane == 0 ? tk[0] : lane == 1 ? tk[1] : lane == 2 ? tk[2] : tk[3];
+                const uint32_t cq = lane == 0 ? tc[0] : lane == 1 ? tc[1] : lane == 2 ? tc[2] : tc[3];
+                res = atomicAdd(a.pcount + set_off + kq, cq);
+            }
+            const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)res, 0), b1 = (uint32_t)__builtin_amdgcn_readlane((int)res, 1);
+            const uint32_t b2 = (uint32_t)__builtin_amdgcn_readlane((int)res, 2), b3 = (uint32_t)__builtin_amdgcn_readlane((int)res, 3);
+#pragma unroll
+            for (uint32_t r = 0; r < Per; ++r) {
+                if (!((pend >> r) & 1u)) continue;
+                const uint32_t q = rk[r] >> 28;
+                const uint32_t pos = (q == 0 ? b0 : q == 1 ? b1 : q == 2 ? b2 : b3) + (rk[r] & 0x0FFFFFFFu);
+                const uint32_t p = q == 0 ? tk[0] : q == 1 ? tk[1] : q == 2 ? tk[2] : tk[3];
+                if (pos < a.pcap) a.pbuf[(uint64_t)((poff + p) * a.nsets + set) * a.pcap + pos] = e[r];
+            }
+            valid &= ~pend;
+        }
+        F2_STAMP(7);
+        return;
+    }
+    for (uint32_t i = threadIdx.x; i <= np; i += kF2Threads) hist[i] = 0;
+    sync_lds();
+#pragma unroll
+    for (uint32_t r = 0; r < Per; ++r) {
+        const uint32_t j = r * kF2Threads + threadIdx.x;
+        if (j < cnt) {
+            e[r] = stage_get<Fmt>(stage, a.stage, ibase, j, pk);
+            rk[r] = atomicAdd(hist + top_bits(e[r].x, a.b1), 1u);
         }
     }
     sync_lds();
@@ -405,11 +397,7 @@ __device__ void f2_flush(const F2Args& a, uint32_t cnt, uint2* stage, uint32_t* 
     if (threadIdx.x == 0) hist[np] = cnt;
 #pragma unroll
     for (uint32_t r = 0; r < Per; ++r) {
-        uint32_t j = r * kF2Threads + threadIdx.x;
-        if (Agg) {
-            const uint32_t C = (cnt + kF2Threads - 1) / kF2Threads * 64;
-            j = r * 64 < C ? (threadIdx.x >> 6) * C + r * 64 + lane : cnt;
-        }
+        const uint32_t j = r * kF2Threads + threadIdx.x;
         if (j < cnt) stage_put<Fmt>(stage, a.stage, ibase, hist[top_bits(e[r].x, a.b1)] + rk[r], e[r].x, e[r].y, pk);
     }
     // wsum is free again: reuse the stage-local starts to turn reservations into deltas
@@ -1861,6 +1849,17 @@ void print_phase_profile(const BatchPlan& P, uint32_t nblk2, uint32_t np, unsign
             for (uint32_t b = 0; b < nblk2; ++b)
                 if (h[b * 16 + 5]) d.push_back((double)(h[b * 16 + i] - h[b * 16 + i - 1]) / 100.0);
             if (!d.empty()) fprintf(stderr, "  F2 %-20s %s\n", nm[i], pct2(d).c_str());
+        }
+        {   // window flushes (the last one's sub-phases): ranks in registers, table, offsets; spill flag
+            const char* nw[] = {"win load", "win reserve+write"};
+            const int from[] = {2, 6}, to[] = {6, 7};
+            for (int i = 0; i < 2; ++i) {
+                std::vector<double> d;
+                for (uint32_t b = 0; b < nblk2; ++b)
+                    if (h[b * 16 + 5] && h[b * 16 + to[i]] > h[b * 16 + from[i]])
+                        d.push_back((double)(h[b * 16 + to[i]] - h[b * 16 + from[i]]) / 100.0);
+                if (!d.empty()) fprintf(stderr, "  F2 %-20s %s\n", nw[i], pct2(d).c_str());
+            }
         }
         std::vector<double> st, en;
         for (uint32_t b = 0; b < nblk2; ++b)

@@ -9,3 +9,7 @@ for r in broadcast prefix; do
   timeout -k 10 300 python tools/batch_probe.py --reps 20 --inflight 2 --cfg3 $r > $OUT/$r.log 2>&1 || { tail -5 $OUT/$r.log; exit 1; }
   echo "$r: $(grep -h 'ms/call' $OUT/$r.log) | $(grep -h phases $OUT/$r.log)"
 done
+if [ -n "$STAMPS" ]; then
+  timeout -k 10 300 env DHTGPU_DBG=256 python tools/batch_probe.py --reps 2 --cfg3 prefix > $OUT/stamps_prefix.log 2>&1 || { tail -5 $OUT/stamps_prefix.log; exit 1; }
+  grep -E "F2 " $OUT/stamps_prefix.log | tail -7
+fi
