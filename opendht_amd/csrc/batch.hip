@@ -2308,17 +2308,13 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
             uint32_t nbw = deal_f2_blocks(Pw, subs, nsub, c.q_plan, c.num_cus, hw, &segw);
             bool segd = false;
             for (uint32_t i = 0; i < nsub; ++i) segd = segd || (hw[i].nblk && hw[i].per_blk > segw);
-            // The segmented 8-B stage, sized so that two F3 workgroups (of this call's plan: the
-            // other call in flight) fit beside F2 on its CU: F2 holding every CU's LDS had F3 / F4
-            // overlap the next call's F2 only at its edges (the cfg-3 shard's period was F1 + F2 +
-            // F3 + F4); its flushes are the window's cheap direct writes.  Also when the ranges
-            // pass one packed stage-full.
-            const size_t fx = (size_t)f2_fixed_words(ww, 1u << Pw.b1) * 4;
-            const size_t l3w = (f3_lds(Pw, Pw.f3cap_wide) + 1023) & ~(size_t)1023;
-            const size_t room2 = kLdsMax > fx + 2 * l3w + 1024 ? (kLdsMax - fx - 2 * l3w - 1024) / 8 : 0;
-            if (Pw.sparse && (segd || room2 >= 4096)) {
-                const size_t room8 = fx < kLdsMax ? (kLdsMax - fx) / 8 : 0;
-                Pw.stage = (uint32_t)std::min<size_t>(room2 >= 4096 ? room2 : room8, kStage);
+            // ranges past one packed stage-full: 8-B segments (kStagePer entries in registers) in the
+            // LDS the window leaves.  (Sizing the segmented stage so that two F3 workgroups of the
+            // other call in flight fit beside F2 measured equal at the cfg-3 prefix rank, 0.148 ms
+            // both, and slower at the broadcast rank, 0.558 -> 0.593 ms: profiles/r06/window_ab.txt)
+            if (Pw.sparse && segd) {
+                const size_t fx = (size_t)f2_fixed_words(ww, 1u << Pw.b1) * 4;
+                Pw.stage = (uint32_t)std::min<size_t>(fx < kLdsMax ? (kLdsMax - fx) / 8 : 0, kStage);
                 Pw.wpack = false;
                 nbw = deal_f2_blocks(Pw, subs, nsub, c.q_plan, c.num_cus, hw, &segw);
             }
