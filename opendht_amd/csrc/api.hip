@@ -874,6 +874,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
     bc.q_plan = q_plan;
     bc.k = k;
     bc.skip = P;
+    bc.pval = c->shard_pval;
     bc.cells = c->cells.as<uint8_t>();
     bc.spans = c->spans.empty() ? nullptr : c->spans.data();
     bc.gidx = global ? c->gidx.as<uint32_t>() : nullptr;
@@ -996,6 +997,7 @@ static int batch_run(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q,
     bc.q_plan = q;
     bc.k = k;
     bc.skip = c->shard_pbits;
+    bc.pval = c->shard_pval;
     bc.w0s = c->shard_pbits ? c->w0s.as<uint32_t>() : nullptr;
     bc.gidx = out_rec ? nullptr : gidx;
     bc.base = out_rec ? 0u : idx_base;

@@ -729,6 +729,10 @@ struct RecOut {
     const uint32_t* gidx;     // context-local -> global index (nullable) ...
     uint32_t base;            // ... or offset
     uint32_t w0_direct;       // the F3 stage holds unshifted word 0 (one set, no shard shift)
+    // else F3's fast path rebuilds word 0 from the stage's shifted word: every id of the set (of a
+    // sub-partition: w0_pre | its index) shares its top w0_shift bits (no plane read per result: at
+    // the cfg-3 broadcast rank the results touch every line of the planes they are read from)
+    uint32_t w0_shift, w0_pre;
 };
 
 // place r of target qi's records: the id at index x of the writer's set (a.planes: the context's,
@@ -1211,7 +1215,10 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                         // dependent ones (the map first, then the context's planes)
 #pragma unroll
                         for (int r = 0; r < K; ++r) {
-                            if (!a.rec.w0_direct) w0[r] = a.planes[res[r]];
+                            if (!a.rec.w0_direct)
+                                w0[r] = a.rec.w0_shift ? ((a.rec.w0_pre | (Subs ? sub : 0u)) << (32 - a.rec.w0_shift)) |
+                                                             (w0[r] >> a.rec.w0_shift)
+                                                       : a.planes[res[r]];
                             w1[r] = a.planes[a.stride + res[r]];
                             res[r] = map_out(res[r], a.gidx, a.base);   // context-local
                         }
@@ -2426,7 +2433,8 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
              c.n, c.tp, c.ts, k, c.gidx, c.base, c.out_idx, c.out_cnt, ctr, fb_list, fb_sub, pstat, tie_hdr, tie_cand, tie_cnt,
              d_desc, np, dbg, stamps, narrow ? P.f3cap : P.f3cap_wide, RecOut{}, P.Lm - P.sib, P.nsets};
     if (c.out_rec)
-        a.rec = RecOut{c.out_rec, c.planes, c.stride, c.rec_gidx, c.rec_base, (nsub == 1 && !c.w0s && !c.skip) ? 1u : 0u};
+        a.rec = RecOut{c.out_rec, c.planes, c.stride, c.rec_gidx, c.rec_base, (nsub == 1 && !c.w0s && !c.skip) ? 1u : 0u,
+                       c.skip && c.skip < 32 ? c.skip : 0u, c.nsub ? c.pval << c.sub_bits : c.pval};
 
     // F3 stages the plan's 6-sigma bound beside F2's narrow stage (which it makes room for), and on
     // sub-partitioned calls whose partitions run in several rounds of workgroups when that lets 5 or

@@ -175,6 +175,8 @@ struct BatchCall {
     uint32_t sub_shift, sub_bits;          // a target's sub-partition: its bits [sub_shift, +sub_bits)
     uint64_t* desc_sig;                    // the workspace's uploaded sub-partition descriptors (signature)
     uint32_t skip; const uint32_t* w0s;    // w0s = 32 id bits from bit `skip` (every id shares its top skip bits)
+    uint32_t pval;                         // skip > 0: the shared top bits' value (of the shard; sub-partitions
+                                           // append their index: sub_bits more)
     const uint8_t* cells;                  // nullable: [nsub][1 << cell_level()] cell counts of the sub-partitions
     const uint32_t* spans;                 // nullable, HOST: [nsub][32] cell spans of the (prefix-sorted) sub-partitions
     const uint32_t* gidx; uint32_t base;   // result index map (nullable) or offset
