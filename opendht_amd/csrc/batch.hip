@@ -1653,24 +1653,25 @@ double poisson_below(double m, uint32_t k) {
     return sum;
 }
 
-BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bool cells, uint32_t wwords);
+BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t pf, uint32_t wwords);
 
-// plan_batch is a pure function of (n, q, k, CUs, cells, window), asked three times per call
+// plan_batch is a pure function of (n, q, k, CUs, plan flags, window), asked three times per call
 // (workspace size, clean head, the launch): the last few plans are kept per host thread
-BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus, bool cells = false, uint32_t wwords = 0) {
-    struct Entry { uint64_t n; uint32_t q, k; int cus; bool cells; uint32_t ww; BatchPlan P; bool used; };
+BatchPlan plan_batch(uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t pf = 0, uint32_t wwords = 0) {
+    struct Entry { uint64_t n; uint32_t q, k; int cus; uint32_t pf; uint32_t ww; BatchPlan P; bool used; };
     thread_local Entry cache[6] = {};
     thread_local uint32_t next = 0;
     for (const Entry& e : cache)
-        if (e.used && e.n == n && e.q == q && e.k == k && e.cus == num_cus && e.cells == cells && e.ww == wwords)
+        if (e.used && e.n == n && e.q == q && e.k == k && e.cus == num_cus && e.pf == pf && e.ww == wwords)
             return e.P;
     Entry& e = cache[next++ % 6u];
-    e = Entry{n, q, k, num_cus, cells, wwords, plan_batch_compute(n, q, k, num_cus, cells, wwords), true};
+    e = Entry{n, q, k, num_cus, pf, wwords, plan_batch_compute(n, q, k, num_cus, pf, wwords), true};
     return e.P;
 }
 
-BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bool cells, uint32_t wwords) {
+BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t pf, uint32_t wwords) {
     BatchPlan P;
+    const bool cells = (pf & kPlanCells) != 0, sorted = (pf & kPlanSorted) != 0;
     P.wwords = wwords;
     // mark level: 4k or more ids per level-Lm subtree -- or one level finer (2k..4k) when, on
     // uniform ids, fewer than 0.01 of the q targets are expected to land in a subtree with
@@ -1722,8 +1723,8 @@ BatchPlan plan_batch_compute(uint64_t n, uint32_t q, uint32_t k, int num_cus, bo
     // narrow prefix range, so a partition's survivors come from one or two workgroups -- one
     // bucket set, sized for the whole partition (with 8 sets planned for an eighth each, every
     // partition overflowed its set)
-    P.nsets = cells ? 1u : kSets;
-    P.clump = cells ? (1.0 - f) * (double)n / (double)(1ull << P.Lm) + 1.0 : 1.0 - f;
+    P.nsets = sorted ? 1u : kSets;
+    P.clump = sorted ? (1.0 - f) * (double)n / (double)(1ull << P.Lm) + 1.0 : 1.0 - f;
     {   // a set holds each id with probability 1 / kSets (ids are spread over the blocks by
         // index, independently of their prefix): mean + 8 sigma + 64 of one set's share
         const double sub = (double)(1ull << (P.Lm - b1)), mu = (double)n / (double)(1ull << P.Lm) / P.nsets;
@@ -2074,9 +2075,9 @@ uint32_t deal_f2_blocks(const BatchPlan& P, const SubSpec* subs, uint32_t nsub, 
 
 }  // namespace
 
-bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t nsub, bool cells) {
+bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t nsub, uint32_t pf) {
     if (k == 0 || k > DHTGPU_MAX_K_DEV || n >= (1ull << 31) || nsub == 0 || nsub > kMaxSubs) return false;
-    const BatchPlan P = plan_batch(n, q, k, num_cus, cells);
+    const BatchPlan P = plan_batch(n, q, k, num_cus, pf);
     if ((uint64_t)q * nsub > kMaxQ) return false;
     if (((uint64_t)nsub << P.b1) > kMaxParts) return false;
     // dense mode flushes whenever less than one sub-step of room is left
@@ -2084,17 +2085,17 @@ bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t n
     return f3_lds(P, P.f3cap_wide) <= kLdsMax && f2_lds(P) <= kLdsMax;
 }
 
-size_t batch_clean_bytes(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub, bool cells) {
-    return ws_layout(plan_batch(n, q_plan, k, num_cus, cells), nsub, 0, k).clean;
+size_t batch_clean_bytes(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub, uint32_t pf) {
+    return ws_layout(plan_batch(n, q_plan, k, num_cus, pf), nsub, 0, k).clean;
 }
 
-size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub, bool cells) {
-    return ws_layout(plan_batch(n, q_plan, k, num_cus, cells), nsub, q, k).total;
+size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub, uint32_t pf) {
+    return ws_layout(plan_batch(n, q_plan, k, num_cus, pf), nsub, q, k).total;
 }
 
 hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus,
-                            uint32_t* stats4, hipStream_t s, uint32_t nsub, bool cells) {
-    const BatchPlan P = plan_batch(n, q_plan, k, num_cus, cells);
+                            uint32_t* stats4, hipStream_t s, uint32_t nsub, uint32_t pf) {
+    const BatchPlan P = plan_batch(n, q_plan, k, num_cus, pf);
     const WsLayout Ly = ws_layout(P, nsub, q, k);
     const size_t NP = (size_t)nsub << P.b1;
     const uint8_t* w = static_cast<const uint8_t*>(ws);
@@ -2262,7 +2263,8 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
         n_all += subs[i].n;
     }
     const bool nt = 4 * n_all > kNtBytes;   // F2's ring: non-temporal past the Infinity Cache
-    BatchPlan P = plan_batch(n_max, c.q_plan, k, c.num_cus, c.cells != nullptr);
+    const uint32_t pf = (c.cells ? kPlanCells : 0u) | (c.sorted ? kPlanSorted : 0u);
+    BatchPlan P = plan_batch(n_max, c.q_plan, k, c.num_cus, pf);
     const uint32_t np = 1u << P.b1, NP = nsub * np;
     uint32_t dbg = c.dbg & 256u;   // the only diagnostics bit: phase stamps (results unchanged)
     hipEvent_t* ev = c.ev;
@@ -2294,7 +2296,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
     // window mode (prefix-sorted sub-partitions with span tables): every workgroup's bitmap window
     // is bounded by its sub-partition's largest cell span over as many consecutive ids as the
     // workgroup holds; taken when that bound is small (the cfg-3 shard: ~520 words of 16,384)
-    if (c.spans && nsub > 1 && P.sparse && P.Lm >= 6 && P.Lm <= kMaxLm) {
+    if (c.spans && c.sorted && nsub > 1 && P.sparse && P.Lm >= 6 && P.Lm <= kMaxLm) {
         auto need = [&](const SubDesc* dd) {
             uint32_t w = 0;
             for (uint32_t i = 0; i < nsub; ++i) {
@@ -2309,7 +2311,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
         uint32_t ww = 64;
         while (ww < need(hd)) ww <<= 1;
         if (ww <= 2 * kF2Threads && 2 * ww <= P.nwords) {
-            BatchPlan Pw = plan_batch(n_max, c.q_plan, k, c.num_cus, c.cells != nullptr, ww);
+            BatchPlan Pw = plan_batch(n_max, c.q_plan, k, c.num_cus, pf, ww);
             SubDesc hw[kMaxSubs];
             uint32_t segw = 0;
             uint32_t nbw = deal_f2_blocks(Pw, subs, nsub, c.q_plan, c.num_cus, hw, &segw);

@@ -119,16 +119,19 @@ hipError_t launch_index_query(const void* ws, uint64_t n, uint32_t B, const uint
 // batch.hip: K6 per-batch target-prefix filter + exact top-k (no persistent index).
 // n: ids of the largest sub-partition (or of the set); q_plan: the targets one sub-partition
 // is planned for (q / nsub); nsub: sub-partitions served by the call (1: the set itself).
-bool batch_supported(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1, bool cells = false);
-size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1, bool cells = false);
+bool batch_supported(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1, uint32_t pf = 0);
+size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1, uint32_t pf = 0);
 // leading workspace bytes that must be zero before a call (the call leaves them zero)
-size_t batch_clean_bytes(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1, bool cells = false);
+size_t batch_clean_bytes(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1, uint32_t pf = 0);
 // stats4 = {fallback targets, survivors, wave-path targets, 0} of the last call on workspace ws
 // (synchronises s)
 hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus,
-                            uint32_t* stats4, hipStream_t s, uint32_t nsub = 1, bool cells = false);
-// cells: the sub-partitions' level-cell_level() id counts (launch_cell_counts) are available, which
-// lets the plan mark one level finer with sibling marking (BatchCall::cells)
+                            uint32_t* stats4, hipStream_t s, uint32_t nsub = 1, uint32_t pf = 0);
+// pf (plan flags): kPlanCells -- the sub-partitions' level-cell_level() id counts (launch_cell_counts)
+// are available, which lets the plan mark one level finer with sibling marking (BatchCall::cells);
+// kPlanSorted -- the sub-partitions are sorted by prefix (one bucket set per partition, survivors
+// of an F2 range clustered in whole cells; BatchCall::sorted)
+constexpr uint32_t kPlanCells = 1u, kPlanSorted = 2u;
 uint32_t cell_level();
 // u8 counts (saturated) of the n ids of a shifted word-0 plane per top-cell_level()-bit prefix;
 // scratch: 4 << cell_level() bytes
@@ -179,6 +182,7 @@ struct BatchCall {
                                            // append their index: sub_bits more)
     const uint8_t* cells;                  // nullable: [nsub][1 << cell_level()] cell counts of the sub-partitions
     const uint32_t* spans;                 // nullable, HOST: [nsub][32] cell spans of the (prefix-sorted) sub-partitions
+    uint32_t sorted;                       // the sub-partitions are sorted by prefix (spans then bound F2's windows)
     const uint32_t* gidx; uint32_t base;   // result index map (nullable) or offset
     uint32_t* out_idx; uint32_t* out_cnt;  // rows of the ORIGINAL target indices
     // record form (nullable): every writer of a result row (F3, the wave paths, F4's scan and

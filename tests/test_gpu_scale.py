@@ -204,15 +204,18 @@ def test_subpartition_deficient_subtree_targets(ctx):
     assert np.array_equal(got[picks], want) and np.array_equal(cnt[picks], wcnt)
 
 
-def test_subpartition_sibling_marking(ctx):
+@pytest.mark.parametrize("q", [65536, 262144])
+def test_subpartition_sibling_marking(ctx, q):
     """Sibling marking (round 6): 31.25 M ids = 2 prefix sub-partitions of ~1.56e7 with 65,536
     targets plan one level finer than the 4k rule (level-19 cells of ~30 ids) because the
     sub-partitions carry their level-19 cell counts: a target whose own cell holds < k ids marks the
     sibling cell too and answers from the complete pair.  Crafted: 48 targets' cells emptied down
     to 3 ids (moved into the sibling: the pair keeps them all), 16 targets' whole pairs emptied
     down to 2 + 2 ids (the pair is short: F3's fallback scan of the sub-partition).  Whole batch
-    == K1 scan; the crafted targets and a sample == std::partial_sort(xorCmp)."""
-    n, q, k = 31_250_000, 65536, 8
+    == K1 scan; the crafted targets and a sample == std::partial_sort(xorCmp).  q = 262,144: the
+    survivors are dense (~22 %), so the sub-partitions are built prefix-sorted and F2 runs its
+    bitmap window (the cfg-3 broadcast rank's route)."""
+    n, k = 31_250_000, 8
     ids = O.gen_ids(3434, n)
     tg = O.gen_ids(3435, q)
     key = lambda a: ((a[:, 0].astype(np.uint32) << 12) | (a[:, 1].astype(np.uint32) << 4) | (a[:, 2] >> 4))
