@@ -218,6 +218,135 @@ __global__ __launch_bounds__(kF1Threads) void k_f1_targets(F1Args a) {
     a.tspill[base + (uint32_t)__popcll(sp & ((1ull << lane) - 1ull))] = i;
 }
 
+// ---- F1 for large batches: the same marks and buckets with no per-target global atomic --------
+// k_f1_targets costs two memory-side atomics per target on distinct lines (bitmap OR, bucket
+// counter): at 2^20 targets that is 2.1 M atomic requests, 95 us at the chip's atomic rate
+// (DESIGN 5d).  Large batches take two passes instead:
+//   F1a k_f1_coarse  groups the targets by a coarse bin = (sub-partition, top c bits): an LDS
+//                    histogram per workgroup of 4,096 targets, ONE returning global atomic per
+//                    (workgroup, bin) reserving the workgroup's run in the bin's bucket cbuf[bin];
+//   F1b k_f1_fine    one workgroup per bin owns the bin's bitmap words and its 2^(b1 - c)
+//                    partitions outright: it marks the bitmap in LDS (sibling marks as F1) and
+//                    ranks the targets per partition with LDS atomics, stores each target at
+//                    tbuf[p][rank], then writes its bitmap words and partition counts with plain
+//                    stores (every word and count of the bin, zeros included).
+// A bin or bucket past its capacity spills the target to the F4 fallback list, as F1 does.
+constexpr uint32_t kF1aThreads = 1024, kF1aPer = 4, kF1aTargets = kF1aThreads * kF1aPer;
+constexpr uint32_t kF1bThreads = 1024, kF1bPer = 4;
+constexpr uint32_t kMaxCoarse = 4096;             // bins (the coarse counters live in the clean head)
+constexpr uint32_t kF1bLdsWords = 16384;          // F1b's bitmap words + partition counts (64 KB)
+constexpr uint32_t kF1CoarseMinQ = 1u << 18;      // smaller batches: k_f1_targets (at 2^17: 14.2 vs 13.5 us)
+
+struct F1cArgs {
+    const uint32_t* tw0; const uint32_t* tw1;
+    uint32_t q, shift, sub_shift, sub_bits;
+    uint32_t c, ccap;                  // coarse bin = sub << c | top c bits; bin bucket capacity
+    uint32_t* ccount; uint2* cbuf;     // [nbins] (all-zero between calls: F1b resets), [nbins][ccap]
+    uint32_t Lm, b1, np, nwords;
+    uint32_t* bitmap;
+    uint32_t* tcount; uint2* tbuf; uint32_t tcap;
+    uint32_t* ctr; uint32_t* tspill;
+    const uint8_t* cells; uint32_t k;
+};
+
+// the lanes with `sp` set append `val` to the spill list (one atomic per wave)
+__device__ __forceinline__ void f1_spill(bool sp, uint32_t val, uint32_t* ctr, uint32_t* tspill) {
+    const uint64_t m = __ballot(sp);
+    if (!m) return;
+    const uint32_t lane = lane_id(), lead = (uint32_t)__ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(ctr + kSpill, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, (int)lead);
+    if (sp) tspill[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = val;
+}
+
+__global__ __launch_bounds__(kF1aThreads) void k_f1_coarse(F1cArgs a) {
+    __shared__ uint32_t hist[kMaxCoarse];
+    const uint32_t nbins = (1u << a.sub_bits) << a.c;
+    if (blockIdx.x == 0 && threadIdx.x < 4) a.ctr[threadIdx.x] = 0;   // fallback, survivors, wave path, -
+    for (uint32_t b = threadIdx.x; b < nbins; b += kF1aThreads) hist[b] = 0;
+    __syncthreads();
+    const uint32_t i0 = blockIdx.x * kF1aTargets + threadIdx.x;
+    uint32_t v[kF1aPer], bin[kF1aPer], r[kF1aPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kF1aPer; ++u) {
+        const uint32_t i = i0 + u * kF1aThreads;
+        if (i < a.q) {
+            const uint32_t w = a.tw0[i];
+            const uint32_t sub = a.sub_bits ? (w << a.sub_shift) >> (32 - a.sub_bits) : 0u;
+            v[u] = a.shift ? (w << a.shift) | (a.tw1[i] >> (32 - a.shift)) : w;
+            bin[u] = (sub << a.c) | top_bits(v[u], a.c);
+            r[u] = atomicAdd(hist + bin[u], 1u);
+        }
+    }
+    __syncthreads();
+    // one reservation per (workgroup, bin): consecutive lanes on consecutive counters
+    for (uint32_t b = threadIdx.x; b < nbins; b += kF1aThreads) {
+        const uint32_t h = hist[b];
+        if (h) hist[b] = atomicAdd(a.ccount + b, h);
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < kF1aPer; ++u) {
+        const uint32_t i = i0 + u * kF1aThreads;
+        const uint32_t pos = i < a.q ? hist[bin[u]] + r[u] : 0u;
+        if (i < a.q && pos < a.ccap) a.cbuf[(uint64_t)bin[u] * a.ccap + pos] = make_uint2(v[u], i);
+        f1_spill(i < a.q && pos >= a.ccap, i, a.ctr, a.tspill);
+    }
+}
+
+__global__ __launch_bounds__(kF1bThreads) void k_f1_fine(F1cArgs a) {
+    extern __shared__ uint32_t sh1[];
+    const uint32_t b = blockIdx.x, sub = b >> a.c, hi = b & ((1u << a.c) - 1u);
+    const uint32_t lw = a.Lm - a.c - 5, nw = 1u << lw;          // the bin's bitmap words
+    const uint32_t lp = a.b1 - a.c, nps = 1u << lp;             // the bin's partitions
+    uint32_t* bm = sh1;
+    uint32_t* fc = sh1 + nw;
+    for (uint32_t j = threadIdx.x; j < nw + nps; j += kF1bThreads) sh1[j] = 0;
+    const uint32_t m0 = a.ccount[b];
+    __syncthreads();   // (every thread has read the count)
+    if (threadIdx.x == 0) a.ccount[b] = 0;   // all-zero again for the next call
+    const uint32_t m = m0 < a.ccap ? m0 : a.ccap;
+    const uint32_t pbase = sub * a.np + (hi << lp);
+    const uint2* src = a.cbuf + (uint64_t)b * a.ccap;
+    const uint8_t* cells = a.cells ? a.cells + ((uint64_t)sub << a.Lm) : nullptr;
+    // kF1bPer entries per thread loaded at once (one round trip per kF1bPer * kF1bThreads entries:
+    // a loop of one load per thread at a time made F1 34 us at 2^20 targets)
+    for (uint32_t j0 = 0; j0 < m; j0 += kF1bPer * kF1bThreads) {   // block-uniform
+        uint2 e[kF1bPer];
+        uint8_t cl[kF1bPer];
+#pragma unroll
+        for (uint32_t u = 0; u < kF1bPer; ++u) {
+            const uint32_t j = j0 + u * kF1bThreads + threadIdx.x;
+            e[u] = j < m ? src[j] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kF1bPer; ++u) {
+            const uint32_t j = j0 + u * kF1bThreads + threadIdx.x;
+            cl[u] = (cells && j < m) ? cells[top_bits(e[u].x, a.Lm)] : (uint8_t)255;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kF1bPer; ++u) {
+            const uint32_t j = j0 + u * kF1bThreads + threadIdx.x;
+            bool sp = false;
+            if (j < m) {
+                const uint32_t pre = top_bits(e[u].x, a.Lm);
+                const bool sib = cl[u] < a.k;
+                atomicOr(bm + ((pre >> 5) & (nw - 1u)), (1u << (pre & 31)) | (sib ? 1u << ((pre ^ 1u) & 31) : 0u));
+                const uint32_t pl = top_bits(e[u].x, a.b1) & (nps - 1u);
+                const uint32_t rk = atomicAdd(fc + pl, 1u);
+                if (rk < a.tcap) a.tbuf[(uint64_t)(pbase + pl) * a.tcap + rk] = e[u];
+                else sp = true;
+            }
+            f1_spill(sp, e[u].y, a.ctr, a.tspill);
+        }
+    }
+    __syncthreads();
+    uint32_t* gbm = a.bitmap + (uint64_t)sub * a.nwords + ((uint64_t)hi << lw);
+    for (uint32_t j = threadIdx.x; j < nw; j += kF1bThreads) gbm[j] = bm[j];
+    for (uint32_t j = threadIdx.x; j < nps; j += kF1bThreads) a.tcount[(uint64_t)(pbase + j) * kCtrStride] = fc[j];
+}
+
 // ---- F2: stream w0, keep ids in marked subtrees, partition them ----------------------
 // Persistent: one workgroup per CU, each owning a contiguous id range streamed through
 // a ring of kF2Ring 16-B loads per lane (32 KB in flight per CU).  Survivors are appended
@@ -670,6 +799,136 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_filter(F2Args a) {
             }
         }
     }
+    F2_STAMP(5);
+}
+
+// ---- F2 direct (prefix-sorted sub-partitions): no stage, no flush ------------------------
+// Over sorted sub-partitions a workgroup's contiguous id range is a contiguous run of partitions,
+// and every partition strictly inside the range belongs to this workgroup alone.  So each wave
+// writes its survivors straight to their partition's bucket: per sub-step it ranks its survivors
+// (ballot + mbcnt; the 256 ids of a wave's sub-step are consecutive in sorted order, so they meet
+// one partition, rarely two) and reserves the run with ONE LDS atomic on the partition's counter
+// -- a returning global atomic only for the range's first and last partitions when a neighbouring
+// workgroup shares them.  At the end the owned partitions' counts are stored plainly.  The LDS
+// holds the bitmap window and the counters only (a few KB, where the staged forms filled the CU's
+// 160 KB), so F3 workgroups of another call in flight fit beside it, and the stream never stops
+// for a flush (the segmented window stage flushed ~6 times per workgroup at the cfg-3 broadcast
+// rank).  A partition past its bucket capacity keeps counting (F3 sends its targets to the
+// fallback), as in the staged forms.
+constexpr uint32_t kDirParts = 4096;   // LDS counters: partitions a range may own (more: global atomics)
+
+template <uint32_t Src>
+__global__ __launch_bounds__(kF2Threads) void k_f2_direct(F2Args a) {
+    constexpr bool NT = Src == kF2SubsNT;
+    extern __shared__ uint32_t sh[];   // misc[8] | bm[wwords] | cnt[kDirParts]
+    uint32_t* misc = sh;
+    uint32_t* bm = sh + 8;
+    uint32_t* cnt = bm + a.wwords;
+    const uint32_t sub = (uint32_t)a.blk_sub[blockIdx.x];
+    const SubDesc d = a.subs[sub];
+    const uint64_t lo64 = (uint64_t)(blockIdx.x - d.blk0) * d.per_blk;
+    if (lo64 >= d.n) return;
+    F2_STAMP(0);
+    const uint32_t* const w0 = d.w0;
+    const uint32_t np = 1u << a.b1, poff = sub * np;
+    const uint32_t lo = (uint32_t)lo64;
+    const uint32_t hi = (uint32_t)(lo64 + d.per_blk < d.n ? lo64 + d.per_blk : d.n);
+    const uint32_t lane = lane_id();
+    const uint32_t pre_off = 32 - a.Lm;
+    const uint32_t lm5 = a.Lm > 5 ? a.Lm - 5 : 0u;
+    const uint32_t tid4 = 4 * threadIdx.x;
+    const uint32_t lim = min(d.lim, ((hi + 3u) & ~3u) - 4u);
+    const __amdgpu_buffer_rsrc_t rs = f2_rsrc(w0, lo, lim);
+    // the range's first and last words (sorted: its smallest and largest prefixes) and their
+    // neighbours outside the range, in one round trip: the bitmap window's base and the partitions
+    // a neighbouring workgroup shares
+    const uint32_t f0 = __builtin_amdgcn_readfirstlane(w0[lo]);
+    const uint32_t fl = __builtin_amdgcn_readfirstlane(w0[hi - 1]);
+    const uint32_t fp = lo > 0 ? __builtin_amdgcn_readfirstlane(w0[lo - 1]) : 0u;
+    const uint32_t fn = hi < d.n ? __builtin_amdgcn_readfirstlane(w0[hi]) : 0u;
+    const uint32_t wbase = a.Lm > 5 ? f0 >> (pre_off + 5) : 0u;
+    const uint32_t p_first = top_bits(f0, a.b1), p_last = top_bits(fl, a.b1);
+    const bool sh_first = lo > 0 && top_bits(fp, a.b1) == p_first;
+    const bool sh_last = hi < d.n && top_bits(fn, a.b1) == p_last;
+    const uint32_t* bsrc = a.bitmap + sub * a.nwords;
+    const uint32_t i0 = wbase + threadIdx.x, i1 = i0 + kF2Threads;
+    const uint32_t wv0 = threadIdx.x < a.wwords && i0 < a.nwords ? bsrc[i0] : 0u;
+    const uint32_t wv1 = threadIdx.x + kF2Threads < a.wwords && i1 < a.nwords ? bsrc[i1] : 0u;
+    uint4 ring[kF2Ring];
+#pragma unroll
+    for (uint32_t r = 0; r < kF2Ring; ++r) ring[r] = f2_load1<NT>(rs, lo, lo + r * kF2Sub, lim);
+    if (threadIdx.x < a.wwords) bm[threadIdx.x] = wv0;
+    if (threadIdx.x + kF2Threads < a.wwords) bm[threadIdx.x + kF2Threads] = wv1;
+    for (uint32_t i = threadIdx.x; i < kDirParts; i += kF2Threads) cnt[i] = 0;
+    sync_lds();
+    F2_STAMP(1);
+    uint32_t* const pc = a.pcount + poff;   // one bucket set (nsets == 1)
+    uint2* const pb = a.pbuf + (uint64_t)poff * a.pcap;
+    for (uint32_t c0 = lo; c0 < hi; c0 += kF2Ring * kF2Sub) {
+#pragma unroll
+        for (uint32_t r = 0; r < kF2Ring; ++r) {
+            const uint32_t sb = c0 + r * kF2Sub;
+            if (sb < hi) {   // block-uniform
+                const uint32_t j0 = sb + tid4;
+                const uint32_t v4[4] = {ring[r].x, ring[r].y, ring[r].z, ring[r].w};
+                const uint32_t rem = hi - sb;
+                uint32_t bw[4];
+#pragma unroll
+                for (uint32_t f = 0; f < 4; ++f) bw[f] = bm[__builtin_amdgcn_ubfe(v4[f], pre_off + 5, lm5) - wbase];
+                bool sv[4];
+                uint64_t bal[4], any = 0;
+#pragma unroll
+                for (uint32_t f = 0; f < 4; ++f) {
+                    const uint32_t pre = __builtin_amdgcn_ubfe(v4[f], pre_off, a.Lm);
+                    sv[f] = __builtin_amdgcn_ubfe(bw[f], pre, 1) != 0 && tid4 + f < rem;
+                    bal[f] = __builtin_amdgcn_ballot_w64(sv[f]);
+                    any |= bal[f];
+                }
+                if (any) {   // wave-uniform
+                    // the wave's survivors meet partitions [plo, phi] (ascending with the lane)
+                    const uint32_t l0 = (uint32_t)__ffsll((long long)any) - 1, l1 = 63u - (uint32_t)__clzll(any);
+                    const uint32_t mylo = sv[0] ? v4[0] : sv[1] ? v4[1] : sv[2] ? v4[2] : v4[3];
+                    const uint32_t myhi = sv[3] ? v4[3] : sv[2] ? v4[2] : sv[1] ? v4[1] : v4[0];
+                    const uint32_t plo = top_bits((uint32_t)__builtin_amdgcn_readlane((int)mylo, (int)l0), a.b1);
+                    const uint32_t phi = top_bits((uint32_t)__builtin_amdgcn_readlane((int)myhi, (int)l1), a.b1);
+                    for (uint32_t p = plo; p <= phi; ++p) {   // wave-uniform, usually one pass
+                        uint64_t bp[4];
+                        uint32_t tot = 0;
+#pragma unroll
+                        for (uint32_t f = 0; f < 4; ++f) {
+                            bp[f] = plo == phi ? bal[f] : bal[f] & __builtin_amdgcn_ballot_w64(top_bits(v4[f], a.b1) == p);
+                            tot += (uint32_t)__popcll(bp[f]);
+                        }
+                        if (!tot) continue;
+                        const uint32_t pl = p - p_first;
+                        const bool glob = (p == p_first && sh_first) || (p == p_last && sh_last) || pl >= kDirParts;
+                        uint32_t base = 0;
+                        if (lane == 0) base = glob ? atomicAdd(pc + p, tot) : atomicAdd(cnt + pl, tot);
+                        uint32_t pos = __builtin_amdgcn_readfirstlane(base);
+#pragma unroll
+                        for (uint32_t f = 0; f < 4; ++f) {
+                            if ((bp[f] >> lane) & 1ull) {
+                                const uint32_t at = __builtin_amdgcn_mbcnt_hi(
+                                    (uint32_t)(bp[f] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bp[f], pos));
+                                if (at < a.pcap) pb[(uint64_t)p * a.pcap + at] = make_uint2(v4[f], j0 + f);
+                            }
+                            pos += (uint32_t)__popcll(bp[f]);
+                        }
+                    }
+                }
+            }
+            ring[r] = f2_load1<NT>(rs, lo, sb + kF2Ring * kF2Sub, lim);
+        }
+    }
+    sync_lds();
+    F2_STAMP(2);
+    // the owned partitions' counts (shared ones were counted in place)
+    const uint32_t nown = min(p_last - p_first + 1u, kDirParts);
+    for (uint32_t i = threadIdx.x; i < nown; i += kF2Threads) {
+        const uint32_t p = p_first + i;
+        if (!((p == p_first && sh_first) || (p == p_last && sh_last))) pc[p] = cnt[i];
+    }
+    (void)misc;
     F2_STAMP(5);
 }
 
@@ -1983,9 +2242,32 @@ constexpr uint32_t kMaxF2Blocks = 65536;
 inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
 struct WsLayout {
-    size_t ctr, bitmap, pcount, tcount, tie_hdr, fb_done, tie_cnt, clean;
-    size_t fb_list, fb_sub, tspill, pstat, tbuf, tie_cand, pbuf, fb_rec, desc, blk_sub, total;
+    size_t ctr, bitmap, pcount, tcount, tie_hdr, fb_done, tie_cnt, ccount, clean;
+    size_t fb_list, fb_sub, tspill, pstat, tbuf, tie_cand, pbuf, fb_rec, desc, blk_sub, cbuf, total;
 };
+
+// F1's two-pass form (k_f1_coarse + k_f1_fine) for batches of >= kF1CoarseMinQ targets: the
+// coarse bins are the finest split (<= b1 and Lm - 5 bits per sub-partition) that keeps >= 512
+// targets per bin and >= 16 per (F1a workgroup, bin) -- each reservation a run of >= 128 B (2,048
+// bins at 2^20 targets left 2 per run: F1a 34 us, 524 K reservations) -- with F1b's LDS within
+// kF1bLdsWords.  c = ~0u: one pass.
+struct F1Coarse { uint32_t c, nbins, ccap; };
+F1Coarse f1_coarse(const BatchPlan& P, uint32_t nsub, uint32_t q) {
+    F1Coarse f{~0u, 0, 0};
+    if (q < kF1CoarseMinQ || P.Lm < 5) return f;
+    auto lds_ok = [&](uint32_t c) { return (1u << (P.Lm - c - 5)) + (1u << (P.b1 - c)) <= kF1bLdsWords; };
+    uint32_t c = 0;
+    while (c < P.b1 && c + 5 < P.Lm && ((uint64_t)nsub << (c + 1)) <= kF1aTargets / 16 &&
+           ((uint64_t)nsub << (c + 1)) * 512 <= q)
+        ++c;
+    while (c < P.b1 && c + 5 < P.Lm && !lds_ok(c)) ++c;
+    if (!lds_ok(c) || ((uint64_t)nsub << c) > kMaxCoarse) return f;
+    f.c = c;
+    f.nbins = nsub << c;
+    const double M = (double)q / (double)f.nbins;
+    f.ccap = ((uint32_t)(M + 8.0 * std::sqrt(M) + 64.0) + 63u) & ~63u;
+    return f;
+}
 
 WsLayout ws_layout(const BatchPlan& P, uint32_t nsub, uint32_t q, uint32_t k) {
     const size_t NP = (size_t)nsub << P.b1;
@@ -2006,6 +2288,7 @@ WsLayout ws_layout(const BatchPlan& P, uint32_t nsub, uint32_t q, uint32_t k) {
     L.tie_hdr = take((size_t)kMaxParts * kTieSlots * 16);
     L.fb_done = take((size_t)kFbBlocks * 4);
     L.tie_cnt = take((size_t)kMaxParts * 4);
+    L.ccount = take((size_t)kMaxCoarse * 4);
     L.clean = off;
     L.fb_list = take((size_t)q * 4);
     L.fb_sub = take((size_t)q);
@@ -2017,6 +2300,8 @@ WsLayout ws_layout(const BatchPlan& P, uint32_t nsub, uint32_t q, uint32_t k) {
     L.fb_rec = take((size_t)kFbBlocks * kFbGroup * k * 24);
     L.desc = take((size_t)kMaxSubs * sizeof(SubDesc));
     L.blk_sub = take(kMaxF2Blocks);
+    const F1Coarse fc = f1_coarse(P, nsub, q);
+    L.cbuf = take((size_t)fc.nbins * fc.ccap * 8);
     L.total = off;
     return L;
 }
@@ -2265,6 +2550,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
     const bool nt = 4 * n_all > kNtBytes;   // F2's ring: non-temporal past the Infinity Cache
     const uint32_t pf = (c.cells ? kPlanCells : 0u) | (c.sorted ? kPlanSorted : 0u);
     BatchPlan P = plan_batch(n_max, c.q_plan, k, c.num_cus, pf);
+    const BatchPlan P0 = P;   // the workspace layout's plan (window mode may refine P below)
     const uint32_t np = 1u << P.b1, NP = nsub * np;
     uint32_t dbg = c.dbg & 256u;   // the only diagnostics bit: phase stamps (results unchanged)
     hipEvent_t* ev = c.ev;
@@ -2296,7 +2582,8 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
     // window mode (prefix-sorted sub-partitions with span tables): every workgroup's bitmap window
     // is bounded by its sub-partition's largest cell span over as many consecutive ids as the
     // workgroup holds; taken when that bound is small (the cfg-3 shard: ~520 words of 16,384)
-    if (c.spans && c.sorted && nsub > 1 && P.sparse && P.Lm >= 6 && P.Lm <= kMaxLm) {
+    bool direct = false;   // k_f2_direct (sorted sub-partitions: no stage)
+    if (c.spans && c.sorted && nsub > 1 && P.Lm >= 6 && P.Lm <= kMaxLm) {
         auto need = [&](const SubDesc* dd) {
             uint32_t w = 0;
             for (uint32_t i = 0; i < nsub; ++i) {
@@ -2308,9 +2595,24 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
             }
             return w;
         };
+        if (P.nsets == 1) {   // direct: one persistent workgroup per CU (no stage bounds a range)
+            BatchPlan Pd = P;
+            Pd.sparse = 0;
+            SubDesc hw[kMaxSubs];
+            uint32_t segw = 0;
+            const uint32_t nbw = deal_f2_blocks(Pd, subs, nsub, c.q_plan, c.num_cus, hw, &segw);
+            uint32_t wd = 64;
+            while (wd < need(hw)) wd <<= 1;
+            if (wd <= 2 * kF2Threads && 2 * wd <= P.nwords && nbw <= kMaxF2Blocks) {
+                direct = true;
+                P.wwords = wd;
+                nblk2 = nbw;
+                std::copy(hw, hw + nsub, hd);
+            }
+        }
         uint32_t ww = 64;
         while (ww < need(hd)) ww <<= 1;
-        if (ww <= 2 * kF2Threads && 2 * ww <= P.nwords) {
+        if (!direct && P.sparse && ww <= 2 * kF2Threads && 2 * ww <= P.nwords) {
             BatchPlan Pw = plan_batch(n_max, c.q_plan, k, c.num_cus, pf, ww);
             SubDesc hw[kMaxSubs];
             uint32_t segw = 0;
@@ -2354,7 +2656,7 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
     if (nblk2 > kMaxF2Blocks) return hipErrorInvalidValue;
     // the narrow stage: every workgroup's range under 2^16 ids and its survivors (mean + 8 sigma
     // + 256 on uniform ids) within the narrow stage; no segments
-    bool narrow = P.nstage && P.sparse && !seg_used;
+    bool narrow = !direct && P.nstage && P.sparse && !seg_used;
     {
         const double f = 1.0 - std::exp(-(double)c.q_plan / (double)(1ull << P.Lm));
         for (uint32_t i = 0; i < nsub && narrow; ++i) {
@@ -2401,7 +2703,24 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
     if (dbg & 256) (void)hipMemsetAsync(stamps, 0, (size_t)3 * 8192 * 16 * 8, s);
     const F1Args a1{c.tp, c.tp + c.ts, q, P.Lm, P.b1, c.skip, c.sub_shift, c.nsub ? c.sub_bits : 0u, np, P.nwords,
                     bitmap, tcount, tbuf, P.tcap, ctr, tspill, P.sib ? c.cells : nullptr, k};
-    go(0, k_f1_targets, dim3((q + kF1Threads - 1) / kF1Threads), dim3(kF1Threads), 0, a1);
+    const F1Coarse f1c = f1_coarse(P0, nsub, q);
+    if (f1c.nbins && P.Lm == P0.Lm && P.b1 == P0.b1) {
+        F1cArgs ac{c.tp, c.tp + c.ts, q, c.skip, c.sub_shift, c.nsub ? c.sub_bits : 0u, f1c.c, f1c.ccap,
+                   reinterpret_cast<uint32_t*>(w + Ly.ccount), reinterpret_cast<uint2*>(w + Ly.cbuf),
+                   P.Lm, P.b1, np, P.nwords, bitmap, tcount, tbuf, P.tcap, ctr, tspill,
+                   P.sib ? c.cells : nullptr, k};
+        const dim3 ga((q + kF1aTargets - 1) / kF1aTargets), gb(f1c.nbins);
+        const size_t lb = (size_t)((1u << (P.Lm - f1c.c - 5)) + (1u << (P.b1 - f1c.c))) * 4;
+        if (ev) {   // pair 0 brackets both passes
+            hipExtLaunchKernelGGL(k_f1_coarse, ga, dim3(kF1aThreads), 0, s, ev[0], nullptr, 0, ac);
+            hipExtLaunchKernelGGL(k_f1_fine, gb, dim3(kF1bThreads), (uint32_t)lb, s, nullptr, ev[1], 0, ac);
+        } else {
+            k_f1_coarse<<<ga, dim3(kF1aThreads), 0, s>>>(ac);
+            k_f1_fine<<<gb, dim3(kF1bThreads), lb, s>>>(ac);
+        }
+    } else {
+        go(0, k_f1_targets, dim3((q + kF1Threads - 1) / kF1Threads), dim3(kF1Threads), 0, a1);
+    }
     if (nblk2) {
         F2Args a2{d_desc, d_blk, hd[0], nsub, NP, P.Lm, P.b1, bitmap, P.nwords, pcount, pbuf, P.scap, ctr,
                   narrow ? P.nstage : P.stage, dbg, P.sparse, seg, (dbg & 256) ? stamps + 8192 * 16 : stamps};
@@ -2416,8 +2735,10 @@ hipError_t launch_batch_topk(const BatchCall& c, hipStream_t s) {
         else if (nsub > 1) go(1, k_f2_filter<MM, kF2Subs>, g2, b2, l2, a2);   \
         else go(1, k_f2_filter<MM, kF2One>, g2, b2, l2, a2);                  \
     } while (0)
-        // window mode: the packed stage with one final flush (P.wpack), or 8-B segments
-        if (win && nt && !P.wpack) go(1, k_f2_filter<kF2Seg, kF2SubsNT, true>, g2, b2, l2, a2);
+        // window mode: no stage (direct), the packed stage with one final flush (P.wpack), or 8-B segments
+        if (direct && nt) go(1, k_f2_direct<kF2SubsNT>, g2, b2, (size_t)(8 + P.wwords + kDirParts) * 4, a2);
+        else if (direct) go(1, k_f2_direct<kF2Subs>, g2, b2, (size_t)(8 + P.wwords + kDirParts) * 4, a2);
+        else if (win && nt && !P.wpack) go(1, k_f2_filter<kF2Seg, kF2SubsNT, true>, g2, b2, l2, a2);
         else if (win && nt) go(1, k_f2_filter<kF2Sparse, kF2SubsNT, true>, g2, b2, l2, a2);
         else if (win && !P.wpack) go(1, k_f2_filter<kF2Seg, kF2Subs, true>, g2, b2, l2, a2);
         else if (win) go(1, k_f2_filter<kF2Sparse, kF2Subs, true>, g2, b2, l2, a2);

@@ -244,6 +244,39 @@ def test_subpartition_sibling_marking(ctx, q):
     assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
 
 
+@pytest.mark.parametrize("n,q", [(1 << 22, 1 << 18), (1 << 25, 1 << 18)])
+def test_f1_two_pass_clustered_targets(ctx, n, q):
+    """F1's two-pass form (batches of >= 2^18 targets, round 6: coarse bins by workgroup-level
+    reservations, then one workgroup per bin marking the bitmap and ranking the partitions in LDS):
+    a quarter of the targets share their top 12 bits (their coarse bin overflows: those targets
+    spill to the fallback scan from the first pass), and groups of 96, 256, 700 and 2,048 targets
+    each share a 22-bit prefix (one partition's bucket overflows in the second pass, or the bin in
+    the first, by size); one set and 2 sub-partitions.  Whole batch == K1 scan, a sample of each
+    group == std::partial_sort(xorCmp)."""
+    k = 8
+    ctx.gen_ids(3737, n)
+    tg = O.gen_ids(3738, q)
+    a = q // 4
+    tg[:a, 0] = 0xA7
+    tg[:a, 1] = (tg[:a, 1] & 0x0F) | 0x30
+    rows = [np.arange(0, a, a // 8)]
+    lo = a
+    for g, pre in zip((96, 256, 700, 2048), (0x1C44, 0x5B12, 0x9E60, 0xD301)):
+        tg[lo:lo + g, 0] = pre >> 8
+        tg[lo:lo + g, 1] = pre & 0xFF
+        tg[lo:lo + g, 2] = (tg[lo:lo + g, 2] & 0x03) | 0x98
+        rows.append(np.arange(lo, lo + g, g // 4))
+        lo += g
+    got, cnt = ctx.batch_topk(tg, k)
+    sc, scnt = ctx.topk(tg, k)
+    assert np.array_equal(cnt, scnt)
+    bad = np.nonzero((got != sc).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} targets differ from the K1 scan, first {bad[:5]}"
+    rows = np.r_[np.concatenate(rows), sample_rows(q, 8)]
+    want, wcnt = O.topk(O.gen_ids(3737, n), tg[rows], k, threads=16)
+    assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
+
+
 @pytest.mark.parametrize("k", [8, 32])
 def test_clustered_ids_fallback_scan(ctx, k):
     """Verdict item 4: 2^24 ids of which 25 % share one 24-bit prefix, and targets inside the

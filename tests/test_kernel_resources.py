@@ -19,7 +19,7 @@ FILES = ("batch.hip", "scan.hip", "table.hip")
 VGPR_CAPS = {
     "k_f2_filterI": 128,         # 109-111: 4 waves / SIMD beside its 152 KB of LDS
     "k_f3_answerILi8E": 96,      # 69-78 (the k <= 8 instantiations)
-    "k_f3_answerILi16E": 136,    # 123-136
+    "k_f3_answerILi16E": 168,    # 123-136 (r05), 141-145 with round 6's record word 0 from the stage: 3 waves / SIMD up to 168
     "k_f4I": 144,                # 139: 3 waves / SIMD
     "k_s1_filterI": 128,
     "k_s2_answerI": 144,
