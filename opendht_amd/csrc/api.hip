@@ -827,12 +827,14 @@ static int build_subs(dhtgpu_ctx* c, bool sort) {
 // (strongly clustered ids: one sub-partition far above 2^24) takes the K1 scan.
 static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32_t q, uint32_t k, uint32_t* out_idx,
                           uint32_t* out_cnt, uint32_t* out_rec, uint32_t idx_base, hipStream_t s, hipEvent_t* ev) {
-    // Prefix-sorted sub-partitions pay where survivors are dense (the cfg-3 broadcast rank: 2^20
-    // targets on 1.25e8 ids, ~22 % of the ids survive): an F2 range's survivors fall into a few
-    // partitions (direct, coalesced bucket writes; a bitmap window instead of the whole bitmap) and
-    // F3's reads stay inside narrow index windows: 1.16 -> 0.50 ms per call.  Where they are sparse
-    // (~3 %: the prefix rank, the 2^27-id shard) index order measured faster (0.152 against 0.158 ms:
-    // the survivor writes spread over two flushes).  Decided once, by the call that builds them.
+    // Prefix-sorted sub-partitions: an F2 range's survivors fall into a few partitions that the
+    // range owns, so F2 writes them straight to their buckets with no stage (k_f2_direct: a few KB
+    // of LDS, F3 workgroups of the other call in flight beside it) and F3's reads stay inside
+    // narrow index windows.  The cfg-3 broadcast rank (2^20 targets on 1.25e8 ids, ~22 % of the
+    // ids survive): 1.16 -> 0.43 ms per call; the prefix rank (~3 %): 0.149 -> 0.135 ms, the
+    // 2^27-id shard 0.157 -> 0.148-0.152 (profiles/r06/experiments).  Below ~2 % survivors a
+    // wave's runs would be one or two entries: index order.  Decided once, by the call that
+    // builds them.
     bool sort = false;
     {
         uint32_t sbe = 1;
@@ -842,7 +844,7 @@ static int batch_run_subs(dhtgpu_ctx* c, const uint32_t* tp, uint64_t ts, uint32
         uint32_t lm = 0;
         while (lm < 19 && (nsub_e >> (lm + 1)) >= 4ull * k) ++lm;
         lm = lm + 1 < 19 ? lm + 1 : 19;
-        sort = 1.0 - std::exp(-qsub / (double)(1ull << lm)) > 0.10;
+        sort = 1.0 - std::exp(-qsub / (double)(1ull << lm)) > 0.02;
     }
     int r = build_subs(c, sort);
     if (r) return r;
