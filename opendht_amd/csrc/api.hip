@@ -99,7 +99,8 @@ struct dhtgpu_ctx {
         DevBuf ws;              // workspace; its zero-between-calls head (bitmap, counters) stays clean
         DevBuf out_idx, out_cnt;   // record mode: local results before the record conversion
         DevBuf sws;             // small-batch path workspace (zero between calls once cleaned)
-        size_t zeroed = 0;      // leading workspace bytes known zero (the last call's clean head)
+        size_t zeroed = 0;      // leading workspace bytes known zero (the last call's clean head) ...
+        size_t ctr_off = 0;     // ... but for the statistics words at this offset (batch_ctr_offset)
         uint64_t desc_sig = 0;  // sub-partition descriptors held by the workspace (launch_batch_topk)
         bool sclean = false;
         uint32_t spar = 0;      // small-batch path: the counter set its next call uses
@@ -682,6 +683,7 @@ static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hi
     const uint32_t pf = (bc.cells ? kPlanCells : 0u) | (bc.sorted ? kPlanSorted : 0u);
     const size_t need = batch_bytes(n_plan, bc.q, bc.q_plan, bc.k, c->num_cus, nsub, pf);
     const size_t head = batch_clean_bytes(n_plan, bc.q_plan, bc.k, c->num_cus, nsub, pf);
+    const size_t ctr_off = batch_ctr_offset(n_plan, bc.q_plan, bc.k, c->num_cus, nsub, pf);
     if (need > b.ws.cap) {   // reallocated: nothing of it is known
         b.zeroed = 0;
         b.desc_sig = 0;
@@ -689,7 +691,11 @@ static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hi
     DHT_TRY(b.ws.ensure(need));
     bc.fb_hint = c->fb_hint;
     bc.fb_hint_dev = c->fb_hint_dev;
-    if (b.zeroed < head) DHT_TRY(hipMemsetAsync(b.ws.p, 0, head, s));
+    // the head is zero after a call but for the statistics words ctr[0..3] (F1 resets them at the
+    // start of the next call): a head laid out with its counters elsewhere (another bitmap size --
+    // a sub-partitioned call, then a one-set call) would meet them inside another array (a partition
+    // count: stale survivors gathered by F3), so it is zeroed again
+    if (b.zeroed < head || (b.zeroed && b.ctr_off != ctr_off)) DHT_TRY(hipMemsetAsync(b.ws.p, 0, head, s));
     b.zeroed = 0;   // re-established below once every launch went through
     if (bc.dbg & 256u) {   // phase stamps (zeroed when allocated)
         const bool fresh = !c->stamps.p;
@@ -701,7 +707,8 @@ static int batch_slot_run(dhtgpu_ctx* c, int si, BatchCall bc, hipStream_t s, hi
     bc.desc_sig = &b.desc_sig;
     DHT_TRY(launch_batch_topk(bc, s));
     b.last = s;
-    b.zeroed = head;   // the call leaves its clean head zero
+    b.zeroed = head;   // the call leaves its clean head zero (but for ctr[0..3])
+    b.ctr_off = ctr_off;
     c->blast = si;
     c->last_n = n_plan;
     c->last_qp = bc.q_plan;

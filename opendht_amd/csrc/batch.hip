@@ -2370,6 +2370,10 @@ bool batch_supported(uint64_t n, uint32_t q, uint32_t k, int num_cus, uint32_t n
     return f3_lds(P, P.f3cap_wide) <= kLdsMax && f2_lds(P) <= kLdsMax;
 }
 
+size_t batch_ctr_offset(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub, uint32_t pf) {
+    return ws_layout(plan_batch(n, q_plan, k, num_cus, pf), nsub, 0, k).ctr;
+}
+
 size_t batch_clean_bytes(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub, uint32_t pf) {
     return ws_layout(plan_batch(n, q_plan, k, num_cus, pf), nsub, 0, k).clean;
 }

@@ -123,6 +123,9 @@ bool batch_supported(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint3
 size_t batch_bytes(uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1, uint32_t pf = 0);
 // leading workspace bytes that must be zero before a call (the call leaves them zero)
 size_t batch_clean_bytes(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1, uint32_t pf = 0);
+// offset of the shared counters in the workspace head: their words 0..3 (the call's statistics, read by
+// batch_read_stats) stay set after a call, so a head laid out with them elsewhere is zeroed again
+size_t batch_ctr_offset(uint64_t n, uint32_t q_plan, uint32_t k, int num_cus, uint32_t nsub = 1, uint32_t pf = 0);
 // stats4 = {fallback targets, survivors, wave-path targets, 0} of the last call on workspace ws
 // (synchronises s)
 hipError_t batch_read_stats(const void* ws, uint64_t n, uint32_t q, uint32_t q_plan, uint32_t k, int num_cus,
