@@ -238,7 +238,17 @@ def pmc_traffic(workload, kernel):
     except (OSError, ValueError):
         return None
     w = d.get("workloads", {}).get(workload)
-    return None if w is None else w.get(kernel, {}).get("traffic_bytes")
+    if w is None:
+        return None
+    # a K6 phase's kernels: F1 is k_f1_targets or (batches >= 2^18) k_f1_coarse + k_f1_fine; F2 is
+    # k_f2_filter or (prefix-sorted sub-partitions) k_f2_direct
+    parts = K6_PHASE_KERNELS.get(kernel, (kernel,))
+    got = [w[kn]["traffic_bytes"] for kn in parts if kn in w]
+    return sum(got) if got else None
+
+
+K6_PHASE_KERNELS = {"k_f1_targets": ("k_f1_targets", "k_f1_coarse", "k_f1_fine"),
+                    "k_f2_filter": ("k_f2_filter", "k_f2_direct")}
 
 
 def cpu_model():
@@ -1032,7 +1042,8 @@ def cfg3_rank_leg(a, L, dev, stream, tstream, route):
         tstep = None
         try:
             d = json.load(open(os.path.join(ROOT, PMC_FILE))).get("workloads", {}).get(key, {})
-            step_k = ("k_f1_targets", "k_f2_filter", "k_f3_answer", "k_f4", "k_merge3")   # the step's kernels only
+            step_k = ("k_f1_targets", "k_f1_coarse", "k_f1_fine", "k_f2_filter", "k_f2_direct", "k_f3_answer", "k_f4",
+                      "k_merge3")   # the step's kernels only
             tstep = sum(d[kn]["traffic_bytes"] for kn in step_k if kn in d) or None
         except (OSError, ValueError):
             pass
@@ -1055,7 +1066,10 @@ def cfg3_rank_leg(a, L, dev, stream, tstream, route):
                             "step_traffic_bytes": tstep,
                             "served_from": f"HBM: the w0 planes ({4 * n / 1e6:.0f} MB) exceed the 256 MiB L3",
                             "how": "frac: F2's algorithmic bytes / its mean event time; step_frac: every kernel's "
-                                   "algorithmic bytes / the 2-in-flight step time; peak 8 TB/s"}}
+                                   "algorithmic bytes / the 2-in-flight step time; peak 8 TB/s",
+                            "kernels": "phases as dispatched: F1 = k_f1_targets, or k_f1_coarse + k_f1_fine at >= 2^18 "
+                                       "targets; F2 = k_f2_filter, or k_f2_direct over prefix-sorted sub-partitions; "
+                                       "PMC traffic summed over a phase's kernels"}}
         if not a.no_cpu:
             O = oracle()
             rows = np.linspace(0, q - 1, 32).astype(np.int64)

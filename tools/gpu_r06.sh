@@ -44,7 +44,8 @@ for k in ("kt_bench20", "kt_cfg3prefix", "kt_cfg3broadcast"):
     f = glob.glob(f"{o}/{k}/**/*kernel_stats.csv", recursive=True)[0]
     for row in csv.DictReader(open(f)):
         if "dhtgpu" in row["Name"]:
-            print(k, row["Name"].split("(")[0].replace("dhtgpu::(anonymous namespace)::", "")[:40], row["Calls"], round(float(row["AverageNs"]) / 1e3, 2), "us")
+            nm = row["Name"].replace("void ", "").replace("(anonymous namespace)::", "").replace("dhtgpu::", "")
+            print(k, nm.split("(")[0][:40], row["Calls"], round(float(row["AverageNs"]) / 1e3, 2), "us")
 PY
 echo all-ok
 exit 0
