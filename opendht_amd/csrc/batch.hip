@@ -235,7 +235,9 @@ constexpr uint32_t kF1aThreads = 1024, kF1aPer = 4, kF1aTargets = kF1aThreads * 
 constexpr uint32_t kF1bThreads = 1024, kF1bPer = 4;
 constexpr uint32_t kMaxCoarse = 4096;             // bins (the coarse counters live in the clean head)
 constexpr uint32_t kF1bLdsWords = 16384;          // F1b's bitmap words + partition counts (64 KB)
-constexpr uint32_t kF1CoarseMinQ = 1u << 18;      // smaller batches: k_f1_targets (at 2^17: 14.2 vs 13.5 us)
+constexpr uint32_t kF1CoarseMinQ = 1u << 17;      // smaller batches: k_f1_targets (at 2^17 F1 is as fast either
+                                                  // way, 13.1-13.4 us, and the two-pass form leaves the other call
+                                                  // in flight the atomics: prefix rank 0.130-0.135 -> 0.127-0.128 ms)
 
 struct F1cArgs {
     const uint32_t* tw0; const uint32_t* tw1;

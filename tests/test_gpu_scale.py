@@ -244,9 +244,9 @@ def test_subpartition_sibling_marking(ctx, q):
     assert np.array_equal(got[rows], want) and np.array_equal(cnt[rows], wcnt)
 
 
-@pytest.mark.parametrize("n,q", [(1 << 22, 1 << 18), (1 << 25, 1 << 18)])
+@pytest.mark.parametrize("n,q", [(1 << 22, 1 << 17), (1 << 25, 1 << 18)])
 def test_f1_two_pass_clustered_targets(ctx, n, q):
-    """F1's two-pass form (batches of >= 2^18 targets, round 6: coarse bins by workgroup-level
+    """F1's two-pass form (batches of >= 2^17 targets, round 6: coarse bins by workgroup-level
     reservations, then one workgroup per bin marking the bitmap and ranking the partitions in LDS):
     a quarter of the targets share their top 12 bits (their coarse bin overflows: those targets
     spill to the fallback scan from the first pass), and groups of 96, 256, 700 and 2,048 targets
