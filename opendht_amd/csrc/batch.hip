@@ -1458,7 +1458,10 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                     } else if (gj == 0) {
                         slow[atomicAdd(slow + kF3Threads, 1u)] = slot;
                     }
-                } else if (gj == 0) {
+                } else if (gj == 0 || (K == 8 && a.rec.out && full_row && G > 1 && ((uintptr_t)a.rec.out & 15) == 0)) {
+                    // (record form, k = 8, whole 16-B aligned rows: the group's G lanes all gather
+                    // the row -- their loads hit the same addresses -- and store its six 16-B
+                    // chunks together, below)
                     uint32_t* orow = a.out_idx + (uint64_t)qi * a.k;
                     // LDS reads first, then (shards) all gidx loads together: one wait before
                     // the stores instead of one per place
@@ -1496,9 +1499,30 @@ __global__ __launch_bounds__(kF3Threads) void k_f3_answer(F3Args a) {
                                 wds[3 * r + 1] = w1[r];
                                 wds[3 * r + 2] = gi[r];
                             }
+                            if (K == 8 && G > 1) {
+                                // lane gj of the group stores chunks gj, gj + G, ..: one store
+                                // instruction covers G adjacent chunks of the row (one or two
+                                // lines) instead of one lane issuing all six
+                                // (straight-line: chunk gj in [0, 4), gj + G in [2, 8), gj + 2G in [4, 6) for G = 2)
+                                auto put = [&](uint32_t c, uint32_t c_lo, uint32_t c_hi) {
+                                    uint32_t x[4];
 #pragma unroll
-                            for (int r = 0; r < 3 * K; r += 4)
-                                *reinterpret_cast<uint4*>(ro + r) = make_uint4(wds[r], wds[r + 1], wds[r + 2], wds[r + 3]);
+                                    for (int i = 0; i < 4; ++i) {
+                                        x[i] = 0u;
+#pragma unroll
+                                        for (uint32_t cc = 0; cc < 6; ++cc)
+                                            if (cc >= c_lo && cc < c_hi) x[i] = c == cc ? wds[(4 * cc + i) % (3 * K)] : x[i];
+                                    }
+                                    *reinterpret_cast<uint4*>(ro + 4 * c) = make_uint4(x[0], x[1], x[2], x[3]);
+                                };
+                                put(gj, 0u, 4u);
+                                if (gj + G < 6) put(gj + G, 2u, 6u);
+                                if (gj + 2 * G < 6) put(gj + 2 * G, 4u, 6u);
+                            } else {
+#pragma unroll
+                                for (int r = 0; r < 3 * K; r += 4)
+                                    *reinterpret_cast<uint4*>(ro + r) = make_uint4(wds[r], wds[r + 1], wds[r + 2], wds[r + 3]);
+                            }
                         } else {
 #pragma unroll
                             for (int r = 0; r < K; ++r) {
