@@ -237,6 +237,26 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge3(const uint32_t* __rest
         a = none ? DHT_NONE : my[3 * p] ^ t0;
         b = none ? DHT_NONE : my[3 * p + 1] ^ t1;
     };
+    if (G == 1 && k == 8 && ((uintptr_t)out_idx & 15) == 0) {
+        // one list (G = 1): the list is the answer, in order up to its first empty slot -- the row
+        // as two 16-B stores (the merge loop's eight dword stores per lane strode 32 B across the
+        // wave: 30 us for 2^20 rows at the cfg-3 broadcast rank)
+        if (!tv) return;
+        uint32_t row[8], cnt = 0;
+        bool stop = false;
+#pragma unroll
+        for (uint32_t r = 0; r < 8; ++r) {
+            const uint32_t ix = r < kin && lv ? my[3 * r + 2] : DHT_NONE;
+            stop = stop || ix == DHT_NONE;
+            row[r] = stop ? DHT_NONE : ix;
+            cnt += stop ? 0u : 1u;
+        }
+        uint4* o = reinterpret_cast<uint4*>(out_idx + (uint64_t)qi * 8);
+        o[0] = make_uint4(row[0], row[1], row[2], row[3]);
+        o[1] = make_uint4(row[4], row[5], row[6], row[7]);
+        out_cnt[qi] = cnt;
+        return;
+    }
     const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (g * G);
     uint32_t p = 0, cnt = 0;
     uint32_t h0, h1, hi;
