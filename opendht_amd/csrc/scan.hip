@@ -262,6 +262,39 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge3(const uint32_t* __rest
     uint32_t h0, h1, hi;
     head(0, h0, h1, hi);
     bool row_tie = false;
+    if (k == 8 && ((uintptr_t)out_idx & 15) == 0) {
+        // k = 8: the row kept in registers and stored as two 16-B stores by the group's lane 0
+        // (the loop below stores one dword per place: a 32-B stride across the wave)
+        uint32_t row[8];
+#pragma unroll
+        for (uint32_t r = 0; r < 8; ++r) {
+            uint32_t m0 = h0, m1 = h1, mi = hi;
+            bool tie = false;
+#pragma unroll
+            for (uint32_t o = 1; o < G; o <<= 1) {
+                const uint32_t p0 = (uint32_t)__shfl_xor((int)m0, (int)o), p1 = (uint32_t)__shfl_xor((int)m1, (int)o);
+                const uint32_t pi = (uint32_t)__shfl_xor((int)mi, (int)o);
+                tie = tie || (p0 == m0 && p1 == m1 && pi != DHT_NONE && mi != DHT_NONE);
+                const bool less = p0 < m0 || (p0 == m0 && (p1 < m1 || (p1 == m1 && pi < mi)));
+                if (less) { m0 = p0; m1 = p1; mi = pi; }
+            }
+            row_tie = row_tie || (__ballot(tie) & gmask) != 0;
+            row[r] = mi;   // DHT_NONE once the target's lists are exhausted (then every later place)
+            cnt += mi != DHT_NONE ? 1u : 0u;
+            if (mi != DHT_NONE && lv && h0 == m0 && h1 == m1 && hi == mi) head(++p, h0, h1, hi);
+        }
+        if (tv && j == 0) {
+            uint4* o = reinterpret_cast<uint4*>(out_idx + (uint64_t)qi * 8);
+            o[0] = make_uint4(row[0], row[1], row[2], row[3]);
+            o[1] = make_uint4(row[4], row[5], row[6], row[7]);
+            out_cnt[qi] = cnt;
+            if (row_tie && ties) {
+                const uint32_t s = atomicAdd(ties, 1u);
+                if (s < tie_cap) ties[1 + s] = qi;
+            }
+        }
+        return;
+    }
     for (uint32_t r = 0; r < k; ++r) {   // wave-uniform
         uint32_t m0 = h0, m1 = h1, mi = hi;
         bool tie = false;
